@@ -1,0 +1,177 @@
+#!/usr/bin/env python3
+"""bench.py -- RaptorQ encode+decode throughput on MI355X (BASELINE.json metric).
+
+Metric: "RaptorQ encode+decode GB/s device-resident, K=1024 T=1200B, 1/2/4/8 MI355X".
+Workload (BASELINE.json configs[2], the largest single-GPU case of the scaling config[3]):
+one step = encode every block of the batch (K=1024, T=1200, N=1100 -> 76 repair symbols per
+block) and then decode every block after erasing exactly 5% of its N symbols (55, a seeded
+uniform subset).  value = source bytes (n_blocks * K * T, all ranks) / (encode + decode time).
+Inputs are resident in HBM when the timed region starts; descriptor arrays for the erasure
+pattern are prepared once (host) and uploaded inside every decode call.
+
+Multi-GPU: one process per GPU (torch.distributed); each rank owns n_blocks independent
+blocks (weak scaling, no collective on the data path -- blocks are independent, SURVEY.md
+sec. 8e).  The only collectives are the timing barrier and the max-over-ranks reduction.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "rl-quic-raptor_amd"))
+sys.path.insert(0, str(ROOT))
+import rqhip  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--blocks", type=int, default=1024, help="blocks per GPU")
+    ap.add_argument("--K", type=int, default=1024)
+    ap.add_argument("--T", type=int, default=1200)
+    ap.add_argument("--N", type=int, default=1100)
+    ap.add_argument("--erase", type=float, default=0.05)
+    ap.add_argument("--cpu-sample", type=int, default=2, help="blocks in the CPU baseline sample (0 = skip)")
+    ap.add_argument("--no-verify", action="store_true")
+    return ap.parse_args()
+
+
+def erasure_pattern(K, N, n_blocks, n_erase, seed):
+    rng = np.random.default_rng(seed)
+    er, rep = [], []
+    for _ in range(n_blocks):
+        lost = set(rng.choice(N, n_erase, replace=False).tolist())
+        er.append(sorted(i for i in lost if i < K))
+        rep.append([e for e in range(K, N) if e not in lost])
+    return er, rep
+
+
+def cpu_baseline(K, T, N, n_erase, n_blocks):
+    """Oracle (C restatement, 1 thread) on a bounded sample of the same workload."""
+    from oracle import oracle as O
+    rng = np.random.default_rng(4242)
+    t_enc = t_dec = 0.0
+    for b in range(n_blocks):
+        data = rng.integers(0, 256, K * T, dtype=np.uint8).tobytes()
+        t0 = time.perf_counter()
+        enc = O.OracleEncoder(data, T)
+        t_enc += time.perf_counter() - t0
+        syms = {i: enc.gen_symbol(i).tobytes() for i in range(N)}
+        lost = set(rng.choice(N, n_erase, replace=False).tolist())
+        dec = O.OracleDecoder(len(data), T)
+        for i in range(N):
+            if i not in lost:
+                dec.add_symbol(i, syms[i])
+        t0 = time.perf_counter()
+        ok, out = dec.decode()
+        t_dec += time.perf_counter() - t0
+        assert ok and out == data
+    gbs = n_blocks * K * T / (t_enc + t_dec) / 1e9
+    return {"value": round(gbs, 6), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": "%d blocks K=%d T=%d N=%d, %d erased, oracle/rq_oracle.c dense-Gauss restatement, "
+                      "encode %.2fs + decode %.2fs" % (n_blocks, K, T, N, n_erase, t_enc, t_dec)}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+        tdist.init_process_group("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    rqhip.lib().rq_set_device(local)
+    K, T, N, B = args.K, args.T, args.N, args.blocks
+    R = N - K
+    n_erase = int(round(args.erase * N))
+    esis = list(range(K, N))
+    g = torch.Generator(device=dev).manual_seed(1337 + rank)
+    src = torch.randint(0, 256, (B, K * T), dtype=torch.uint8, device=dev, generator=g)
+    rep = torch.empty((B, R * T), dtype=torch.uint8, device=dev)
+    er, rl = erasure_pattern(K, N, B, n_erase, 7 + rank)
+    # received repair rows, gathered once (decode input), and the decoder's working buffer
+    rb = torch.tensor([b for b in range(B) for _ in rl[b]], device=dev, dtype=torch.long)
+    rr = torch.tensor([e - K for b in range(B) for e in rl[b]], device=dev, dtype=torch.long)
+    data = src.clone()
+    db = rqhip.DecodeBatch(K, T, er, rl)
+    stream = torch.cuda.current_stream(dev)
+
+    # correctness of one full step before timing
+    rqhip.encode_batch(src, K, T, esis, rep, stream=stream)
+    recv = rep.view(B, R, T)[rb, rr].contiguous()
+    for b in range(B):
+        for i in er[b]:
+            data[b, i * T:(i + 1) * T] = 0
+    st = db.run(data, recv, stream=stream)
+    torch.cuda.synchronize()
+    ok_frac = float((st == 1).mean())
+    if not args.no_verify:
+        good = torch.tensor(st == 1, device=dev)
+        assert torch.equal(data[good], src[good]), "decode mismatch"
+
+    for _ in range(args.warmup):
+        rqhip.encode_batch(src, K, T, esis, rep, stream=stream)
+        db.run(data, recv, stream=stream)
+    torch.cuda.synchronize()
+
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    ev_e0 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ev_e1 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        ev_e0[s].record(stream)
+        rqhip.encode_batch(src, K, T, esis, rep, stream=stream)
+        ev_e1[s].record(stream)
+        db.run(data, recv, stream=stream)
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    enc_ms = float(np.mean([ev_e0[s].elapsed_time(ev_e1[s]) for s in range(args.steps)]))
+    if dist:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        dt = float(t.item())
+    src_bytes = B * K * T * world
+    value = src_bytes * args.steps / dt / 1e9
+    if rank == 0:
+        achieved = B * K * T / (enc_ms * 1e-3) / 1e9
+        line = {
+            "metric": "RaptorQ encode+decode GB/s device-resident, K=1024 T=1200B, 1/2/4/8 MI355X",
+            "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (torch.randint payload, seeded exact-count 5% erasures)",
+            "config": {"workload": "encode+decode K=%d T=%d N=%d erase=%d/%d symbols" % (K, T, N, n_erase, N),
+                       "blocks_per_gpu": B, "bytes_per_gpu": B * K * T, "parallelism": "block-sharded x%d" % world,
+                       "decode_ok_fraction": ok_frac},
+            "roofline": {"bound": "hbm", "kernel": "k_encode (encode batch)", "achieved": round(achieved, 2),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                         "traffic": None, "encode_ms_per_launch": round(enc_ms, 4),
+                         "algorithmic_bytes_per_launch": B * K * T},
+        }
+        if args.cpu_sample > 0 and world == 1:
+            line["cpu_baseline"] = cpu_baseline(K, T, N, n_erase, args.cpu_sample)
+        print(json.dumps(line), flush=True)
+    if dist:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,121 @@
+/*
+ * rqhip.h -- C-ABI of the MI355X-native RaptorQ engine (librqhip.so).
+ *
+ * Drop-in boundary for the reference's go/fec RaptorQ path (go/fec/raptorq_wrap.go:13-124),
+ * which wraps github.com/xssnick/raptorq v1.1.0.  Plain pointers and sizes only: no HIP or
+ * torch types, so a cgo shim needs no ROCm headers (see INTEGRATION.md for the Go binding).
+ * Device pointers appear only in the batch API and are documented as such; streams are passed
+ * as opaque `void*` (a hipStream_t, or NULL for the null stream).
+ *
+ * Error model: functions return 0 (RQ_OK) or a negative RQ_ERR_* code; rq_strerror() gives the
+ * reference's message text where one exists; rq_last_error() gives the detail of the calling
+ * thread's last failure.  No exceptions cross the ABI.  Handles are independent: distinct
+ * handles may be used concurrently from different threads (the reference Decoder is not
+ * thread-safe per handle, and neither is this one).
+ */
+#ifndef RQHIP_H
+#define RQHIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RQ_OK 0
+#define RQ_ERR_SYMBOL_SIZE_ZERO (-1) /* "symbol size cannot be zero"      RQ/params.go:31-61   */
+#define RQ_ERR_K_TOO_BIG (-2)        /* "k is too big"                    RQ/raw-params.go:14  */
+#define RQ_ERR_NOT_ENOUGH (-3)       /* "not enough symbols to decode"    RQ/decoder.go:65-66  */
+#define RQ_ERR_SYMBOL_SIZE (-4)      /* "incorrect symbol size %d, should be %d" RQ/decoder.go:39-57 */
+#define RQ_ERR_BAD_ARG (-5)          /* wrapper argument errors ("bad K or L", "bad N/K/L", ...) */
+#define RQ_ERR_DEVICE (-6)           /* HIP runtime failure or no usable gfx950 device            */
+#define RQ_ERR_UNSUPPORTED (-7)      /* shape outside the device path's limits    */
+#define RQ_ERR_PLAN (-8)             /* schedule compiler failure (singular system; never expected) */
+
+const char* rq_strerror(int code);
+const char* rq_last_error(void);
+
+/* ---------------- parameters (xssnick calcParams, RQ/params.go:31-61) ---------------- */
+/* out[11] = {K, K', J, S, H, W, L, P, P1, U, B} for a payload of `size` bytes, symbol size T.
+ * P1 is the smallest prime strictly greater than P (the library's deviation from RFC 6330). */
+int rq_params(uint64_t size, uint32_t T, uint32_t out[11]);
+
+/* ---------------- encoder: replaces rqq.NewRaptorQ(L).CreateEncoder(data) -----------------
+ * go/fec/raptorq_wrap.go:29-40 (NewRaptorQEncoder), :44-46 (GenSymbol), :49 (BaseSymbolsNum);
+ * library RQ/encoder.go:15-41.  The payload is copied; symbols are computed on the GPU. */
+typedef struct rq_enc rq_enc;
+rq_enc* rq_encoder_create(const uint8_t* data, size_t len, uint32_t T, int* err);
+uint32_t rq_encoder_k(const rq_enc* e);           /* BaseSymbolsNum: library K = ceil(len/T) */
+uint32_t rq_encoder_symbol_size(const rq_enc* e);
+/* GenSymbol(esi): T bytes into out.  esi < K -> padded source symbol, else repair symbol. */
+int rq_encoder_symbol(rq_enc* e, uint32_t esi, uint8_t* out);
+/* count consecutive symbols first_esi.. into out (count*T bytes); one GPU launch for repairs. */
+int rq_encoder_symbols(rq_enc* e, uint32_t first_esi, uint32_t count, uint8_t* out);
+void rq_encoder_free(rq_enc* e);
+
+/* ---------------- decoder: replaces rqq.NewRaptorQ(L).CreateDecoder(size) -----------------
+ * go/fec/raptorq_wrap.go:52-74; library RQ/decoder.go:23-134. */
+typedef struct rq_dec rq_dec;
+rq_dec* rq_decoder_create(uint64_t data_size, uint32_t T, int* err);
+uint32_t rq_decoder_k(const rq_dec* d);           /* FastSymbolsNumRequired (RQ/decoder.go:61) */
+/* AddSymbol: *can_try = (K <= unique symbols held), the library's bool (RQ/decoder.go:47,57). */
+int rq_decoder_add(rq_dec* d, uint32_t esi, const uint8_t* sym, size_t len, int* can_try);
+/* Decode: *ok = 1 and data_size bytes in out; *ok = 0 if the system is rank-deficient
+ * (library returns (false, nil, nil)); RQ_ERR_NOT_ENOUGH if fewer than K unique symbols. */
+int rq_decoder_decode(rq_dec* d, uint8_t* out, int* ok);
+void rq_decoder_free(rq_dec* d);
+
+/* ---------------- batched, device-resident API (the hot path) ---------------------------
+ * All blocks of one call share T and K (hence K').  Pointers marked (device) are HIP device
+ * memory on the current device; (host) are host memory.  Work is enqueued on `stream`;
+ * rq_encode_batch returns without synchronising, rq_decode_batch synchronises once to report
+ * per-block status. */
+typedef struct {
+    uint32_t T;              /* symbol size in bytes, multiple of 4                            */
+    uint32_t K;              /* source symbols per block (library K)                           */
+    uint32_t n_blocks;
+    const void* src;         /* (device) block b symbol i at src + b*src_stride + i*T          */
+    uint64_t src_stride;     /* bytes between blocks (>= K*T)                                  */
+    uint32_t n_esi;          /* repair symbols to generate per block                           */
+    const uint32_t* esi;     /* (host) n_esi ESIs (>= K), the same for every block             */
+    void* out;               /* (device) repair r of block b at out + b*out_stride + r*T       */
+    uint64_t out_stride;     /* bytes between blocks (>= n_esi*T)                              */
+    void* c_out;             /* optional (device): intermediate symbols, L rows per block      */
+    uint64_t c_stride;
+    void* stream;            /* hipStream_t or NULL                                            */
+} rq_encode_desc;
+int rq_encode_batch(const rq_encode_desc* d);
+
+typedef struct {
+    uint32_t T, K, n_blocks;
+    void* data;                  /* (device) block b source row i at data + b*data_stride + i*T;
+                                    received rows present, erased rows are overwritten on success */
+    uint64_t data_stride;
+    const uint32_t* n_erased;    /* (host) [n_blocks] erased source symbols per block          */
+    const uint32_t* erased;      /* (host) concatenated erased source ESIs (< K), unique        */
+    const uint32_t* n_repair;    /* (host) [n_blocks] received repair symbols per block        */
+    const uint32_t* repair_esi;  /* (host) concatenated repair ESIs (>= K), unique per block   */
+    const void* repair;          /* (device) repair rows (T bytes each) in repair_esi order     */
+    int32_t* status;             /* (host out) [n_blocks]: 1 decoded, 0 rank-deficient,
+                                    RQ_ERR_NOT_ENOUGH if received < K, RQ_ERR_UNSUPPORTED       */
+    void* stream;
+} rq_decode_desc;
+int rq_decode_batch(const rq_decode_desc* d);
+
+/* ---------------- device / plan control ---------------- */
+int rq_device_count(void);
+int rq_set_device(int device);      /* selects the HIP device for subsequent calls on this thread */
+/* Compile (and cache) the encode schedule for the K' row of K; returns its statistics:
+ * stats[0..10] = {n_stmts, n_levels, n_src_xor, n_src_mul, n_global, u, inactivated,
+ *                 n_pivots, n_slots, passB_inplace, passB_rebuild}.  Host only. */
+int rq_plan_stats(uint32_t K, uint32_t stats[11]);
+/* Export the compiled program for host-side verification (tests): sizes first with NULL
+ * buffers.  sizes[0..4] = {n_levels+1, n_stmts+1, n_words, K', L}. */
+int rq_plan_export(uint32_t K, uint32_t sizes[5], uint32_t* level_start, uint32_t* stmt_off,
+                   uint32_t* words, uint16_t* load_slot, uint16_t* col_slot);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RQHIP_H */

@@ -1,0 +1,399 @@
+// rq_kernels.hip -- HIP kernels for gfx950 (CDNA4): RaptorQ encode-schedule replay, LT repair
+// generation, and syndrome decode (solve + apply).  No MFMA: GF(2)/GF(256) byte arithmetic.
+//
+// Reference hot routines replaced (native inventory):
+//   asmSSE2XORBlocks  RQ/discmath/optimizations.s:9-28   -> dword XOR of LDS-resident strip rows
+//   asmSSSE3MulAdd    RQ/discmath/optimizations.s:36-78  -> gfmul4 (packed 4-byte GF(256) mul)
+//   Solve             RQ/solver.go:25-185                -> k_encode replaying the per-K' plan
+//   encodeGen         RQ/params.go:162-182               -> k_encode output stage / k_gather
+//   Decoder.Decode    RQ/decoder.go:64-134               -> k_encode (syndromes) + k_solve + k_apply
+//
+// Data layout: a source block is K rows of T bytes (row-major, as the wire carries symbols).
+// One workgroup owns one (block, column strip); the strip of every intermediate-symbol slot
+// (n_slots x sd dwords) lives in LDS for the whole program, so HBM is touched only to read the
+// source strip once (plus L2-resident re-reads of rows named by SRC_GLOBAL terms) and to write
+// the requested output rows.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "rfc6330_tables.h"
+#include "rq_device.hpp"
+
+namespace rq {
+
+// must match rq_plan.hpp
+constexpr uint32_t ST_XOR_ = 0, ST_MUL_ = 1, ST_SCALE_ = 3, ST_HORNER_ = 4;
+constexpr uint32_t SLOT_NONE_ = 0xFFFFu;
+
+__constant__ uint32_t c_V[4][256];
+__constant__ uint32_t c_DEG[31];
+
+int upload_tables() {
+    uint32_t v[4][256];
+    for (int i = 0; i < 256; ++i) {
+        v[0][i] = RQ_V0[i]; v[1][i] = RQ_V1[i]; v[2][i] = RQ_V2[i]; v[3][i] = RQ_V3[i];
+    }
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_V), v, sizeof v);
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(c_DEG), RQ_DEGREE_F, sizeof(uint32_t) * 31);
+    return (int)e;
+}
+
+// ------------------------------ GF(256) on packed dwords ------------------------------------
+__device__ __forceinline__ uint32_t xtime4(uint32_t x) {
+    const uint32_t hi = (x >> 7) & 0x01010101u;
+    return ((x & 0x7F7F7F7Fu) << 1) ^ (hi * 0x1Du);
+}
+// x * c in GF(256) for each of the 4 bytes of x (poly 0x11D).
+__device__ __forceinline__ uint32_t gfmul4(uint32_t x, uint32_t c) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        r ^= (c & (1u << b)) ? x : 0u;
+        x = xtime4(x);
+    }
+    return r;
+}
+__device__ __forceinline__ uint32_t alpha_pow(uint32_t h) {  // alpha^h, h < 16
+    constexpr uint32_t tab[16] = {1, 2, 4, 8, 16, 32, 64, 128, 29, 58, 116, 232, 205, 135, 19, 38};
+    return tab[h & 15];
+}
+
+// ------------------------------ LT tuple on device (RQ/params.go:83-112) -------------------
+__device__ __forceinline__ uint32_t d_rand(uint32_t y, uint32_t i, uint32_t m) {
+    return (c_V[0][(y + i) & 255u] ^ c_V[1][((y >> 8) + i) & 255u] ^ c_V[2][((y >> 16) + i) & 255u] ^
+            c_V[3][((y >> 24) + i) & 255u]) % m;
+}
+struct LtIter {
+    uint32_t d, a, b, d1, a1, b1;
+};
+__device__ __forceinline__ LtIter d_tuple(const DevParams& p, uint32_t X) {
+    uint32_t A = 53591u + 997u * p.J;
+    if ((A & 1u) == 0) ++A;
+    const uint32_t y = 10267u * (p.J + 1u) + X * A;
+    const uint32_t v = d_rand(y, 0, 1u << 20);
+    uint32_t d = 30;
+    for (uint32_t i = 0; i < 31; ++i)
+        if (v < c_DEG[i]) { d = i; break; }
+    if (d > p.W - 2) d = p.W - 2;
+    LtIter t;
+    t.d = d;
+    t.a = 1 + d_rand(y, 1, p.W - 1);
+    t.b = d_rand(y, 2, p.W);
+    t.d1 = d < 4 ? 2 + d_rand(X, 3, 2) : 2;
+    t.a1 = 1 + d_rand(X, 4, p.P1 - 1);
+    t.b1 = d_rand(X, 5, p.P1);
+    return t;
+}
+// Calls f(col) for every column XORed into the symbol of ISI X (encodeGen order).
+template <class F>
+__device__ __forceinline__ void d_for_cols(const DevParams& p, uint32_t X, F&& f) {
+    LtIter t = d_tuple(p, X);
+    uint32_t b = t.b;
+    f(b);
+    for (uint32_t j = 1; j < t.d; ++j) { b = (b + t.a) % p.W; f(b); }
+    uint32_t b1 = t.b1;
+    while (b1 >= p.P) b1 = (b1 + t.a1) % p.P1;
+    f(p.W + b1);
+    for (uint32_t j = 1; j < t.d1; ++j) {
+        b1 = (b1 + t.a1) % p.P1;
+        while (b1 >= p.P) b1 = (b1 + t.a1) % p.P1;
+        f(p.W + b1);
+    }
+}
+
+// ------------------------------ encode: plan replay ------------------------------------------
+// grid = (n_strips, n_blocks), block = 256 threads = 256/GS lane groups; LDS = n_slots*sd dwords
+// (+ erasure bitmap).  Each level's statements are independent; lane group g executes
+// statements g, g+ngrp, ... of the level, one dword of the strip per lane.
+template <int GS>
+__global__ void __launch_bounds__(256) k_encode(EncArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const uint32_t sd = a.sd, T = a.T, Td = T >> 2;
+    const uint32_t strip = blockIdx.x;
+    const uint32_t b = a.blk_map ? a.blk_map[blockIdx.y] : blockIdx.y;
+    const uint32_t c0 = strip * sd;
+    const uint32_t width = min(sd, Td - c0);
+    const uint32_t tid = threadIdx.x, nthr = blockDim.x;
+    const uint32_t K = a.p.K;
+    const uint32_t nebw = a.erased_off ? (K + 31) / 32 : 0;
+    uint32_t* ebits = lds + a.n_slots * sd;
+
+    for (uint32_t i = tid; i < a.n_slots * sd + nebw; i += nthr) lds[i] = 0;
+    __syncthreads();
+    if (nebw) {
+        for (uint32_t i = a.erased_off[b] + tid; i < a.erased_off[b + 1]; i += nthr) {
+            const uint32_t e = a.erased[i];
+            if (e < K) atomicOr(&ebits[e >> 5], 1u << (e & 31));
+        }
+        __syncthreads();
+    }
+    const uint8_t* blk = a.src + (size_t)b * a.src_stride;
+    for (uint32_t i = tid; i < K * sd; i += nthr) {
+        const uint32_t row = i / sd, c = i - row * sd;
+        const bool er = nebw && ((ebits[row >> 5] >> (row & 31)) & 1u);
+        if (c < width && !er)
+            lds[(uint32_t)a.load_slot[row] * sd + c] =
+                *reinterpret_cast<const uint32_t*>(blk + (size_t)row * T + (size_t)(c0 + c) * 4);
+    }
+    __syncthreads();
+
+    const uint32_t grp = tid / GS, lane = tid % GS, ngrp = nthr / GS;
+    const bool live = lane < sd;
+    const bool inb = lane < width;
+    const uint8_t* gcol = blk + (size_t)(c0 + lane) * 4;
+    auto gload = [&](uint32_t isi) -> uint32_t {
+        if (!inb || isi >= K) return 0u;
+        if (nebw && ((ebits[isi >> 5] >> (isi & 31)) & 1u)) return 0u;
+        return *reinterpret_cast<const uint32_t*>(gcol + (size_t)isi * T);
+    };
+
+    for (uint32_t lv = 0; lv < a.n_levels; ++lv) {
+        const uint32_t s1 = a.level_start[lv + 1];
+        for (uint32_t s = a.level_start[lv] + grp; s < s1; s += ngrp) {
+            if (!live) continue;
+            const uint32_t* w = a.words + a.stmt_off[s];
+            const uint32_t w0 = w[0];
+            const uint32_t dst = w0 & 0xFFFFu, ns = (w0 >> 16) & 0xFFFu, ty = (w0 >> 28) & 7u;
+            uint32_t* D = lds + dst * sd + lane;
+            if (ty == ST_XOR_) {
+                uint32_t v = (w0 >> 31) ? *D : 0u;
+                for (uint32_t k = 0; k < ns; ++k) {
+                    const uint32_t sw = w[1 + k];
+                    v ^= (sw >> 31) ? gload(sw & 0xFFFFFFu) : lds[(sw & 0xFFFFu) * sd + lane];
+                }
+                *D = v;
+            } else if (ty == ST_MUL_) {
+                uint32_t v = (w0 >> 31) ? *D : 0u;
+                for (uint32_t k = 0; k < ns; ++k) {
+                    const uint32_t sw = w[1 + k];
+                    const uint32_t x = (sw >> 31) ? gload(sw & 0xFFFFFFu) : lds[(sw & 0xFFFFu) * sd + lane];
+                    v ^= gfmul4(x, (sw >> 16) & 0xFFu);
+                }
+                *D = v;
+            } else if (ty == ST_SCALE_) {
+                *D = gfmul4(*D, w[1]);
+            } else if (ty == ST_HORNER_) {
+                // HDPC chunk: t = alpha*t ^ y_j over the chunk; partial[h] ^= MT[h][j]*t;
+                // finally partial[h] ^= tau_h * t (contribution of the tail of MT*Gamma).
+                const uint32_t H = a.p.H;
+                for (uint32_t h = 0; h < H; ++h) D[h * sd] = 0u;
+                uint32_t t = 0;
+                for (uint32_t j = 0; j < ns; ++j) {
+                    const uint32_t e = w[1 + j];
+                    const uint32_t sl = e & 0xFFFFu;
+                    t = xtime4(t) ^ (sl != SLOT_NONE_ ? lds[sl * sd + lane] : 0u);
+                    if ((e >> 26) & 1u) {
+                        for (uint32_t h = 0; h < H; ++h) D[h * sd] ^= gfmul4(t, alpha_pow(h));
+                    } else {
+                        D[((e >> 16) & 31u) * sd] ^= t;
+                        D[((e >> 21) & 31u) * sd] ^= t;
+                    }
+                }
+                for (uint32_t h = 0; h < H; ++h) {
+                    const uint32_t tau = (w[1 + ns + (h >> 2)] >> (8 * (h & 3))) & 0xFFu;
+                    D[h * sd] ^= gfmul4(t, tau);
+                }
+            }
+        }
+        __syncthreads();
+    }
+
+    // ---- outputs: repair symbols (encodeGen) or syndromes (decode) ----
+    if (a.out) {
+        uint32_t o0 = 0, o1 = a.n_out;
+        if (a.out_off) { o0 = a.out_off[b]; o1 = a.out_off[b + 1]; }
+        for (uint32_t o = o0 + grp; o < o1; o += ngrp) {
+            const uint32_t esi = a.out_esi[o];
+            uint32_t v = 0;
+            if (esi < K) {
+                v = live ? gload(esi) : 0u;
+            } else if (live) {
+                d_for_cols(a.p, esi + a.p.Kp - K, [&](uint32_t c) { v ^= lds[(uint32_t)a.col_slot[c] * sd + lane]; });
+            }
+            const size_t off = a.out_off ? (size_t)o * T : (size_t)b * a.out_stride + (size_t)(o - o0) * T;
+            if (inb) {
+                if (a.xor_in) v ^= *reinterpret_cast<const uint32_t*>(a.xor_in + off + (size_t)(c0 + lane) * 4);
+                *reinterpret_cast<uint32_t*>(a.out + off + (size_t)(c0 + lane) * 4) = v;
+            }
+        }
+    }
+    if (a.c_out) {
+        for (uint32_t c = grp; c < a.p.L; c += ngrp)
+            if (inb)
+                *reinterpret_cast<uint32_t*>(a.c_out + (size_t)b * a.c_stride + (size_t)c * T + (size_t)(c0 + lane) * 4) =
+                    lds[(uint32_t)a.col_slot[c] * sd + lane];
+    }
+}
+
+// ------------------------------ decode: per-block GF(256) solve ------------------------------
+// M[j][k] = sum_{c in LT(isi_j)} Ainv[c][e_k] (received repair j, erased source e_k);
+// Gauss-Jordan on [M | I]: rank e <=> the reference's system is full rank.
+// Output: X (e x e) and the e received repairs it combines: x_k = sum_m X[k][m] sigma_{piv[m]}.
+__device__ __forceinline__ uint8_t gmul_t(const uint8_t* lg, const uint8_t* ex, uint8_t a, uint8_t b) {
+    return (a && b) ? ex[lg[a] + lg[b]] : (uint8_t)0;
+}
+
+__global__ void __launch_bounds__(256) k_solve(SolveArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
+    __shared__ uint8_t ex[512], lg[256];
+    __shared__ uint8_t fac[256];
+    __shared__ uint16_t rowid[256];
+    __shared__ int piv;
+    const uint32_t b = a.blk_map[blockIdx.x];
+    const uint32_t tid = threadIdx.x, nthr = blockDim.x;
+    const uint32_t e = a.erased_off[b + 1] - a.erased_off[b];
+    const uint32_t nr = a.rep_off[b + 1] - a.rep_off[b];
+    const uint32_t* E = a.erased + a.erased_off[b];
+    const uint32_t* R = a.rep_esi + a.rep_off[b];
+    const uint32_t ws = e + nr;
+    if (tid == 0) {
+        uint32_t x = 1;
+        for (int i = 0; i < 255; ++i) {
+            ex[i] = (uint8_t)x; ex[i + 255] = (uint8_t)x; lg[x] = (uint8_t)i;
+            x <<= 1; if (x & 0x100) x ^= 0x11D;
+        }
+        ex[510] = ex[0]; ex[511] = ex[1]; lg[0] = 0;
+    }
+    for (uint32_t r = tid; r < nr; r += nthr) rowid[r] = (uint16_t)r;
+    for (uint32_t idx = tid; idx < nr * ws; idx += nthr) sm[idx] = 0;
+    __syncthreads();
+    for (uint32_t idx = tid; idx < nr * e; idx += nthr) {
+        const uint32_t j = idx / e, k = idx - j * e;
+        const uint32_t col = E[k];
+        uint8_t v = 0;
+        d_for_cols(a.p, R[j] + a.p.Kp - a.p.K, [&](uint32_t c) { v ^= a.cid[(size_t)c * a.cid_stride + col]; });
+        sm[j * ws + k] = v;
+    }
+    for (uint32_t j = tid; j < nr; j += nthr) sm[j * ws + e + j] = 1;
+    __syncthreads();
+    for (uint32_t k = 0; k < e; ++k) {
+        if (tid == 0) piv = (int)nr;
+        __syncthreads();
+        for (uint32_t r = k + tid; r < nr; r += nthr)
+            if (sm[r * ws + k]) atomicMin(&piv, (int)r);
+        __syncthreads();
+        const uint32_t p = (uint32_t)piv;
+        if (p >= nr) {
+            if (tid == 0) a.status[b] = 0;
+            return;
+        }
+        if (p != k) {
+            for (uint32_t c = tid; c < ws; c += nthr) {
+                const uint8_t t = sm[p * ws + c]; sm[p * ws + c] = sm[k * ws + c]; sm[k * ws + c] = t;
+            }
+            if (tid == 0) { const uint16_t t = rowid[p]; rowid[p] = rowid[k]; rowid[k] = t; }
+            __syncthreads();
+        }
+        const uint8_t pv = sm[k * ws + k];
+        const uint8_t inv = ex[255 - lg[pv]];
+        __syncthreads();
+        for (uint32_t c = k + tid; c < ws; c += nthr) sm[k * ws + c] = gmul_t(lg, ex, sm[k * ws + c], inv);
+        for (uint32_t r = tid; r < nr; r += nthr) fac[r] = (r == k) ? 0 : sm[r * ws + k];
+        __syncthreads();
+        for (uint32_t idx = tid; idx < nr * (ws - k); idx += nthr) {
+            const uint32_t r = idx / (ws - k), c = k + (idx - r * (ws - k));
+            const uint8_t f = fac[r];
+            if (f) sm[r * ws + c] ^= gmul_t(lg, ex, f, sm[k * ws + c]);
+        }
+        __syncthreads();
+    }
+    uint8_t* X = a.xmat + (size_t)blockIdx.x * a.max_e * a.max_e;
+    uint16_t* XP = a.xpiv + (size_t)blockIdx.x * a.max_e;
+    for (uint32_t m = tid; m < e; m += nthr) XP[m] = rowid[m];
+    for (uint32_t idx = tid; idx < e * e; idx += nthr) {
+        const uint32_t k = idx / e, m = idx - k * e;
+        X[k * e + m] = sm[k * ws + e + rowid[m]];
+    }
+    if (tid == 0) a.status[b] = 1;
+}
+
+// ------------------------------ decode: x_E = X * sigma --------------------------------------
+// grid = (strips of 64 dwords, blocks); one wave per erased row at a time, one dword per lane.
+__global__ void __launch_bounds__(256) k_apply(ApplyArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t sg[];
+    const uint32_t b = a.blk_map[blockIdx.y];
+    if (a.status[b] != 1) return;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+    const uint32_t e = a.erased_off[b + 1] - a.erased_off[b];
+    const uint32_t Td = a.T >> 2, c0 = blockIdx.x * 64, width = min(64u, Td - c0);
+    const uint32_t* E = a.erased + a.erased_off[b];
+    const uint8_t* X = a.xmat + (size_t)blockIdx.y * a.max_e * a.max_e;
+    const uint16_t* XP = a.xpiv + (size_t)blockIdx.y * a.max_e;
+    uint8_t* xs = reinterpret_cast<uint8_t*>(sg + e * 64);
+    for (uint32_t i = tid; i < e * 64; i += blockDim.x) {
+        const uint32_t m = i >> 6, c = i & 63;
+        sg[i] = (c < width) ? *reinterpret_cast<const uint32_t*>(a.sigma + (size_t)(a.rep_off[b] + XP[m]) * a.T +
+                                                                  (size_t)(c0 + c) * 4)
+                            : 0u;
+    }
+    for (uint32_t i = tid; i < e * e; i += blockDim.x) xs[i] = X[i];
+    __syncthreads();
+    uint8_t* blk = a.data + (size_t)b * a.data_stride;
+    for (uint32_t k = wave; k < e; k += nw) {
+        uint32_t acc = 0;
+        for (uint32_t m = 0; m < e; ++m) {
+            const uint32_t c = xs[k * e + m];
+            if (c) acc ^= gfmul4(sg[m * 64 + lane], c);
+        }
+        if (lane < width) *reinterpret_cast<uint32_t*>(blk + (size_t)E[k] * a.T + (size_t)(c0 + lane) * 4) = acc;
+    }
+}
+
+int launch_solve(const SolveArgs& a, uint32_t n_blocks, uint32_t lds_bytes, void* stream) {
+    hipLaunchKernelGGL(k_solve, dim3(n_blocks), dim3(256), lds_bytes, (hipStream_t)stream, a);
+    return (int)hipGetLastError();
+}
+
+int launch_apply(const ApplyArgs& a, uint32_t n_strips, uint32_t n_blocks, uint32_t lds_bytes, void* stream) {
+    hipLaunchKernelGGL(k_apply, dim3(n_strips, n_blocks), dim3(256), lds_bytes, (hipStream_t)stream, a);
+    return (int)hipGetLastError();
+}
+
+// ------------------------------ gather repairs from a device-resident C ----------------------
+// Per-call API: out[r] = XOR of C rows of LT(isi_r) (encodeGen, RQ/params.go:162-182).
+__global__ void __launch_bounds__(256) k_gather(DevParams p, const uint8_t* C, uint32_t T, const uint32_t* esi,
+                                                uint32_t n, uint8_t* out) {
+    const uint32_t r = blockIdx.x;
+    if (r >= n) return;
+    const uint32_t Td = T >> 2;
+    const uint32_t isi = esi[r] + p.Kp - p.K;
+    for (uint32_t c = threadIdx.x; c < Td; c += blockDim.x) {
+        uint32_t v = 0;
+        d_for_cols(p, isi, [&](uint32_t col) { v ^= reinterpret_cast<const uint32_t*>(C + (size_t)col * T)[c]; });
+        reinterpret_cast<uint32_t*>(out + (size_t)r * T)[c] = v;
+    }
+}
+
+int launch_gather(const DevParams& p, const uint8_t* C, uint32_t T, const uint32_t* esi, uint32_t n, uint8_t* out,
+                  void* stream) {
+    hipLaunchKernelGGL(k_gather, dim3(n), dim3(256), 0, (hipStream_t)stream, p, C, T, esi, n, out);
+    return (int)hipGetLastError();
+}
+
+int launch_encode(const EncArgs& a, uint32_t n_strips, uint32_t n_blocks, uint32_t group, void* stream) {
+    const uint32_t nebw = a.erased_off ? (a.p.K + 31) / 32 : 0;
+    const size_t lds = ((size_t)a.n_slots * a.sd + nebw) * 4;
+    dim3 grid(n_strips, n_blocks), block(256);
+    hipStream_t s = (hipStream_t)stream;
+    static bool attr_set = false;  // allow the full 160 KiB of LDS for every instantiation
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)k_encode<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_encode<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_encode<32>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_encode<64>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_solve, hipFuncAttributeMaxDynamicSharedMemorySize, 158 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_apply, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr_set = true;
+    }
+    switch (group) {
+        case 8: hipLaunchKernelGGL(k_encode<8>, grid, block, lds, s, a); break;
+        case 16: hipLaunchKernelGGL(k_encode<16>, grid, block, lds, s, a); break;
+        case 32: hipLaunchKernelGGL(k_encode<32>, grid, block, lds, s, a); break;
+        case 64: hipLaunchKernelGGL(k_encode<64>, grid, block, lds, s, a); break;
+        default: return (int)hipErrorInvalidValue;
+    }
+    return (int)hipGetLastError();
+}
+
+}  // namespace rq

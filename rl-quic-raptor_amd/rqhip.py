@@ -1,0 +1,330 @@
+"""Python binding of librqhip.so (ctypes), mirroring go/fec/raptorq_wrap.go.
+
+The reference API (go/fec/raptorq_wrap.go:13-124) is reproduced name for name so the parity
+tests read like the reference's own usage (go/cmd/raptorq_eval/main.go:199-222,
+go/integrationtests/fec/raptorq_experiments_test.go:142-172):
+
+    NewRaptorQEncoder(data, K, L) -> RaptorQEncoder   .GenSymbol(id) .BaseSymbolsNum()
+    NewRaptorQDecoder(dataSize, L) -> RaptorQDecoder  .AddSymbol(id, data) .Decode()
+    RaptorQEncodeBlock(data, N, K, L) -> [Packet]
+    RaptorQDecodeBytes(recv, N, K, L, dataSize) -> (bytes, ok)
+
+Go's (value, error) returns become Python exceptions (RaptorQError) carrying the same message.
+The batch functions take torch CUDA tensors (device pointers) and drive the device-resident
+hot path.  All compute happens in the HIP kernels of librqhip.so: if the library or a gfx950
+device is missing the calls fail loudly -- there is no CPU fallback.
+"""
+import ctypes
+import os
+import subprocess
+from dataclasses import dataclass
+from pathlib import Path
+
+_HERE = Path(__file__).resolve().parent
+LIB_PATH = _HERE / "build" / "librqhip.so"
+_lib = None
+
+RQ_OK = 0
+RQ_ERR_SYMBOL_SIZE_ZERO = -1
+RQ_ERR_K_TOO_BIG = -2
+RQ_ERR_NOT_ENOUGH = -3
+RQ_ERR_SYMBOL_SIZE = -4
+RQ_ERR_BAD_ARG = -5
+RQ_ERR_DEVICE = -6
+RQ_ERR_UNSUPPORTED = -7
+RQ_ERR_PLAN = -8
+
+EXPORTED = (
+    "rq_strerror", "rq_last_error", "rq_params", "rq_encoder_create", "rq_encoder_k",
+    "rq_encoder_symbol_size", "rq_encoder_symbol", "rq_encoder_symbols", "rq_encoder_free",
+    "rq_decoder_create", "rq_decoder_k", "rq_decoder_add", "rq_decoder_decode", "rq_decoder_free",
+    "rq_encode_batch", "rq_decode_batch", "rq_device_count", "rq_set_device", "rq_plan_stats",
+    "rq_plan_export",
+)
+
+
+class RaptorQError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(msg)
+        self.code = code
+
+
+class EncodeDesc(ctypes.Structure):
+    _fields_ = [("T", ctypes.c_uint32), ("K", ctypes.c_uint32), ("n_blocks", ctypes.c_uint32),
+                ("src", ctypes.c_void_p), ("src_stride", ctypes.c_uint64), ("n_esi", ctypes.c_uint32),
+                ("esi", ctypes.POINTER(ctypes.c_uint32)), ("out", ctypes.c_void_p),
+                ("out_stride", ctypes.c_uint64), ("c_out", ctypes.c_void_p), ("c_stride", ctypes.c_uint64),
+                ("stream", ctypes.c_void_p)]
+
+
+class DecodeDesc(ctypes.Structure):
+    _fields_ = [("T", ctypes.c_uint32), ("K", ctypes.c_uint32), ("n_blocks", ctypes.c_uint32),
+                ("data", ctypes.c_void_p), ("data_stride", ctypes.c_uint64),
+                ("n_erased", ctypes.POINTER(ctypes.c_uint32)), ("erased", ctypes.POINTER(ctypes.c_uint32)),
+                ("n_repair", ctypes.POINTER(ctypes.c_uint32)), ("repair_esi", ctypes.POINTER(ctypes.c_uint32)),
+                ("repair", ctypes.c_void_p), ("status", ctypes.POINTER(ctypes.c_int32)),
+                ("stream", ctypes.c_void_p)]
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", str(_HERE), "-j8"], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise RaptorQError(RQ_ERR_DEVICE, "librqhip.so not built (run `make -C rl-quic-raptor_amd`)")
+        L = ctypes.CDLL(str(LIB_PATH))
+        u8p = ctypes.POINTER(ctypes.c_uint8)
+        u16p = ctypes.POINTER(ctypes.c_uint16)
+        u32p = ctypes.POINTER(ctypes.c_uint32)
+        ip = ctypes.POINTER(ctypes.c_int)
+        vp = ctypes.c_void_p
+        sig = {
+            "rq_strerror": ([ctypes.c_int], ctypes.c_char_p),
+            "rq_last_error": ([], ctypes.c_char_p),
+            "rq_params": ([ctypes.c_uint64, ctypes.c_uint32, u32p], ctypes.c_int),
+            "rq_encoder_create": ([u8p, ctypes.c_size_t, ctypes.c_uint32, ip], vp),
+            "rq_encoder_k": ([vp], ctypes.c_uint32),
+            "rq_encoder_symbol_size": ([vp], ctypes.c_uint32),
+            "rq_encoder_symbol": ([vp, ctypes.c_uint32, u8p], ctypes.c_int),
+            "rq_encoder_symbols": ([vp, ctypes.c_uint32, ctypes.c_uint32, u8p], ctypes.c_int),
+            "rq_encoder_free": ([vp], None),
+            "rq_decoder_create": ([ctypes.c_uint64, ctypes.c_uint32, ip], vp),
+            "rq_decoder_k": ([vp], ctypes.c_uint32),
+            "rq_decoder_add": ([vp, ctypes.c_uint32, u8p, ctypes.c_size_t, ip], ctypes.c_int),
+            "rq_decoder_decode": ([vp, u8p, ip], ctypes.c_int),
+            "rq_decoder_free": ([vp], None),
+            "rq_encode_batch": ([ctypes.POINTER(EncodeDesc)], ctypes.c_int),
+            "rq_decode_batch": ([ctypes.POINTER(DecodeDesc)], ctypes.c_int),
+            "rq_device_count": ([], ctypes.c_int),
+            "rq_set_device": ([ctypes.c_int], ctypes.c_int),
+            "rq_plan_stats": ([ctypes.c_uint32, u32p], ctypes.c_int),
+            "rq_plan_export": ([ctypes.c_uint32, u32p, u32p, u32p, u32p, u16p, u16p], ctypes.c_int),
+        }
+        for name, (args, res) in sig.items():
+            f = getattr(L, name)
+            f.argtypes = args
+            f.restype = res
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != RQ_OK:
+        detail = lib().rq_last_error().decode() or lib().rq_strerror(rc).decode()
+        raise RaptorQError(rc, detail)
+    return rc
+
+
+def _buf(data):
+    b = bytes(data)
+    return b, (ctypes.c_uint8 * max(len(b), 1)).from_buffer_copy(b if b else b"\0")
+
+
+# ------------------------------------------------------------------ parameters / plans
+PARAM_NAMES = ("K", "Kp", "J", "S", "H", "W", "L", "P", "P1", "U", "B")
+
+
+def params(size, T):
+    out = (ctypes.c_uint32 * 11)()
+    _check(lib().rq_params(size, T, out))
+    return dict(zip(PARAM_NAMES, list(out)))
+
+
+PLAN_STAT_NAMES = ("n_stmts", "n_levels", "n_src_xor", "n_src_mul", "n_global", "u", "inactivated",
+                   "n_pivots", "n_slots", "passB_inplace", "passB_rebuild")
+
+
+def plan_stats(K):
+    out = (ctypes.c_uint32 * 11)()
+    _check(lib().rq_plan_stats(K, out))
+    return dict(zip(PLAN_STAT_NAMES, list(out)))
+
+
+def plan_export(K):
+    """The compiled per-K' program (numpy arrays) for host-side verification in tests."""
+    import numpy as np
+    sizes = (ctypes.c_uint32 * 5)()
+    _check(lib().rq_plan_export(K, sizes, None, None, None, None, None))
+    n_lv, n_so, n_w, Kp, L = list(sizes)
+    lv = np.zeros(n_lv, np.uint32)
+    so = np.zeros(n_so, np.uint32)
+    w = np.zeros(n_w, np.uint32)
+    ls = np.zeros(Kp, np.uint16)
+    cs = np.zeros(L, np.uint16)
+    P32 = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+    P16 = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16))
+    _check(lib().rq_plan_export(K, sizes, P32(lv), P32(so), P32(w), P16(ls), P16(cs)))
+    return dict(level_start=lv, stmt_off=so, words=w, load_slot=ls, col_slot=cs, Kp=Kp, L=L)
+
+
+def device_count():
+    return lib().rq_device_count()
+
+
+# ------------------------------------------------------------------ go/fec mirror
+@dataclass
+class Packet:
+    """fec.Packet (go/fec/packet_polar.go:87-90)."""
+    Index: int
+    Data: bytes
+
+
+class RaptorQEncoder:
+    """go/fec RaptorQEncoder (raptorq_wrap.go:13-18, 29-49)."""
+
+    def __init__(self, handle, K, L):
+        self._h = handle
+        self.K = K
+        self.L = L
+
+    def GenSymbol(self, id):
+        T = lib().rq_encoder_symbol_size(self._h)
+        out = (ctypes.c_uint8 * T)()
+        _check(lib().rq_encoder_symbol(self._h, id, out))
+        return bytes(out)
+
+    def GenSymbols(self, first, count):
+        """Batch extension: symbols first..first+count-1 in one device launch."""
+        T = lib().rq_encoder_symbol_size(self._h)
+        out = (ctypes.c_uint8 * max(T * count, 1))()
+        _check(lib().rq_encoder_symbols(self._h, first, count, out))
+        b = bytes(out)
+        return [b[i * T:(i + 1) * T] for i in range(count)]
+
+    def BaseSymbolsNum(self):
+        return lib().rq_encoder_k(self._h)
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.rq_encoder_free(self._h)
+            self._h = None
+
+
+def NewRaptorQEncoder(data, K, L):
+    if K <= 0 or L <= 0:
+        raise RaptorQError(RQ_ERR_BAD_ARG, "bad K or L")
+    b, arr = _buf(data)
+    err = ctypes.c_int(0)
+    h = lib().rq_encoder_create(arr, len(b), L, ctypes.byref(err))
+    if not h:
+        _check(err.value)
+    return RaptorQEncoder(h, K, L)
+
+
+class RaptorQDecoder:
+    """go/fec RaptorQDecoder (raptorq_wrap.go:20-25, 52-74)."""
+
+    def __init__(self, handle, K, L, size):
+        self._h = handle
+        self.K = K
+        self.L = L
+        self._size = size
+
+    def AddSymbol(self, id, data):
+        b, arr = _buf(data)
+        can = ctypes.c_int(0)
+        _check(lib().rq_decoder_add(self._h, id, arr, len(b), ctypes.byref(can)))
+        return bool(can.value)
+
+    def Decode(self):
+        """(ok, bytes|None); raises RaptorQError('not enough symbols to decode')."""
+        out = (ctypes.c_uint8 * max(self._size, 1))()
+        ok = ctypes.c_int(0)
+        _check(lib().rq_decoder_decode(self._h, out, ctypes.byref(ok)))
+        if not ok.value:
+            return False, None
+        return True, bytes(out)[:self._size]
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.rq_decoder_free(self._h)
+            self._h = None
+
+
+def NewRaptorQDecoder(dataSize, L):
+    if dataSize < 0 or L <= 0:
+        raise RaptorQError(RQ_ERR_BAD_ARG, "bad dataSize or L")
+    err = ctypes.c_int(0)
+    h = lib().rq_decoder_create(dataSize, L, ctypes.byref(err))
+    if not h:
+        _check(err.value)
+    return RaptorQDecoder(h, lib().rq_decoder_k(h), L, dataSize)
+
+
+def RaptorQEncodeBlock(data, N, K, L):
+    """raptorq_wrap.go:81-99 (GenSymbol 0..N-1; repairs generated in one launch)."""
+    if N <= 0 or K <= 0 or L <= 0 or K > N:
+        raise RaptorQError(RQ_ERR_BAD_ARG, "bad N/K/L")
+    data = bytes(data)[:K * L]
+    enc = NewRaptorQEncoder(data, K, L)
+    return [Packet(i, s) for i, s in enumerate(enc.GenSymbols(0, N))]
+
+
+def RaptorQDecodeBytes(recv, N, K, L, dataSize):
+    """raptorq_wrap.go:103-124: ignores out-of-range indices and AddSymbol errors."""
+    if K <= 0 or L <= 0 or dataSize < 0:
+        return None, False
+    try:
+        dec = NewRaptorQDecoder(dataSize, L)
+    except RaptorQError:
+        return None, False
+    for p in recv:
+        if p.Index < 0 or p.Index >= N:
+            continue
+        try:
+            dec.AddSymbol(p.Index, p.Data)
+        except RaptorQError:
+            pass
+    try:
+        ok, out = dec.Decode()
+    except RaptorQError:
+        return None, False
+    if not ok:
+        return None, False
+    return out, True
+
+
+# ------------------------------------------------------------------ device-resident batch API
+def _stream_ptr(stream):
+    if stream is None:
+        return None
+    return ctypes.c_void_p(stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream))
+
+
+def encode_batch(src, K, T, esis, out, c_out=None, stream=None):
+    """src: uint8 CUDA tensor [n_blocks, K*T] (contiguous rows); out: [n_blocks, len(esis)*T]."""
+    n_blocks = src.shape[0]
+    esi_arr = (ctypes.c_uint32 * max(len(esis), 1))(*esis)
+    d = EncodeDesc(T=T, K=K, n_blocks=n_blocks, src=src.data_ptr(), src_stride=src.stride(0),
+                   n_esi=len(esis), esi=esi_arr, out=out.data_ptr() if out is not None else None,
+                   out_stride=out.stride(0) if out is not None else 0,
+                   c_out=c_out.data_ptr() if c_out is not None else None,
+                   c_stride=c_out.stride(0) if c_out is not None else 0, stream=_stream_ptr(stream))
+    _check(lib().rq_encode_batch(ctypes.byref(d)))
+
+
+class DecodeBatch:
+    """Host-side descriptor arrays for decode_batch, prepared once per erasure pattern."""
+
+    def __init__(self, K, T, erased_lists, repair_lists):
+        import numpy as np
+        self.K, self.T = K, T
+        self.n_blocks = len(erased_lists)
+        self.n_erased = np.array([len(e) for e in erased_lists], np.uint32)
+        self.erased = np.concatenate([np.asarray(e, np.uint32) for e in erased_lists] + [np.zeros(1, np.uint32)])
+        self.n_repair = np.array([len(r) for r in repair_lists], np.uint32)
+        self.repair_esi = np.concatenate([np.asarray(r, np.uint32) for r in repair_lists] + [np.zeros(1, np.uint32)])
+        self.status = np.zeros(self.n_blocks, np.int32)
+
+    def run(self, data, repair, stream=None):
+        P32 = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+        d = DecodeDesc(T=self.T, K=self.K, n_blocks=self.n_blocks, data=data.data_ptr(),
+                       data_stride=data.stride(0), n_erased=P32(self.n_erased), erased=P32(self.erased),
+                       n_repair=P32(self.n_repair), repair_esi=P32(self.repair_esi),
+                       repair=repair.data_ptr(), status=self.status.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                       stream=_stream_ptr(stream))
+        _check(lib().rq_decode_batch(ctypes.byref(d)))
+        return self.status

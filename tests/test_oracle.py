@@ -1,0 +1,159 @@
+"""Pin the oracle (oracle/rq_oracle.c) before trusting it.
+
+The reference holds no golden vectors for this path (its tests check
+round-trip equality only), so the oracle is pinned by every known answer available:
+RFC 6330 table spot values, the derived-parameter rows of SURVEY.md sec. 8 (incl. the library's
+P1 quirk, RQ/params.go:55-58), the GF(256) tables (RQ/discmath/oct.go), the algebraic
+invariants of Appendix A (C satisfies every LDPC/HDPC/LT equation; repairs are LT XORs of C),
+and round trips mirroring raptorq_experiments_test.go:105-310.
+"""
+import numpy as np
+import pytest
+
+# SURVEY.md sec. 8 "Derived parameters at the configs" (from ParamsTable @0x5f6b20)
+SURVEY_ROWS = {
+    64: (69, 157, 13, 10, 79, 92, 13, 17, 66, 3),
+    128: (138, 660, 19, 10, 149, 167, 18, 19, 130, 8),
+    256: (257, 265, 29, 10, 271, 296, 25, 29, 242, 15),
+    512: (526, 923, 41, 10, 541, 577, 36, 37, 500, 26),
+    1024: (1032, 824, 59, 10, 1051, 1101, 50, 53, 992, 40),
+    2048: (2070, 506, 89, 11, 2099, 2170, 71, 73, 2010, 60),
+}
+
+
+@pytest.mark.parametrize("K", sorted(SURVEY_ROWS))
+def test_params_match_survey_rows(oracle, K):
+    p, _ = oracle.params(K * 1200, 1200)
+    Kp, J, S, H, W, L, P, P1, B, U = SURVEY_ROWS[K]
+    assert (p["K"], p["Kp"], p["J"], p["S"], p["H"], p["W"], p["L"], p["P"], p["P1"], p["B"], p["U"]) == \
+        (K, Kp, J, S, H, W, L, P, P1, B, U)
+
+
+def test_p1_quirk_strictly_greater(oracle):
+    # K=64: P=13 is prime, library P1=17 (RFC 6330 would give 13); K=2048: P=71 -> 73.
+    assert oracle.params(64 * 16, 16)[0]["P1"] == 17
+    assert oracle.params(2048 * 16, 16)[0]["P1"] == 73
+
+
+def test_p1_quirk_row_count(oracle):
+    def isprime(n):
+        return n > 1 and all(n % d for d in range(2, int(n ** 0.5) + 1))
+    import re
+    from pathlib import Path
+    src = (Path(__file__).resolve().parent.parent / "rl-quic-raptor_amd/csrc/rfc6330_tables.h").read_text()
+    rows = re.findall(r"\{(\d+)u, (\d+)u, (\d+)u, (\d+)u, (\d+)u\}", src)
+    assert len(rows) == 477
+    n_prime = 0
+    for r in rows:
+        Kp = int(r[0])
+        p, _ = oracle.params(Kp, 1)
+        if isprime(p["P"]):
+            n_prime += 1
+            assert p["P1"] > p["P"]
+    assert n_prime == 99
+
+
+def test_errors(oracle):
+    with pytest.raises(ValueError, match="symbol size cannot be zero"):
+        oracle.params(100, 0)
+    with pytest.raises(ValueError, match="k is too big"):
+        oracle.params(56404 * 4, 4)
+    assert oracle.params(56403 * 4, 4)[0]["Kp"] == 56403
+
+
+def test_gf_tables(oracle):
+    exp, log = oracle.gf_tables()
+    assert exp[8] == 29 and list(exp[:16]) == [1, 2, 4, 8, 16, 32, 64, 128, 29, 58, 116, 232, 205, 135, 19, 38]
+    assert list(log[:16]) == [0, 0, 1, 25, 2, 50, 26, 198, 3, 223, 51, 238, 27, 104, 199, 75]
+    for a in (1, 2, 3, 29, 200, 255):
+        for b in (1, 7, 128, 254):
+            assert oracle.lib().rqo_gf_mul(a, b) == oracle.lib().rqo_gf_mul(b, a)
+
+
+def test_rand_spot_values(oracle):
+    # Rand(y, i, m) with m = 2^32 - 1 exposes the raw table XOR (RFC 6330 sec. 5.3.5.1)
+    assert oracle.rand(0, 0, 0xFFFFFFFF) == (251291136 ^ 807385413 ^ 1629829892 ^ 1191369816) % 0xFFFFFFFF
+
+
+def _gf_mat_vec(oracle, row, C):
+    """row (L GF(256) coefs) . C (L x T) over GF(256)."""
+    exp, log = oracle.gf_tables()
+    acc = np.zeros(C.shape[1], np.uint8)
+    for c in np.nonzero(row)[0]:
+        coef = int(row[c])
+        x = C[c]
+        if coef == 1:
+            acc ^= x
+        else:
+            nz = x != 0
+            y = np.zeros_like(x)
+            y[nz] = exp[(log[x[nz]].astype(np.int32) + int(log[coef])) % 255]
+            acc ^= y
+    return acc
+
+
+@pytest.mark.parametrize("K,T", [(64, 48), (5, 20), (257, 16)])
+def test_intermediate_symbols_satisfy_constraints(oracle, K, T):
+    """Appendix A: captured C satisfied every LDPC/HDPC/LT row."""
+    rng = np.random.default_rng(K)
+    data = rng.integers(0, 256, K * T - 3, dtype=np.uint8)
+    p, pvec = oracle.params(len(data), T)
+    C = oracle.encode_C(data, T)
+    ldpc, hdpc = oracle.constraint_rows(pvec)
+    for r in range(p["S"]):
+        assert not _gf_mat_vec(oracle, ldpc[r], C).any()
+    for r in range(p["H"]):
+        assert not _gf_mat_vec(oracle, hdpc[r], C).any()
+    src = np.zeros((p["Kp"], T), np.uint8)
+    src.reshape(-1)[:len(data)] = data
+    for i in range(p["Kp"]):
+        acc = np.zeros(T, np.uint8)
+        for c in oracle.lt_cols(pvec, i):
+            acc ^= C[c]
+        assert np.array_equal(acc, src[i]), i
+
+
+def test_lt_cols_distinct(oracle):
+    """encodeGen XORs each listed row and the matrix uses Set(.,1); they agree only if the
+    columns of a tuple are distinct (Appendix A note) -- check it over many ISIs."""
+    for K in (64, 256, 1024, 2048):
+        _, pvec = oracle.params(K * 8, 8)
+        for isi in range(0, 3000, 7):
+            cols = oracle.lt_cols(pvec, isi)
+            assert len(cols) == len(set(cols))
+
+
+@pytest.mark.parametrize("K,T,N,p_loss,seed", [(5, 1100, 8, 0.25, 1337), (26, 64, 32, 0.15, 7),
+                                                (64, 48, 80, 0.10, 3)])
+def test_round_trip(oracle, K, T, N, p_loss, seed):
+    """Mirrors TestRaptorQ_ExperimentB_Scaled (raptorq_experiments_test.go:105-310)."""
+    rng = np.random.default_rng(seed)
+    data = rng.integers(0, 256, K * T, dtype=np.uint8).tobytes()
+    enc = oracle.OracleEncoder(data, T)
+    for trial in range(5):
+        dec = oracle.OracleDecoder(len(data), T)
+        ok_add = False
+        for i in range(N):
+            if rng.random() < p_loss:
+                continue
+            ok_add = dec.add_symbol(i, enc.gen_symbol(i).tobytes())
+        if not ok_add:
+            with pytest.raises(RuntimeError, match="not enough"):
+                dec.decode()
+            continue
+        ok, out = dec.decode()
+        if ok:
+            assert out == data
+
+
+def test_add_symbol_bool_semantics(oracle):
+    """AddSymbol returns K <= unique symbols held (RQ/decoder.go:47,57)."""
+    K, T = 26, 16
+    data = bytes(i % 251 for i in range(K * T))
+    enc = oracle.OracleEncoder(data, T)
+    dec = oracle.OracleDecoder(len(data), T)
+    res = [dec.add_symbol(i, enc.gen_symbol(i).tobytes()) for i in range(32)]
+    assert res == [False] * 25 + [True] * 7
+    assert dec.add_symbol(3, enc.gen_symbol(3).tobytes())  # duplicate, still >= K
+    with pytest.raises(ValueError, match="incorrect symbol size 15, should be 16"):
+        dec.add_symbol(40, b"x" * 15)
