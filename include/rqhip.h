@@ -115,6 +115,10 @@ int rq_plan_stats(uint32_t K, uint32_t stats[11]);
 int rq_plan_export(uint32_t K, uint32_t sizes[5], uint32_t* level_start, uint32_t* stmt_off,
                    uint32_t* words, uint16_t* load_slot, uint16_t* col_slot);
 
+/* Export the per-wave instruction streams k_encode executes (tests).  sizes[0..3] =
+ * {n_words, n_waves, n_levels, n_slots}; wave_off receives n_waves stream offsets. */
+int rq_wave_export(uint32_t K, uint32_t sizes[4], uint32_t* words, uint32_t* wave_off);
+
 #ifdef __cplusplus
 }
 #endif

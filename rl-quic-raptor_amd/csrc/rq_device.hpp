@@ -19,9 +19,9 @@ struct EncArgs {
     uint32_t sd;               // strip width in dwords (<= group size)
     uint32_t n_levels;
     const uint16_t* load_slot; // [K']
-    const uint32_t* level_start;
-    const uint32_t* stmt_off;
-    const uint32_t* words;
+    const uint32_t* wstream;   // wave program (WaveProgram::words)
+    const uint32_t* wave_off;  // [n_waves] stream offsets
+    uint32_t n_waves;
     const uint16_t* col_slot;  // [L]
     const uint32_t* blk_map;   // optional: grid.y -> block index
     // erasures (decode): per block [erased_off[b], erased_off[b+1]) into erased[] (source ESIs)

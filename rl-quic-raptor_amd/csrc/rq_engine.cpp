@@ -54,9 +54,12 @@ struct DevBuf {
     ~DevBuf() { if (p) (void)hipFree(p); }
 };
 
+constexpr uint32_t ENC_WAVES = 8;  // waves per k_encode workgroup (rq_kernels.hip)
+
 struct DevPlan {
     Plan host;
-    DevBuf load_slot, level_start, stmt_off, words, col_slot;
+    WaveProgram wp;
+    DevBuf load_slot, wstream, wave_off, col_slot;
     DevBuf cid;            // A^-1 restricted to source columns (decode), L x cid_stride bytes
     uint32_t cid_stride = 0;
     bool cid_ready = false;
@@ -140,10 +143,11 @@ int get_dev_plan(DevCtx* ctx, const Params& p, DevPlan** out) {
         if (rc) return rc;
         std::unique_ptr<DevPlan> n(new DevPlan());
         n->host = *hp;
+        std::string err;
+        if (!build_wave_program(n->host, ENC_WAVES, &n->wp, &err)) return fail(RQ_ERR_PLAN, err);
         if ((rc = upload(n->load_slot, n->host.load_slot))) return rc;
-        if ((rc = upload(n->level_start, n->host.level_start))) return rc;
-        if ((rc = upload(n->stmt_off, n->host.stmt_off))) return rc;
-        if ((rc = upload(n->words, n->host.words))) return rc;
+        if ((rc = upload(n->wstream, n->wp.words))) return rc;
+        if ((rc = upload(n->wave_off, n->wp.wave_off))) return rc;
         if ((rc = upload(n->col_slot, n->host.col_slot))) return rc;
         dp = std::move(n);
     }
@@ -161,13 +165,13 @@ DevParams dev_params(const Params& p) {
 struct Geometry {
     uint32_t sd, n_strips, group;
 };
-int geometry(const Plan& pl, uint32_t T, uint32_t K, bool erasures, Geometry* g) {
+int geometry(const DevPlan& dp, uint32_t T, uint32_t K, bool erasures, Geometry* g) {
     const uint32_t Td = T / 4;
-    const size_t budget = 160 * 1024 - (erasures ? ((K + 31) / 32) * 4 : 0);
-    const size_t per_dword = (size_t)pl.n_slots * 4;
+    const size_t budget = 160 * 1024 - 128 * 6 * 4 - (erasures ? ((K + 31) / 32) * 4 : 0);  // - tuple staging
+    const size_t per_dword = (size_t)dp.wp.n_slots * 4;
     uint32_t sd_max = (uint32_t)std::min<size_t>(32, budget / per_dword);
     if (sd_max == 0) return fail(RQ_ERR_UNSUPPORTED, "K' too large for the LDS-resident plan (n_slots=" +
-                                                         std::to_string(pl.n_slots) + ")");
+                                                         std::to_string(dp.wp.n_slots) + ")");
     g->n_strips = (Td + sd_max - 1) / sd_max;
     g->sd = (Td + g->n_strips - 1) / g->n_strips;
     g->group = 8;
@@ -180,13 +184,13 @@ EncArgs base_args(const DevPlan& dp, const Params& p, uint32_t T, uint32_t sd) {
     std::memset(&a, 0, sizeof a);
     a.p = dev_params(p);
     a.T = T;
-    a.n_slots = dp.host.n_slots;
+    a.n_slots = dp.wp.n_slots;
     a.sd = sd;
-    a.n_levels = (uint32_t)dp.host.level_start.size() - 1;
+    a.n_levels = dp.wp.n_levels;
     a.load_slot = dp.load_slot.as<uint16_t>();
-    a.level_start = dp.level_start.as<uint32_t>();
-    a.stmt_off = dp.stmt_off.as<uint32_t>();
-    a.words = dp.words.as<uint32_t>();
+    a.wstream = dp.wstream.as<uint32_t>();
+    a.wave_off = dp.wave_off.as<uint32_t>();
+    a.n_waves = dp.wp.n_waves;
     a.col_slot = dp.col_slot.as<uint16_t>();
     return a;
 }
@@ -199,7 +203,7 @@ int encode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, c
     int rc = get_dev_plan(ctx, p, &dp);
     if (rc) return rc;
     Geometry g;
-    if ((rc = geometry(dp->host, T, p.K, false, &g))) return rc;
+    if ((rc = geometry(*dp, T, p.K, false, &g))) return rc;
     EncArgs a = base_args(*dp, p, T, g.sd);
     a.src = static_cast<const uint8_t*>(src);
     a.src_stride = src_stride;
@@ -289,7 +293,7 @@ int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, v
 
     // 1) syndromes: sigma_j = r_j ^ G_j A^-1 D(S with erased rows zeroed)
     Geometry g;
-    if ((rc = geometry(dp->host, T, p.K, true, &g))) return rc;
+    if ((rc = geometry(*dp, T, p.K, true, &g))) return rc;
     EncArgs a = base_args(*dp, p, T, g.sd);
     a.src = static_cast<const uint8_t*>(data);
     a.src_stride = data_stride;
@@ -434,6 +438,22 @@ int rq_plan_export(uint32_t K, uint32_t sizes[5], uint32_t* level_start, uint32_
     if (words) std::memcpy(words, pl->words.data(), pl->words.size() * 4);
     if (load_slot) std::memcpy(load_slot, pl->load_slot.data(), pl->load_slot.size() * 2);
     if (col_slot) std::memcpy(col_slot, pl->col_slot.data(), pl->col_slot.size() * 2);
+    return RQ_OK;
+}
+
+int rq_wave_export(uint32_t K, uint32_t sizes[4], uint32_t* words, uint32_t* wave_off) {
+    const Plan* pl;
+    int rc = host_plan(K, &pl);
+    if (rc) return rc;
+    WaveProgram wp;
+    std::string err;
+    if (!build_wave_program(*pl, ENC_WAVES, &wp, &err)) return fail(RQ_ERR_PLAN, err);
+    sizes[0] = (uint32_t)wp.words.size();
+    sizes[1] = wp.n_waves;
+    sizes[2] = wp.n_levels;
+    sizes[3] = wp.n_slots;
+    if (words) std::memcpy(words, wp.words.data(), wp.words.size() * 4);
+    if (wave_off) std::memcpy(wave_off, wp.wave_off.data(), wp.wave_off.size() * 4);
     return RQ_OK;
 }
 

@@ -103,23 +103,53 @@ __device__ __forceinline__ void d_for_cols(const DevParams& p, uint32_t X, F&& f
 }
 
 // ------------------------------ encode: plan replay ------------------------------------------
-// grid = (n_strips, n_blocks), block = 256 threads = 256/GS lane groups; LDS = n_slots*sd dwords
-// (+ erasure bitmap).  Each level's statements are independent; lane group g executes
-// statements g, g+ngrp, ... of the level, one dword of the strip per lane.
-template <int GS>
-__global__ void __launch_bounds__(256) k_encode(EncArgs a) {
+constexpr uint32_t OUT_BATCH = 128;  // LT tuples staged in LDS per output batch
+
+__device__ __forceinline__ uint32_t d_degree(uint32_t v, uint32_t W) {
+    // first d with v < DEG[d] (DEG[0] = 0, DEG[30] = 2^20 > v): branch-free binary search
+    uint32_t lo = 0;
+#pragma unroll
+    for (uint32_t step = 16; step; step >>= 1)
+        if (lo + step <= 30 && c_DEG[lo + step - 1] <= v) lo += step;
+    const uint32_t d = lo;  // c_DEG[d-1] <= v < c_DEG[d]
+    return d > W - 2 ? W - 2 : d;
+}
+
+// grid = (n_strips, n_blocks), block = NW waves.  LDS: n_slots x sd dwords, the LT-tuple
+// staging area (OUT_BATCH x 6 words) and the erasure bitmap.  Each wave executes its own
+// instruction stream (WaveProgram): an op runs two statements side by side (lanes 0-31
+// statement A, lanes 32-63 statement B, one strip dword per lane); a workgroup barrier closes
+// each dependency level.  Descriptor words are wave-uniform and live in two VGPR pages (current
+// and prefetched next), extracted with v_readlane: no memory latency inside a segment.
+template <int NW>
+__global__ void __launch_bounds__(NW * 64) k_encode(EncArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t sd = a.sd, T = a.T, Td = T >> 2;
     const uint32_t strip = blockIdx.x;
     const uint32_t b = a.blk_map ? a.blk_map[blockIdx.y] : blockIdx.y;
     const uint32_t c0 = strip * sd;
     const uint32_t width = min(sd, Td - c0);
-    const uint32_t tid = threadIdx.x, nthr = blockDim.x;
+    const uint32_t tid = threadIdx.x, nthr = NW * 64;
     const uint32_t K = a.p.K;
     const uint32_t nebw = a.erased_off ? (K + 31) / 32 : 0;
-    uint32_t* ebits = lds + a.n_slots * sd;
+    uint32_t* tup = lds + a.n_slots * sd;          // OUT_BATCH x 6
+    uint32_t* ebits = tup + OUT_BATCH * 6;
 
-    for (uint32_t i = tid; i < a.n_slots * sd + nebw; i += nthr) lds[i] = 0;
+    // stream pages: prefetch the first two before the prologue
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t lane = tid & 63u;
+    const uint32_t* ws = a.wstream;
+    uint32_t page = __builtin_amdgcn_readfirstlane(a.wave_off[wave]);  // word offset of current page
+    uint32_t q0 = ws[page + lane];
+    uint32_t qn = ws[page + 64 + lane];
+
+    {   // zero the slot image (16-byte stores) and the bitmap
+        const uint32_t nw4 = (a.n_slots * sd) >> 2;
+        uint4* l4 = reinterpret_cast<uint4*>(lds);
+        for (uint32_t i = tid; i < nw4; i += nthr) l4[i] = make_uint4(0, 0, 0, 0);
+        for (uint32_t i = (nw4 << 2) + tid; i < a.n_slots * sd; i += nthr) lds[i] = 0;
+        for (uint32_t i = tid; i < nebw; i += nthr) ebits[i] = 0;
+    }
     __syncthreads();
     if (nebw) {
         for (uint32_t i = a.erased_off[b] + tid; i < a.erased_off[b + 1]; i += nthr) {
@@ -128,101 +158,192 @@ __global__ void __launch_bounds__(256) k_encode(EncArgs a) {
         }
         __syncthreads();
     }
+    const uint32_t half = lane >> 5, hl = lane & 31u;
+    const uint32_t grp = tid >> 5, ngrp = nthr >> 5;
+    const uint32_t hlc = min(hl, sd - 1);  // lanes past the strip read a valid column, never write
+    const bool live = hl < sd;
+    const bool inb = hl < width;
     const uint8_t* blk = a.src + (size_t)b * a.src_stride;
-    for (uint32_t i = tid; i < K * sd; i += nthr) {
-        const uint32_t row = i / sd, c = i - row * sd;
-        const bool er = nebw && ((ebits[row >> 5] >> (row & 31)) & 1u);
-        if (c < width && !er)
-            lds[(uint32_t)a.load_slot[row] * sd + c] =
-                *reinterpret_cast<const uint32_t*>(blk + (size_t)row * T + (size_t)(c0 + c) * 4);
+    const uint8_t* gcol = blk + (size_t)(c0 + hlc) * 4;
+    auto erased_row = [&](uint32_t r) -> bool { return nebw && ((ebits[r >> 5] >> (r & 31)) & 1u); };
+    {   // source strip -> slots: one 32-lane group per row, 4 rows in flight per group
+        uint32_t r = grp;
+        for (; r + 3 * ngrp < K; r += 4 * ngrp) {
+            uint32_t v[4], s[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t row = r + u * ngrp;
+                v[u] = inb ? *reinterpret_cast<const uint32_t*>(gcol + (size_t)row * T) : 0u;
+                s[u] = a.load_slot[row];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (inb && !erased_row(r + u * ngrp)) lds[s[u] * sd + hl] = v[u];
+        }
+        for (; r < K; r += ngrp)
+            if (inb && !erased_row(r)) lds[(uint32_t)a.load_slot[r] * sd + hl] = *reinterpret_cast<const uint32_t*>(gcol + (size_t)r * T);
     }
     __syncthreads();
 
-    const uint32_t grp = tid / GS, lane = tid % GS, ngrp = nthr / GS;
-    const bool live = lane < sd;
-    const bool inb = lane < width;
-    const uint8_t* gcol = blk + (size_t)(c0 + lane) * 4;
     auto gload = [&](uint32_t isi) -> uint32_t {
-        if (!inb || isi >= K) return 0u;
-        if (nebw && ((ebits[isi >> 5] >> (isi & 31)) & 1u)) return 0u;
+        if (!inb || isi >= K || erased_row(isi)) return 0u;
         return *reinterpret_cast<const uint32_t*>(gcol + (size_t)isi * T);
     };
+    uint32_t pos = 0;  // word index within the current page (wave-uniform)
+    auto fetch = [&]() -> uint32_t { return __builtin_amdgcn_readlane(q0, pos++); };
+    auto pick = [&](uint32_t w) -> uint32_t { return half ? (w >> 16) : (w & 0xFFFFu); };
+    uint32_t ht = 0;  // Horner running value (kept across continuation pieces)
 
     for (uint32_t lv = 0; lv < a.n_levels; ++lv) {
-        const uint32_t s1 = a.level_start[lv + 1];
-        for (uint32_t s = a.level_start[lv] + grp; s < s1; s += ngrp) {
-            if (!live) continue;
-            const uint32_t* w = a.words + a.stmt_off[s];
-            const uint32_t w0 = w[0];
-            const uint32_t dst = w0 & 0xFFFFu, ns = (w0 >> 16) & 0xFFFu, ty = (w0 >> 28) & 7u;
-            uint32_t* D = lds + dst * sd + lane;
-            if (ty == ST_XOR_) {
-                uint32_t v = (w0 >> 31) ? *D : 0u;
-                for (uint32_t k = 0; k < ns; ++k) {
-                    const uint32_t sw = w[1 + k];
-                    v ^= (sw >> 31) ? gload(sw & 0xFFFFFFu) : lds[(sw & 0xFFFFu) * sd + lane];
+        for (;;) {  // segments of this level
+            const uint32_t nops = fetch();
+            for (uint32_t op = 0; op < nops; ++op) {
+                const uint32_t hdr = fetch();
+                const uint32_t ty = hdr & 7u, n = hdr >> 16;
+                const uint32_t dst = pick(fetch());
+                uint32_t gi = 0xFFFFFFFFu;
+                if (hdr & 32u) {
+                    const uint32_t ga = fetch(), gb = fetch();
+                    gi = half ? gb : ga;
                 }
-                *D = v;
-            } else if (ty == ST_MUL_) {
-                uint32_t v = (w0 >> 31) ? *D : 0u;
-                for (uint32_t k = 0; k < ns; ++k) {
-                    const uint32_t sw = w[1 + k];
-                    const uint32_t x = (sw >> 31) ? gload(sw & 0xFFFFFFu) : lds[(sw & 0xFFFFu) * sd + lane];
-                    v ^= gfmul4(x, (sw >> 16) & 0xFFu);
-                }
-                *D = v;
-            } else if (ty == ST_SCALE_) {
-                *D = gfmul4(*D, w[1]);
-            } else if (ty == ST_HORNER_) {
-                // HDPC chunk: t = alpha*t ^ y_j over the chunk; partial[h] ^= MT[h][j]*t;
-                // finally partial[h] ^= tau_h * t (contribution of the tail of MT*Gamma).
-                const uint32_t H = a.p.H;
-                for (uint32_t h = 0; h < H; ++h) D[h * sd] = 0u;
-                uint32_t t = 0;
-                for (uint32_t j = 0; j < ns; ++j) {
-                    const uint32_t e = w[1 + j];
-                    const uint32_t sl = e & 0xFFFFu;
-                    t = xtime4(t) ^ (sl != SLOT_NONE_ ? lds[sl * sd + lane] : 0u);
-                    if ((e >> 26) & 1u) {
-                        for (uint32_t h = 0; h < H; ++h) D[h * sd] ^= gfmul4(t, alpha_pow(h));
-                    } else {
-                        D[((e >> 16) & 31u) * sd] ^= t;
-                        D[((e >> 21) & 31u) * sd] ^= t;
+                const bool acc = half ? ((hdr >> 4) & 1u) : ((hdr >> 3) & 1u);
+                uint32_t* D = lds + dst * sd + hlc;
+                if (ty == ST_XOR_) {
+                    uint32_t v = acc ? *D : 0u;
+                    if (gi != 0xFFFFFFFFu) v ^= gload(gi);
+                    uint32_t k = 0;
+                    for (; k + 4 <= n; k += 4) {
+                        const uint32_t s0 = pick(fetch()), s1 = pick(fetch()), s2 = pick(fetch()), s3 = pick(fetch());
+                        const uint32_t x0 = lds[s0 * sd + hlc], x1 = lds[s1 * sd + hlc];
+                        const uint32_t x2 = lds[s2 * sd + hlc], x3 = lds[s3 * sd + hlc];
+                        v ^= (x0 ^ x1) ^ (x2 ^ x3);
+                    }
+                    for (; k < n; ++k) v ^= lds[pick(fetch()) * sd + hlc];
+                    if (live) *D = v;
+                } else if (ty == ST_MUL_) {
+                    uint32_t v = acc ? *D : 0u;
+                    for (uint32_t k = 0; k < n; ++k) {
+                        const uint32_t s = pick(fetch());
+                        const uint32_t cw = fetch();
+                        const uint32_t c = half ? ((cw >> 8) & 0xFFu) : (cw & 0xFFu);
+                        v ^= gfmul4(lds[s * sd + hlc], c);
+                    }
+                    if (live) *D = v;
+                } else if (ty == ST_SCALE_) {
+                    const uint32_t cw = fetch();
+                    const uint32_t c = half ? ((cw >> 8) & 0xFFu) : (cw & 0xFFu);
+                    const uint32_t v = gfmul4(*D, c);
+                    if (live) *D = v;
+                } else if (ty == ST_HORNER_) {
+                    // HDPC chunk: t = alpha*t ^ y_j; partial[h] ^= MT[h][j]*t; at the end
+                    // partial[h] ^= tau_h * t (contribution of the tail of MT*Gamma).
+                    const uint32_t H = a.p.H;
+                    if (hdr & 64u) {
+                        ht = 0;
+                        if (live)
+                            for (uint32_t h = 0; h < H; ++h) D[h * sd] = 0u;
+                    }
+                    for (uint32_t j = 0; j < n; ++j) {
+                        const uint32_t ea = fetch(), eb = fetch();
+                        const uint32_t e = half ? eb : ea;
+                        const uint32_t sl = e & 0xFFFFu;
+                        ht = xtime4(ht) ^ (sl != SLOT_NONE_ ? lds[sl * sd + hlc] : 0u);
+                        if (live) {
+                            if ((e >> 26) & 1u) {
+                                for (uint32_t h = 0; h < H; ++h) D[h * sd] ^= gfmul4(ht, alpha_pow(h));
+                            } else {
+                                D[((e >> 16) & 31u) * sd] ^= ht;
+                                D[((e >> 21) & 31u) * sd] ^= ht;
+                            }
+                        }
+                    }
+                    if (hdr & 128u) {
+                        const uint32_t nt = (H + 3) / 4;
+                        uint32_t ta0 = fetch(), ta1 = nt > 1 ? fetch() : 0u, ta2 = nt > 2 ? fetch() : 0u, ta3 = nt > 3 ? fetch() : 0u;
+                        uint32_t tb0 = fetch(), tb1 = nt > 1 ? fetch() : 0u, tb2 = nt > 2 ? fetch() : 0u, tb3 = nt > 3 ? fetch() : 0u;
+                        const uint32_t t0 = half ? tb0 : ta0, t1 = half ? tb1 : ta1, t2 = half ? tb2 : ta2, t3 = half ? tb3 : ta3;
+                        if (live)
+                            for (uint32_t h = 0; h < H; ++h) {
+                                const uint32_t tw = (h < 4) ? t0 : (h < 8) ? t1 : (h < 12) ? t2 : t3;
+                                D[h * sd] ^= gfmul4(ht, (tw >> (8 * (h & 3))) & 0xFFu);
+                            }
                     }
                 }
-                for (uint32_t h = 0; h < H; ++h) {
-                    const uint32_t tau = (w[1 + ns + (h >> 2)] >> (8 * (h & 3))) & 0xFFu;
-                    D[h * sd] ^= gfmul4(t, tau);
-                }
             }
+            const uint32_t nx = fetch();
+            if (nx & 2u) {  // next segment on the next page (prefetched at the previous switch)
+                q0 = qn;
+                page += 64;
+                qn = ws[page + 64 + lane];
+                pos = 0;
+            }
+            if (nx & 1u) break;
         }
         __syncthreads();
     }
 
-    // ---- outputs: repair symbols (encodeGen) or syndromes (decode) ----
+    // ---- outputs: repair symbols (encodeGen, RQ/params.go:162-182) or syndromes (decode) ----
     if (a.out) {
         uint32_t o0 = 0, o1 = a.n_out;
         if (a.out_off) { o0 = a.out_off[b]; o1 = a.out_off[b + 1]; }
-        for (uint32_t o = o0 + grp; o < o1; o += ngrp) {
-            const uint32_t esi = a.out_esi[o];
-            uint32_t v = 0;
-            if (esi < K) {
-                v = live ? gload(esi) : 0u;
-            } else if (live) {
-                d_for_cols(a.p, esi + a.p.Kp - K, [&](uint32_t c) { v ^= lds[(uint32_t)a.col_slot[c] * sd + lane]; });
+        const DevParams p = a.p;
+        for (uint32_t ob = o0; ob < o1; ob += OUT_BATCH) {
+            const uint32_t on = min(OUT_BATCH, o1 - ob);
+            if (tid < on) {  // one thread per output: the tuple of its ISI
+                const uint32_t esi = a.out_esi[ob + tid];
+                uint32_t* t6 = tup + tid * 6;
+                if (esi < K) {
+                    t6[0] = 0xFFFFFFFFu; t6[1] = esi;
+                } else {
+                    const uint32_t X = esi + p.Kp - K;
+                    uint32_t A = 53591u + 997u * p.J;
+                    if ((A & 1u) == 0) ++A;
+                    const uint32_t y = 10267u * (p.J + 1u) + X * A;
+                    t6[0] = d_degree(d_rand(y, 0, 1u << 20), p.W);
+                    t6[1] = 1 + d_rand(y, 1, p.W - 1);
+                    t6[2] = d_rand(y, 2, p.W);
+                    t6[3] = t6[0] < 4 ? 2 + d_rand(X, 3, 2) : 2;
+                    t6[4] = 1 + d_rand(X, 4, p.P1 - 1);
+                    t6[5] = d_rand(X, 5, p.P1);
+                }
             }
-            const size_t off = a.out_off ? (size_t)o * T : (size_t)b * a.out_stride + (size_t)(o - o0) * T;
-            if (inb) {
-                if (a.xor_in) v ^= *reinterpret_cast<const uint32_t*>(a.xor_in + off + (size_t)(c0 + lane) * 4);
-                *reinterpret_cast<uint32_t*>(a.out + off + (size_t)(c0 + lane) * 4) = v;
+            __syncthreads();
+            for (uint32_t o = grp; o < on; o += ngrp) {
+                const uint32_t* t6 = tup + o * 6;
+                uint32_t v = 0;
+                if (t6[0] == 0xFFFFFFFFu) {
+                    v = gload(t6[1]);
+                } else {
+                    const uint32_t d = t6[0], aa = t6[1], d1 = t6[3], a1 = t6[4];
+                    uint32_t bb = t6[2], b1 = t6[5];
+                    v = lds[(uint32_t)a.col_slot[bb] * sd + hlc];
+                    for (uint32_t j = 1; j < d; ++j) {
+                        bb += aa; if (bb >= p.W) bb -= p.W;
+                        v ^= lds[(uint32_t)a.col_slot[bb] * sd + hlc];
+                    }
+                    while (b1 >= p.P) { b1 += a1; if (b1 >= p.P1) b1 -= p.P1; }
+                    v ^= lds[(uint32_t)a.col_slot[p.W + b1] * sd + hlc];
+                    for (uint32_t j = 1; j < d1; ++j) {
+                        b1 += a1; if (b1 >= p.P1) b1 -= p.P1;
+                        while (b1 >= p.P) { b1 += a1; if (b1 >= p.P1) b1 -= p.P1; }
+                        v ^= lds[(uint32_t)a.col_slot[p.W + b1] * sd + hlc];
+                    }
+                }
+                const uint32_t og = ob + o;
+                const size_t off = a.out_off ? (size_t)og * T : (size_t)b * a.out_stride + (size_t)(og - o0) * T;
+                if (inb) {
+                    if (a.xor_in) v ^= *reinterpret_cast<const uint32_t*>(a.xor_in + off + (size_t)(c0 + hl) * 4);
+                    *reinterpret_cast<uint32_t*>(a.out + off + (size_t)(c0 + hl) * 4) = v;
+                }
             }
+            __syncthreads();
         }
     }
     if (a.c_out) {
         for (uint32_t c = grp; c < a.p.L; c += ngrp)
             if (inb)
-                *reinterpret_cast<uint32_t*>(a.c_out + (size_t)b * a.c_stride + (size_t)c * T + (size_t)(c0 + lane) * 4) =
-                    lds[(uint32_t)a.col_slot[c] * sd + lane];
+                *reinterpret_cast<uint32_t*>(a.c_out + (size_t)b * a.c_stride + (size_t)c * T + (size_t)(c0 + hl) * 4) =
+                    lds[(uint32_t)a.col_slot[c] * sd + hlc];
     }
 }
 
@@ -371,28 +492,20 @@ int launch_gather(const DevParams& p, const uint8_t* C, uint32_t T, const uint32
     return (int)hipGetLastError();
 }
 
-int launch_encode(const EncArgs& a, uint32_t n_strips, uint32_t n_blocks, uint32_t group, void* stream) {
+constexpr int ENC_WAVES = 8;
+
+int launch_encode(const EncArgs& a, uint32_t n_strips, uint32_t n_blocks, uint32_t /*group*/, void* stream) {
     const uint32_t nebw = a.erased_off ? (a.p.K + 31) / 32 : 0;
-    const size_t lds = ((size_t)a.n_slots * a.sd + nebw) * 4;
-    dim3 grid(n_strips, n_blocks), block(256);
-    hipStream_t s = (hipStream_t)stream;
-    static bool attr_set = false;  // allow the full 160 KiB of LDS for every instantiation
+    const size_t lds = ((size_t)a.n_slots * a.sd + OUT_BATCH * 6 + nebw) * 4;
+    if (a.n_waves != ENC_WAVES || a.sd > 32 || lds > 160 * 1024) return (int)hipErrorInvalidValue;
+    static bool attr_set = false;  // allow the full 160 KiB of LDS
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)k_encode<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute((const void*)k_encode<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute((const void*)k_encode<32>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute((const void*)k_encode<64>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_encode<ENC_WAVES>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         (void)hipFuncSetAttribute((const void*)k_solve, hipFuncAttributeMaxDynamicSharedMemorySize, 158 * 1024);
         (void)hipFuncSetAttribute((const void*)k_apply, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_set = true;
     }
-    switch (group) {
-        case 8: hipLaunchKernelGGL(k_encode<8>, grid, block, lds, s, a); break;
-        case 16: hipLaunchKernelGGL(k_encode<16>, grid, block, lds, s, a); break;
-        case 32: hipLaunchKernelGGL(k_encode<32>, grid, block, lds, s, a); break;
-        case 64: hipLaunchKernelGGL(k_encode<64>, grid, block, lds, s, a); break;
-        default: return (int)hipErrorInvalidValue;
-    }
+    hipLaunchKernelGGL(k_encode<ENC_WAVES>, dim3(n_strips, n_blocks), dim3(ENC_WAVES * 64), lds, (hipStream_t)stream, a);
     return (int)hipGetLastError();
 }
 

@@ -78,6 +78,26 @@ struct PlanOptions {
 };
 bool compile_encode_plan(const Params& p, Plan* out, std::string* err, const PlanOptions& opt = PlanOptions());
 
+// ---------------------------------------------------------------------------------------
+// Wave program: the level-scheduled statements re-packed for execution by whole wavefronts.
+// Each op runs two statements of the same type side by side (lanes 0-31: A, 32-63: B), so every
+// descriptor word is wave-uniform.  Streams are 64-word pages of segments (rq_wave.cpp):
+//   segment   : count, ops..., NEXT (bit0: barrier = end of level, bit1: next segment on next page)
+//   op header : type(3) | accA<<3 | accB<<4 | hasG<<5 | hornerStart<<6 | hornerFinish<<7 | n<<16
+//   dst word  : dstA | dstB<<16
+//   [hasG]    : isiA, isiB (0xFFFFFFFF = none) -- source rows re-read from global memory
+//   XOR       : n words srcA | srcB<<16
+//   MUL       : n x (srcA | srcB<<16, coefA | coefB<<8)
+//   SCALE     : 1 word coefA | coefB<<8 (n = 0)
+//   HORNER    : n column pairs (wordA, wordB) as in Stmt; [finish] ceil(H/4) tau words of A, of B
+struct WaveProgram {
+    uint32_t n_waves = 0, n_levels = 0, n_slots = 0, zero_slot = 0, trash_slot = 0;
+    std::vector<uint32_t> words;      // all streams, padded for chunk prefetch
+    std::vector<uint32_t> wave_off;   // [n_waves] stream start
+    uint32_t max_stream = 0;          // longest stream (words)
+};
+bool build_wave_program(const Plan& plan, uint32_t n_waves, WaveProgram* out, std::string* err);
+
 // Encode the output (LT gather) statements for a list of ISIs: per output one word
 // nsrc(8) followed by nsrc slots (C columns mapped through col_slot).  Appended to *words;
 // returns the offset of each output in *offs.

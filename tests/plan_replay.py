@@ -85,3 +85,90 @@ def replay(plan, src_rows, K, H, erased=()):
             raise ValueError("bad statement type %d" % ty)
     C32 = slots[plan["col_slot"].astype(np.int64)]
     return C32.view(np.uint8).reshape(L, T)
+
+
+def replay_waves(wave, plan, src_rows, K, H):
+    """Emulate k_encode's wave streams (paged segments, paired statements A|B, Horner pieces)."""
+    Kp, L = plan["Kp"], plan["L"]
+    T = src_rows.shape[1]
+    Td = T // 4
+    words = wave["words"]
+    src32 = np.ascontiguousarray(src_rows).view(np.uint32).reshape(Kp, Td).copy()
+    src32[K:] = 0
+    slots = np.zeros((wave["n_slots"], Td), np.uint32)
+    for i in range(K):
+        slots[plan["load_slot"][i]] = src32[i]
+    nw = wave["n_waves"]
+    page = [int(o) for o in wave["wave_off"]]
+    pos = [0] * nw
+    ht = [[np.zeros(Td, np.uint32), np.zeros(Td, np.uint32)] for _ in range(nw)]
+    for _lv in range(wave["n_levels"]):
+        for w in range(nw):
+            def F():
+                assert pos[w] < 64, "segment crosses a page"
+                v = int(words[page[w] + pos[w]])
+                pos[w] += 1
+                return v
+            while True:
+                nops = F()
+                for _ in range(nops):
+                    hdr = F()
+                    ty, n = hdr & 7, hdr >> 16
+                    dd = F()
+                    g = (F(), F()) if hdr & 32 else (0xFFFFFFFF, 0xFFFFFFFF)
+                    if ty == ST_XOR:
+                        body = [F() for _ in range(n)]
+                    elif ty == ST_MUL:
+                        body = [(F(), F()) for _ in range(n)]
+                    elif ty == ST_SCALE:
+                        body = F()
+                    else:
+                        body = [(F(), F()) for _ in range(n)]
+                        nt = (H + 3) // 4
+                        taus = ([F() for _ in range(nt)], [F() for _ in range(nt)]) if hdr & 128 else None
+                    for half in (0, 1):
+                        dst = (dd >> 16) if half else (dd & 0xFFFF)
+                        acc = (hdr >> (4 if half else 3)) & 1
+                        pk = (lambda x: x >> 16) if half else (lambda x: x & 0xFFFF)
+                        if ty == ST_XOR:
+                            v = slots[dst].copy() if acc else np.zeros(Td, np.uint32)
+                            gi = g[half]
+                            if gi != 0xFFFFFFFF and gi < K:
+                                v ^= src32[gi]
+                            for x in body:
+                                v ^= slots[pk(x)]
+                            slots[dst] = v
+                        elif ty == ST_MUL:
+                            v = slots[dst].copy() if acc else np.zeros(Td, np.uint32)
+                            for x, c in body:
+                                v ^= gfmul4(slots[pk(x)], (c >> 8) & 0xFF if half else c & 0xFF)
+                            slots[dst] = v
+                        elif ty == ST_SCALE:
+                            slots[dst] = gfmul4(slots[dst], (body >> 8) & 0xFF if half else body & 0xFF)
+                        else:
+                            if hdr & 64:
+                                ht[w][half] = np.zeros(Td, np.uint32)
+                                slots[dst:dst + H] = 0
+                            t = ht[w][half]
+                            for ea, eb in body:
+                                e = eb if half else ea
+                                sl = e & 0xFFFF
+                                t = xtime4(t) ^ (slots[sl] if sl != 0xFFFF else 0)
+                                if (e >> 26) & 1:
+                                    for h in range(H):
+                                        slots[dst + h] ^= gfmul4(t, ALPHA_POW[h])
+                                else:
+                                    slots[dst + ((e >> 16) & 31)] ^= t
+                                    slots[dst + ((e >> 21) & 31)] ^= t
+                            ht[w][half] = t
+                            if taus is not None:
+                                tw = taus[half]
+                                for h in range(H):
+                                    slots[dst + h] ^= gfmul4(t, (tw[h // 4] >> (8 * (h & 3))) & 0xFF)
+                nx = F()
+                if nx & 2:
+                    page[w] += 64
+                    pos[w] = 0
+                if nx & 1:
+                    break
+    return slots[plan["col_slot"].astype(np.int64)].view(np.uint8).reshape(L, T)

@@ -50,3 +50,19 @@ def test_plan_op_counts_beat_reference(rq):
 def test_plan_fits_lds(rq, K):
     s = rq.plan_stats(K)
     assert s["n_slots"] * 4 * 8 <= 160 * 1024  # at least an 8-dword strip fits the LDS
+
+
+@pytest.mark.parametrize("K,T", [(5, 16), (64, 8), (256, 8), (1024, 4)])
+def test_wave_streams_match_oracle(rq, oracle, K, T):
+    """The per-wave instruction streams k_encode executes (paired statements, paged segments,
+    split Horner pieces) reproduce the oracle's intermediate symbols."""
+    from tests.plan_replay import replay_waves
+    rng = np.random.default_rng(77 + K)
+    data = rng.integers(0, 256, K * T, dtype=np.uint8)
+    p = rq.params(len(data), T)
+    plan = rq.plan_export(K)
+    wave = rq.wave_export(K)
+    assert wave["words"].size % 64 == 0
+    src = np.zeros((p["Kp"], T), np.uint8)
+    src.reshape(-1)[:len(data)] = data
+    assert np.array_equal(replay_waves(wave, plan, src, p["K"], p["H"]), oracle.encode_C(data, T))
