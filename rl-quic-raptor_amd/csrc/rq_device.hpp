@@ -36,6 +36,8 @@ struct EncArgs {
     const uint8_t* xor_in;     // optional, indexed like out (syndrome: received repair rows)
     uint8_t* c_out;            // optional intermediate symbols: c_out + b*c_stride + c*T
     uint64_t c_stride;
+    unsigned long long* stamp; // diagnostics only: s_memtime per level of workgroup (0,0), or null
+    uint32_t dbg;              // ablation bits (timing experiments only): 1 no source loads, 2 no program, 4 no outputs
 };
 
 struct SolveArgs {

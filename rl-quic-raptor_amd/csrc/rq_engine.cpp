@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -192,6 +193,11 @@ EncArgs base_args(const DevPlan& dp, const Params& p, uint32_t T, uint32_t sd) {
     a.wave_off = dp.wave_off.as<uint32_t>();
     a.n_waves = dp.wp.n_waves;
     a.col_slot = dp.col_slot.as<uint16_t>();
+    static const uint32_t dbg = [] {  // timing ablations only (tools/ablate.py)
+        const char* s = std::getenv("RQHIP_DBG");
+        return s ? (uint32_t)std::strtoul(s, nullptr, 0) : 0u;
+    }();
+    a.dbg = dbg;
     return a;
 }
 
@@ -213,8 +219,26 @@ int encode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, c
     a.out_stride = out_stride;
     a.c_out = static_cast<uint8_t*>(c_out);
     a.c_stride = c_stride;
+    static const char* stamp_file = std::getenv("RQHIP_STAMP_FILE");  // diagnostics only
+    DevBuf stamps;
+    if (stamp_file && stamps.ensure((size_t)a.n_levels * a.n_waves * 16) == RQ_OK) a.stamp = stamps.as<unsigned long long>();
     const int e = launch_encode(a, g.n_strips, n_blocks, g.group, stream);
     if (e) return fail(RQ_ERR_DEVICE, std::string("k_encode launch: ") + hipGetErrorString((hipError_t)e));
+    if (a.stamp) {
+        std::vector<unsigned long long> h((size_t)a.n_levels * a.n_waves * 2);
+        if (hipStreamSynchronize((hipStream_t)stream) == hipSuccess &&
+            hipMemcpy(h.data(), a.stamp, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+            if (FILE* f = std::fopen(stamp_file, "w")) {
+                for (uint32_t l = 0; l < a.n_levels; ++l) {
+                    std::fprintf(f, "%u", l);
+                    for (uint32_t w = 0; w < a.n_waves; ++w)
+                        std::fprintf(f, " %llu:%llu", h[((size_t)l * a.n_waves + w) * 2], h[((size_t)l * a.n_waves + w) * 2 + 1]);
+                    std::fprintf(f, "\n");
+                }
+                std::fclose(f);
+            }
+        }
+    }
     return RQ_OK;
 }
 
@@ -259,8 +283,8 @@ int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, v
         const uint32_t e = n_erased[b], nr = n_repair[b];
         if ((p.K - e) + nr < p.K) { status[b] = RQ_ERR_NOT_ENOUGH; continue; }
         if (e == 0) { status[b] = 1; continue; }
-        const size_t need = (size_t)nr * (e + nr);
-        if (e > MAX_E || nr > 1024 || need > 150 * 1024) { status[b] = RQ_ERR_UNSUPPORTED; continue; }
+        const size_t need = (((size_t)nr * (e + nr) + 15) & ~size_t(15)) + (size_t)nr * 24;  // [M | I] + tuples
+        if (e > MAX_E || nr > 255 || need > 150 * 1024) { status[b] = RQ_ERR_UNSUPPORTED; continue; }
         status[b] = -100;  // pending
         blk_map.push_back(b);
         max_lds_solve = std::max(max_lds_solve, need);

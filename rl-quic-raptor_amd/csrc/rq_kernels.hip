@@ -42,15 +42,19 @@ int upload_tables() {
 // ------------------------------ GF(256) on packed dwords ------------------------------------
 __device__ __forceinline__ uint32_t xtime4(uint32_t x) {
     const uint32_t hi = (x >> 7) & 0x01010101u;
-    return ((x & 0x7F7F7F7Fu) << 1) ^ (hi * 0x1Du);
+    const uint32_t mask = (hi << 8) - hi;  // 0x00 / 0xFF per byte (no multiply)
+    return ((x & 0x7F7F7F7Fu) << 1) ^ (mask & 0x1D1D1D1Du);
 }
-// x * c in GF(256) for each of the 4 bytes of x (poly 0x11D).
+// x * c in GF(256) for each of the 4 bytes of x (poly 0x11D): XOR over the bits b of x of
+// (c * 2^b) -- eight independent terms (short dependency chain) instead of a doubling chain on x.
 __device__ __forceinline__ uint32_t gfmul4(uint32_t x, uint32_t c) {
-    uint32_t r = 0;
+    uint32_t r = 0, kb = c & 0xFFu;
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
-        r ^= (c & (1u << b)) ? x : 0u;
-        x = xtime4(x);
+        const uint32_t m = (x >> b) & 0x01010101u;
+        const uint32_t mask = (m << 8) - m;            // 0x00 / 0xFF per byte
+        r ^= mask & (__umul24(kb, 0x010101u) | (kb << 24));  // kb replicated to 4 bytes
+        kb = ((kb << 1) ^ ((kb & 0x80u) ? 0x11Du : 0u)) & 0xFFu;
     }
     return r;
 }
@@ -140,8 +144,10 @@ __global__ void __launch_bounds__(NW * 64) k_encode(EncArgs a) {
     const uint32_t lane = tid & 63u;
     const uint32_t* ws = a.wstream;
     uint32_t page = __builtin_amdgcn_readfirstlane(a.wave_off[wave]);  // word offset of current page
-    uint32_t q0 = ws[page + lane];
-    uint32_t qn = ws[page + 64 + lane];
+    // Two page registers used ping-pong: the segment processor is instantiated once per register
+    // (qa current / qb current), so a refill load always targets the idle register directly and
+    // no register copy of an in-flight load exists (which would force vmcnt(0) on every page).
+    uint32_t qa = ws[page + lane], qb = ws[page + 64 + lane];
 
     {   // zero the slot image (16-byte stores) and the bitmap
         const uint32_t nw4 = (a.n_slots * sd) >> 2;
@@ -166,7 +172,7 @@ __global__ void __launch_bounds__(NW * 64) k_encode(EncArgs a) {
     const uint8_t* blk = a.src + (size_t)b * a.src_stride;
     const uint8_t* gcol = blk + (size_t)(c0 + hlc) * 4;
     auto erased_row = [&](uint32_t r) -> bool { return nebw && ((ebits[r >> 5] >> (r & 31)) & 1u); };
-    {   // source strip -> slots: one 32-lane group per row, 4 rows in flight per group
+    if (!(a.dbg & 1u)) {   // source strip -> slots: one 32-lane group per row, 4 rows in flight per group
         uint32_t r = grp;
         for (; r + 3 * ngrp < K; r += 4 * ngrp) {
             uint32_t v[4], s[4];
@@ -189,101 +195,174 @@ __global__ void __launch_bounds__(NW * 64) k_encode(EncArgs a) {
         if (!inb || isi >= K || erased_row(isi)) return 0u;
         return *reinterpret_cast<const uint32_t*>(gcol + (size_t)isi * T);
     };
-    uint32_t pos = 0;  // word index within the current page (wave-uniform)
-    auto fetch = [&]() -> uint32_t { return __builtin_amdgcn_readlane(q0, pos++); };
+    // Descriptor words: readlane from the current page; the cursor is wave-uniform.
+    uint32_t pos = 0;
     auto pick = [&](uint32_t w) -> uint32_t { return half ? (w >> 16) : (w & 0xFFFFu); };
+    // Lanes past the strip never write real slots: they write the trash slot instead, so the
+    // statement loop has no divergent control flow.
+    uint32_t* const trash = lds + (a.n_slots - 1) * sd;
+    const uint32_t zero_slot = a.n_slots - 1 - a.p.H;  // WaveProgram: zero slot, then H trash slots
     uint32_t ht = 0;  // Horner running value (kept across continuation pieces)
 
-    for (uint32_t lv = 0; lv < a.n_levels; ++lv) {
-        for (;;) {  // segments of this level
-            const uint32_t nops = fetch();
-            for (uint32_t op = 0; op < nops; ++op) {
-                const uint32_t hdr = fetch();
-                const uint32_t ty = hdr & 7u, n = hdr >> 16;
-                const uint32_t dst = pick(fetch());
-                uint32_t gi = 0xFFFFFFFFu;
-                if (hdr & 32u) {
-                    const uint32_t ga = fetch(), gb = fetch();
-                    gi = half ? gb : ga;
+    const uint32_t n_levels = (a.dbg & 2u) ? 0u : a.n_levels;
+    // diagnostics: per level and wave, [cycles working, cycles at the barrier] of workgroup (0,0)
+    const bool stamping = a.stamp && blockIdx.x == 0 && blockIdx.y == 0 && lane == 0;
+    unsigned long long t_lv = stamping ? __builtin_amdgcn_s_memtime() : 0ull;
+    // One segment: its ops, then the NEXT word (bit0 barrier, bit1 page switch).
+    auto segment = [&](const uint32_t cur) -> uint32_t {
+        auto fetch = [&]() -> uint32_t {
+            const uint32_t w = __builtin_amdgcn_readlane(cur, __builtin_amdgcn_readfirstlane(pos));
+            ++pos;
+            return w;
+        };
+        const uint32_t nops = fetch();
+        for (uint32_t op = 0; op < nops; ++op) {
+            const uint32_t hdr = fetch();
+            const uint32_t ty = hdr & 7u, n = hdr >> 16;
+            const uint32_t dst = pick(fetch());
+            uint32_t gi = 0xFFFFFFFFu;
+            if (hdr & 32u) {
+                const uint32_t ga = fetch(), gb = fetch();
+                gi = half ? gb : ga;
+            }
+            const uint32_t accm = ((hdr >> (half ? 4 : 3)) & 1u) ? 0xFFFFFFFFu : 0u;
+            uint32_t* D = lds + __umul24(dst, sd) + hlc;
+            uint32_t* Dw = live ? D : trash;
+            if (ty == ST_XOR_) {
+                uint32_t v = *D & accm;
+                if (hdr & 32u) v ^= gload(gi == 0xFFFFFFFFu ? K : gi);
+                uint32_t k = 0;
+                for (; k + 4 <= n; k += 4) {
+                    const uint32_t s0 = pick(fetch()), s1 = pick(fetch()), s2 = pick(fetch()), s3 = pick(fetch());
+                    const uint32_t x0 = lds[__umul24(s0, sd) + hlc], x1 = lds[__umul24(s1, sd) + hlc];
+                    const uint32_t x2 = lds[__umul24(s2, sd) + hlc], x3 = lds[__umul24(s3, sd) + hlc];
+                    v ^= (x0 ^ x1) ^ (x2 ^ x3);
                 }
-                const bool acc = half ? ((hdr >> 4) & 1u) : ((hdr >> 3) & 1u);
-                uint32_t* D = lds + dst * sd + hlc;
-                if (ty == ST_XOR_) {
-                    uint32_t v = acc ? *D : 0u;
-                    if (gi != 0xFFFFFFFFu) v ^= gload(gi);
-                    uint32_t k = 0;
-                    for (; k + 4 <= n; k += 4) {
-                        const uint32_t s0 = pick(fetch()), s1 = pick(fetch()), s2 = pick(fetch()), s3 = pick(fetch());
-                        const uint32_t x0 = lds[s0 * sd + hlc], x1 = lds[s1 * sd + hlc];
-                        const uint32_t x2 = lds[s2 * sd + hlc], x3 = lds[s3 * sd + hlc];
-                        v ^= (x0 ^ x1) ^ (x2 ^ x3);
-                    }
-                    for (; k < n; ++k) v ^= lds[pick(fetch()) * sd + hlc];
-                    if (live) *D = v;
-                } else if (ty == ST_MUL_) {
-                    uint32_t v = acc ? *D : 0u;
-                    for (uint32_t k = 0; k < n; ++k) {
-                        const uint32_t s = pick(fetch());
-                        const uint32_t cw = fetch();
-                        const uint32_t c = half ? ((cw >> 8) & 0xFFu) : (cw & 0xFFu);
-                        v ^= gfmul4(lds[s * sd + hlc], c);
-                    }
-                    if (live) *D = v;
-                } else if (ty == ST_SCALE_) {
+                for (; k < n; ++k) v ^= lds[__umul24(pick(fetch()), sd) + hlc];
+                *Dw = v;
+            } else if (ty == ST_MUL_) {
+                uint32_t v = *D & accm;
+                uint32_t k = 0;
+                for (; k + 2 <= n; k += 2) {
+                    const uint32_t sa = pick(fetch()), ca = fetch(), sb = pick(fetch()), cb = fetch();
+                    const uint32_t xa = lds[__umul24(sa, sd) + hlc], xb = lds[__umul24(sb, sd) + hlc];
+                    v ^= gfmul4(xa, half ? (ca >> 8) : ca) ^ gfmul4(xb, half ? (cb >> 8) : cb);
+                }
+                for (; k < n; ++k) {
+                    const uint32_t s = pick(fetch());
                     const uint32_t cw = fetch();
-                    const uint32_t c = half ? ((cw >> 8) & 0xFFu) : (cw & 0xFFu);
-                    const uint32_t v = gfmul4(*D, c);
-                    if (live) *D = v;
-                } else if (ty == ST_HORNER_) {
-                    // HDPC chunk: t = alpha*t ^ y_j; partial[h] ^= MT[h][j]*t; at the end
-                    // partial[h] ^= tau_h * t (contribution of the tail of MT*Gamma).
-                    const uint32_t H = a.p.H;
-                    if (hdr & 64u) {
-                        ht = 0;
-                        if (live)
-                            for (uint32_t h = 0; h < H; ++h) D[h * sd] = 0u;
-                    }
-                    for (uint32_t j = 0; j < n; ++j) {
+                    v ^= gfmul4(lds[__umul24(s, sd) + hlc], half ? (cw >> 8) : cw);
+                }
+                *Dw = v;
+            } else if (ty == ST_SCALE_) {
+                const uint32_t cw = fetch();
+                *Dw = gfmul4(*D, half ? (cw >> 8) : cw);
+            } else if (ty == ST_HORNER_) {
+                // HDPC chunk: t = alpha*t ^ y_j; partial[h] ^= MT[h][j]*t (fire-and-forget
+                // LDS atomics, no round trip on the chain); finish: partial[h] ^= tau_h * t.
+                const uint32_t H = a.p.H;
+                const uint32_t pstride = live ? sd : 0u;  // non-live lanes hit the trash slot
+                uint32_t* P = live ? D : trash;
+                if (hdr & 64u) {
+                    ht = 0;
+                    for (uint32_t h = 0; h < H; ++h) P[h * pstride] = 0u;
+                }
+                uint32_t j = 0;
+                for (; j + 4 <= n; j += 4) {
+                    uint32_t e[4], y[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
                         const uint32_t ea = fetch(), eb = fetch();
-                        const uint32_t e = half ? eb : ea;
-                        const uint32_t sl = e & 0xFFFFu;
-                        ht = xtime4(ht) ^ (sl != SLOT_NONE_ ? lds[sl * sd + hlc] : 0u);
-                        if (live) {
-                            if ((e >> 26) & 1u) {
-                                for (uint32_t h = 0; h < H; ++h) D[h * sd] ^= gfmul4(ht, alpha_pow(h));
-                            } else {
-                                D[((e >> 16) & 31u) * sd] ^= ht;
-                                D[((e >> 21) & 31u) * sd] ^= ht;
-                            }
+                        e[u] = half ? eb : ea;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const uint32_t sl = e[u] & 0xFFFFu;
+                        y[u] = lds[__umul24(sl != SLOT_NONE_ ? sl : zero_slot, sd) + hlc];  // n_slots-2 = zero slot
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        ht = xtime4(ht) ^ y[u];
+                        if ((e[u] >> 26) & 1u) {
+                            for (uint32_t h = 0; h < H; ++h) __hip_atomic_fetch_xor(P + h * pstride, gfmul4(ht, alpha_pow(h)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        } else {
+                            __hip_atomic_fetch_xor(P + ((e[u] >> 16) & 31u) * pstride, ht, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            __hip_atomic_fetch_xor(P + ((e[u] >> 21) & 31u) * pstride, ht, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         }
                     }
-                    if (hdr & 128u) {
-                        const uint32_t nt = (H + 3) / 4;
-                        uint32_t ta0 = fetch(), ta1 = nt > 1 ? fetch() : 0u, ta2 = nt > 2 ? fetch() : 0u, ta3 = nt > 3 ? fetch() : 0u;
-                        uint32_t tb0 = fetch(), tb1 = nt > 1 ? fetch() : 0u, tb2 = nt > 2 ? fetch() : 0u, tb3 = nt > 3 ? fetch() : 0u;
-                        const uint32_t t0 = half ? tb0 : ta0, t1 = half ? tb1 : ta1, t2 = half ? tb2 : ta2, t3 = half ? tb3 : ta3;
-                        if (live)
-                            for (uint32_t h = 0; h < H; ++h) {
-                                const uint32_t tw = (h < 4) ? t0 : (h < 8) ? t1 : (h < 12) ? t2 : t3;
-                                D[h * sd] ^= gfmul4(ht, (tw >> (8 * (h & 3))) & 0xFFu);
-                            }
+                }
+                for (; j < n; ++j) {
+                    const uint32_t ea = fetch(), eb = fetch();
+                    const uint32_t e = half ? eb : ea;
+                    const uint32_t sl = e & 0xFFFFu;
+                    ht = xtime4(ht) ^ lds[__umul24(sl != SLOT_NONE_ ? sl : zero_slot, sd) + hlc];
+                    if ((e >> 26) & 1u) {
+                        for (uint32_t h = 0; h < H; ++h) __hip_atomic_fetch_xor(P + h * pstride, gfmul4(ht, alpha_pow(h)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    } else {
+                        __hip_atomic_fetch_xor(P + ((e >> 16) & 31u) * pstride, ht, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_fetch_xor(P + ((e >> 21) & 31u) * pstride, ht, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                }
+                if (hdr & 128u) {
+                    const uint32_t nt = (H + 3) / 4;
+                    const uint32_t ta0 = fetch(), ta1 = nt > 1 ? fetch() : 0u, ta2 = nt > 2 ? fetch() : 0u, ta3 = nt > 3 ? fetch() : 0u;
+                    const uint32_t tb0 = fetch(), tb1 = nt > 1 ? fetch() : 0u, tb2 = nt > 2 ? fetch() : 0u, tb3 = nt > 3 ? fetch() : 0u;
+                    const uint32_t t0 = half ? tb0 : ta0, t1 = half ? tb1 : ta1, t2 = half ? tb2 : ta2, t3 = half ? tb3 : ta3;
+                    for (uint32_t h = 0; h < H; ++h) {
+                        const uint32_t tw = (h < 4) ? t0 : (h < 8) ? t1 : (h < 12) ? t2 : t3;
+                        __hip_atomic_fetch_xor(P + h * pstride, gfmul4(ht, tw >> (8 * (h & 3))), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
                 }
             }
-            const uint32_t nx = fetch();
-            if (nx & 2u) {  // next segment on the next page (prefetched at the previous switch)
-                q0 = qn;
-                page += 64;
-                qn = ws[page + 64 + lane];
-                pos = 0;
-            }
-            if (nx & 1u) break;
         }
-        __syncthreads();
+        return fetch();
+    };
+    uint32_t lv = 0;
+    auto after = [&](uint32_t nx) -> bool {  // barrier bookkeeping; true when the program is done
+        if (nx & 1u) {
+            unsigned long long t_w = 0;
+            if (stamping) t_w = __builtin_amdgcn_s_memtime();
+            // Level barrier: only LDS traffic must be complete (lgkmcnt); page and source-row loads
+            // stay in flight (a __syncthreads() would also drain vmcnt).
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            if (stamping) {
+                const unsigned long long t_b = __builtin_amdgcn_s_memtime();
+                a.stamp[(lv * NW + wave) * 2] = t_w - t_lv;
+                a.stamp[(lv * NW + wave) * 2 + 1] = t_b - t_w;
+                t_lv = t_b;
+            }
+            ++lv;
+        }
+        return lv >= n_levels;
+    };
+    // Page refills are issued as inline-asm loads, invisible to the compiler's wait-count pass
+    // (which otherwise drains vmcnt(0) at every segment for loop-carried loads); the page that
+    // becomes current is waited for explicitly at the switch.  VMEM ops retire in order, so the
+    // compiler's own counted waits for its loads stay correct with these extra loads in flight.
+    auto refill = [&](uint32_t& reg) {
+        const uint32_t* p = ws + page + 64 + lane;
+        asm volatile("global_load_dword %0, %1, off" : "=v"(reg) : "v"(p) : "memory");
+    };
+    // Compiler-visible drain of the prologue's page loads (vmcnt(0), lgkm/exp untouched), so the
+    // wait-count pass sees no VMEM pending at the loop header and inserts no wait there.
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    bool done = n_levels == 0;
+    while (!done) {
+        uint32_t nx;
+        do { nx = segment(qa); done = after(nx); } while (!done && !(nx & 2u));
+        if (done) break;
+        page += 64; pos = 0;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // qb (page + 0) has landed
+        refill(qa);                                         // qa <- page + 1
+        do { nx = segment(qb); done = after(nx); } while (!done && !(nx & 2u));
+        if (done) break;
+        page += 64; pos = 0;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        refill(qb);
     }
-
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no asm load outlives the program
     // ---- outputs: repair symbols (encodeGen, RQ/params.go:162-182) or syndromes (decode) ----
-    if (a.out) {
+    if (a.out && !(a.dbg & 4u)) {
         uint32_t o0 = 0, o1 = a.n_out;
         if (a.out_off) { o0 = a.out_off[b]; o1 = a.out_off[b + 1]; }
         const DevParams p = a.p;
@@ -316,17 +395,17 @@ __global__ void __launch_bounds__(NW * 64) k_encode(EncArgs a) {
                 } else {
                     const uint32_t d = t6[0], aa = t6[1], d1 = t6[3], a1 = t6[4];
                     uint32_t bb = t6[2], b1 = t6[5];
-                    v = lds[(uint32_t)a.col_slot[bb] * sd + hlc];
+                    v = lds[__umul24((uint32_t)a.col_slot[bb], sd) + hlc];
                     for (uint32_t j = 1; j < d; ++j) {
                         bb += aa; if (bb >= p.W) bb -= p.W;
-                        v ^= lds[(uint32_t)a.col_slot[bb] * sd + hlc];
+                        v ^= lds[__umul24((uint32_t)a.col_slot[bb], sd) + hlc];
                     }
                     while (b1 >= p.P) { b1 += a1; if (b1 >= p.P1) b1 -= p.P1; }
-                    v ^= lds[(uint32_t)a.col_slot[p.W + b1] * sd + hlc];
+                    v ^= lds[__umul24((uint32_t)a.col_slot[p.W + b1], sd) + hlc];
                     for (uint32_t j = 1; j < d1; ++j) {
                         b1 += a1; if (b1 >= p.P1) b1 -= p.P1;
                         while (b1 >= p.P) { b1 += a1; if (b1 >= p.P1) b1 -= p.P1; }
-                        v ^= lds[(uint32_t)a.col_slot[p.W + b1] * sd + hlc];
+                        v ^= lds[__umul24((uint32_t)a.col_slot[p.W + b1], sd) + hlc];
                     }
                 }
                 const uint32_t og = ob + o;
@@ -355,6 +434,34 @@ __device__ __forceinline__ uint8_t gmul_t(const uint8_t* lg, const uint8_t* ex, 
     return (a && b) ? ex[lg[a] + lg[b]] : (uint8_t)0;
 }
 
+// LT tuple of ISI X into t6[0..5] = {d, a, b, d1, a1, b1} (RQ/params.go:83-112).
+__device__ __forceinline__ void d_tuple6(const DevParams& p, uint32_t X, uint32_t* t6) {
+    uint32_t A = 53591u + 997u * p.J;
+    if ((A & 1u) == 0) ++A;
+    const uint32_t y = 10267u * (p.J + 1u) + X * A;
+    t6[0] = d_degree(d_rand(y, 0, 1u << 20), p.W);
+    t6[1] = 1 + d_rand(y, 1, p.W - 1);
+    t6[2] = d_rand(y, 2, p.W);
+    t6[3] = t6[0] < 4 ? 2 + d_rand(X, 3, 2) : 2;
+    t6[4] = 1 + d_rand(X, 4, p.P1 - 1);
+    t6[5] = d_rand(X, 5, p.P1);
+}
+// Calls f(col) for the columns of a staged tuple (modular steps by add/subtract).
+template <class F>
+__device__ __forceinline__ void d_cols6(const DevParams& p, const uint32_t* t6, F&& f) {
+    const uint32_t d = t6[0], aa = t6[1], d1 = t6[3], a1 = t6[4];
+    uint32_t bb = t6[2], b1 = t6[5];
+    f(bb);
+    for (uint32_t j = 1; j < d; ++j) { bb += aa; if (bb >= p.W) bb -= p.W; f(bb); }
+    while (b1 >= p.P) { b1 += a1; if (b1 >= p.P1) b1 -= p.P1; }
+    f(p.W + b1);
+    for (uint32_t j = 1; j < d1; ++j) {
+        b1 += a1; if (b1 >= p.P1) b1 -= p.P1;
+        while (b1 >= p.P) { b1 += a1; if (b1 >= p.P1) b1 -= p.P1; }
+        f(p.W + b1);
+    }
+}
+
 __global__ void __launch_bounds__(256) k_solve(SolveArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
     __shared__ uint8_t ex[512], lg[256];
@@ -368,6 +475,7 @@ __global__ void __launch_bounds__(256) k_solve(SolveArgs a) {
     const uint32_t* E = a.erased + a.erased_off[b];
     const uint32_t* R = a.rep_esi + a.rep_off[b];
     const uint32_t ws = e + nr;
+    uint32_t* tup = reinterpret_cast<uint32_t*>(sm + ((nr * ws + 15) & ~15u));  // nr x 6 words
     if (tid == 0) {
         uint32_t x = 1;
         for (int i = 0; i < 255; ++i) {
@@ -376,14 +484,17 @@ __global__ void __launch_bounds__(256) k_solve(SolveArgs a) {
         }
         ex[510] = ex[0]; ex[511] = ex[1]; lg[0] = 0;
     }
-    for (uint32_t r = tid; r < nr; r += nthr) rowid[r] = (uint16_t)r;
+    for (uint32_t r = tid; r < nr; r += nthr) {
+        rowid[r] = (uint16_t)r;
+        d_tuple6(a.p, R[r] + a.p.Kp - a.p.K, tup + r * 6);
+    }
     for (uint32_t idx = tid; idx < nr * ws; idx += nthr) sm[idx] = 0;
     __syncthreads();
     for (uint32_t idx = tid; idx < nr * e; idx += nthr) {
         const uint32_t j = idx / e, k = idx - j * e;
         const uint32_t col = E[k];
         uint8_t v = 0;
-        d_for_cols(a.p, R[j] + a.p.Kp - a.p.K, [&](uint32_t c) { v ^= a.cid[(size_t)c * a.cid_stride + col]; });
+        d_cols6(a.p, tup + j * 6, [&](uint32_t c) { v ^= a.cid[(size_t)c * a.cid_stride + col]; });
         sm[j * ws + k] = v;
     }
     for (uint32_t j = tid; j < nr; j += nthr) sm[j * ws + e + j] = 1;
