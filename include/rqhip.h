@@ -115,9 +115,16 @@ int rq_plan_stats(uint32_t K, uint32_t stats[11]);
 int rq_plan_export(uint32_t K, uint32_t sizes[5], uint32_t* level_start, uint32_t* stmt_off,
                    uint32_t* words, uint16_t* load_slot, uint16_t* col_slot);
 
-/* Export the per-wave instruction streams k_encode executes (tests).  sizes[0..3] =
- * {n_words, n_waves, n_levels, n_slots}; wave_off receives n_waves stream offsets. */
-int rq_wave_export(uint32_t K, uint32_t sizes[4], uint32_t* words, uint32_t* wave_off);
+/* Export the per-wave instruction streams k_encode executes (tests).  sd = strip width in
+ * dwords (slot fields become LDS dword offsets slot*sd), or 0 for raw slot indices.
+ * sizes[0..3] = {n_words, n_waves, n_levels, n_slots}; wave_off receives n_waves offsets. */
+int rq_wave_export(uint32_t K, uint32_t sd, uint32_t sizes[4], uint32_t* words, uint32_t* wave_off);
+
+/* Diagnostics: run k_encode on a caller-supplied wave program (host arrays) over n_blocks
+ * synthetic zero blocks of K rows x T bytes; returns the average kernel time in ms via *ms. */
+int rq_debug_run_wave_program(uint32_t K, uint32_t T, const uint32_t* words, uint32_t n_words,
+                              const uint32_t* wave_off, uint32_t n_levels, uint32_t n_blocks,
+                              uint32_t iters, float* ms);
 
 #ifdef __cplusplus
 }

@@ -55,12 +55,27 @@ struct DevBuf {
     ~DevBuf() { if (p) (void)hipFree(p); }
 };
 
-constexpr uint32_t ENC_WAVES = 8;  // waves per k_encode workgroup (rq_kernels.hip)
+// Waves per k_encode workgroup (8 or 16; rq_kernels.hip instantiates both).  RQHIP_WAVES
+// overrides the default for experiments; it is read once per process.
+uint32_t enc_waves() {
+    static const uint32_t nw = [] {
+        const char* e = std::getenv("RQHIP_WAVES");
+        const uint32_t v = e ? (uint32_t)std::atoi(e) : 8u;
+        return (v == 16u) ? 16u : 8u;
+    }();
+    return nw;
+}
+
+struct DevWave {  // the wave program for one strip width (slot fields are LDS dword offsets)
+    WaveProgram wp;
+    DevBuf wstream, wave_off;
+};
 
 struct DevPlan {
     Plan host;
-    WaveProgram wp;
-    DevBuf load_slot, wstream, wave_off, col_slot;
+    uint32_t n_slots = 0;  // slot image rows: plan slots + zero slot + H trash slots
+    std::map<uint32_t, std::unique_ptr<DevWave>> waves;  // keyed by strip width sd
+    DevBuf load_slot, col_slot;
     DevBuf cid;            // A^-1 restricted to source columns (decode), L x cid_stride bytes
     uint32_t cid_stride = 0;
     bool cid_ready = false;
@@ -144,11 +159,8 @@ int get_dev_plan(DevCtx* ctx, const Params& p, DevPlan** out) {
         if (rc) return rc;
         std::unique_ptr<DevPlan> n(new DevPlan());
         n->host = *hp;
-        std::string err;
-        if (!build_wave_program(n->host, ENC_WAVES, &n->wp, &err)) return fail(RQ_ERR_PLAN, err);
+        n->n_slots = n->host.n_slots + 1 + std::max<uint32_t>(n->host.p.H, 1);
         if ((rc = upload(n->load_slot, n->host.load_slot))) return rc;
-        if ((rc = upload(n->wstream, n->wp.words))) return rc;
-        if ((rc = upload(n->wave_off, n->wp.wave_off))) return rc;
         if ((rc = upload(n->col_slot, n->host.col_slot))) return rc;
         dp = std::move(n);
     }
@@ -162,6 +174,21 @@ DevParams dev_params(const Params& p) {
     return d;
 }
 
+int get_dev_wave(DevPlan* dp, uint32_t sd, DevWave** out) {
+    auto& dw = dp->waves[sd];
+    if (!dw) {
+        std::unique_ptr<DevWave> n(new DevWave());
+        std::string err;
+        if (!build_wave_program(dp->host, enc_waves(), sd, &n->wp, &err)) return fail(RQ_ERR_PLAN, err);
+        int rc;
+        if ((rc = upload(n->wstream, n->wp.words))) return rc;
+        if ((rc = upload(n->wave_off, n->wp.wave_off))) return rc;
+        dw = std::move(n);
+    }
+    *out = dw.get();
+    return RQ_OK;
+}
+
 // Strip geometry: the widest strip (<= 32 dwords) whose n_slots x sd image fits the LDS.
 struct Geometry {
     uint32_t sd, n_strips, group;
@@ -169,10 +196,10 @@ struct Geometry {
 int geometry(const DevPlan& dp, uint32_t T, uint32_t K, bool erasures, Geometry* g) {
     const uint32_t Td = T / 4;
     const size_t budget = 160 * 1024 - 128 * 6 * 4 - (erasures ? ((K + 31) / 32) * 4 : 0);  // - tuple staging
-    const size_t per_dword = (size_t)dp.wp.n_slots * 4;
+    const size_t per_dword = (size_t)dp.n_slots * 4;
     uint32_t sd_max = (uint32_t)std::min<size_t>(32, budget / per_dword);
     if (sd_max == 0) return fail(RQ_ERR_UNSUPPORTED, "K' too large for the LDS-resident plan (n_slots=" +
-                                                         std::to_string(dp.wp.n_slots) + ")");
+                                                         std::to_string(dp.n_slots) + ")");
     g->n_strips = (Td + sd_max - 1) / sd_max;
     g->sd = (Td + g->n_strips - 1) / g->n_strips;
     g->group = 8;
@@ -180,18 +207,18 @@ int geometry(const DevPlan& dp, uint32_t T, uint32_t K, bool erasures, Geometry*
     return RQ_OK;
 }
 
-EncArgs base_args(const DevPlan& dp, const Params& p, uint32_t T, uint32_t sd) {
+EncArgs base_args(const DevPlan& dp, const DevWave& dw, const Params& p, uint32_t T, uint32_t sd) {
     EncArgs a;
     std::memset(&a, 0, sizeof a);
     a.p = dev_params(p);
     a.T = T;
-    a.n_slots = dp.wp.n_slots;
+    a.n_slots = dw.wp.n_slots;
     a.sd = sd;
-    a.n_levels = dp.wp.n_levels;
+    a.n_levels = dw.wp.n_levels;
     a.load_slot = dp.load_slot.as<uint16_t>();
-    a.wstream = dp.wstream.as<uint32_t>();
-    a.wave_off = dp.wave_off.as<uint32_t>();
-    a.n_waves = dp.wp.n_waves;
+    a.wstream = dw.wstream.as<uint32_t>();
+    a.wave_off = dw.wave_off.as<uint32_t>();
+    a.n_waves = dw.wp.n_waves;
     a.col_slot = dp.col_slot.as<uint16_t>();
     static const uint32_t dbg = [] {  // timing ablations only (tools/ablate.py)
         const char* s = std::getenv("RQHIP_DBG");
@@ -210,7 +237,9 @@ int encode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, c
     if (rc) return rc;
     Geometry g;
     if ((rc = geometry(*dp, T, p.K, false, &g))) return rc;
-    EncArgs a = base_args(*dp, p, T, g.sd);
+    DevWave* dw;
+    if ((rc = get_dev_wave(dp, g.sd, &dw))) return rc;
+    EncArgs a = base_args(*dp, *dw, p, T, g.sd);
     a.src = static_cast<const uint8_t*>(src);
     a.src_stride = src_stride;
     a.out_esi = d_esi;
@@ -318,7 +347,9 @@ int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, v
     // 1) syndromes: sigma_j = r_j ^ G_j A^-1 D(S with erased rows zeroed)
     Geometry g;
     if ((rc = geometry(*dp, T, p.K, true, &g))) return rc;
-    EncArgs a = base_args(*dp, p, T, g.sd);
+    DevWave* dw;
+    if ((rc = get_dev_wave(dp, g.sd, &dw))) return rc;
+    EncArgs a = base_args(*dp, *dw, p, T, g.sd);
     a.src = static_cast<const uint8_t*>(data);
     a.src_stride = data_stride;
     a.blk_map = di + o_map;
@@ -465,19 +496,62 @@ int rq_plan_export(uint32_t K, uint32_t sizes[5], uint32_t* level_start, uint32_
     return RQ_OK;
 }
 
-int rq_wave_export(uint32_t K, uint32_t sizes[4], uint32_t* words, uint32_t* wave_off) {
+int rq_wave_export(uint32_t K, uint32_t sd, uint32_t sizes[4], uint32_t* words, uint32_t* wave_off) {
     const Plan* pl;
     int rc = host_plan(K, &pl);
     if (rc) return rc;
     WaveProgram wp;
     std::string err;
-    if (!build_wave_program(*pl, ENC_WAVES, &wp, &err)) return fail(RQ_ERR_PLAN, err);
+    if (!build_wave_program(*pl, enc_waves(), sd, &wp, &err)) return fail(RQ_ERR_PLAN, err);
     sizes[0] = (uint32_t)wp.words.size();
     sizes[1] = wp.n_waves;
     sizes[2] = wp.n_levels;
     sizes[3] = wp.n_slots;
     if (words) std::memcpy(words, wp.words.data(), wp.words.size() * 4);
     if (wave_off) std::memcpy(wave_off, wp.wave_off.data(), wp.wave_off.size() * 4);
+    return RQ_OK;
+}
+
+int rq_debug_run_wave_program(uint32_t K, uint32_t T, const uint32_t* words, uint32_t n_words,
+                              const uint32_t* wave_off, uint32_t n_levels, uint32_t n_blocks, uint32_t iters,
+                              float* ms) {
+    Params p;
+    int rc = params_for_K(K, &p);
+    if (rc) return fail(rc, "k is too big");
+    DevCtx* ctx;
+    if ((rc = get_ctx(&ctx))) return rc;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DevPlan* dp;
+    if ((rc = get_dev_plan(ctx, p, &dp))) return rc;
+    Geometry g;
+    if ((rc = geometry(*dp, T, p.K, false, &g))) return rc;
+    DevWave* dwv;
+    if ((rc = get_dev_wave(dp, g.sd, &dwv))) return rc;
+    EncArgs a = base_args(*dp, *dwv, p, T, g.sd);
+    DevBuf w, wo, src;
+    std::vector<uint32_t> wv(words, words + n_words);
+    wv.resize(wv.size() + 256, 0);
+    std::vector<uint32_t> ov(wave_off, wave_off + enc_waves());
+    if ((rc = upload(w, wv)) || (rc = upload(wo, ov)) || (rc = src.ensure((size_t)n_blocks * K * T))) return rc;
+    HIP_TRY(hipMemset(src.p, 0, (size_t)n_blocks * K * T));
+    a.wstream = w.as<uint32_t>();
+    a.wave_off = wo.as<uint32_t>();
+    a.n_levels = n_levels;
+    a.src = src.as<uint8_t>();
+    a.src_stride = (uint64_t)K * T;
+    hipEvent_t e0, e1;
+    HIP_TRY(hipEventCreate(&e0));
+    HIP_TRY(hipEventCreate(&e1));
+    launch_encode(a, g.n_strips, n_blocks, g.group, nullptr);
+    HIP_TRY(hipEventRecord(e0, nullptr));
+    for (uint32_t i = 0; i < iters; ++i) launch_encode(a, g.n_strips, n_blocks, g.group, nullptr);
+    HIP_TRY(hipEventRecord(e1, nullptr));
+    HIP_TRY(hipEventSynchronize(e1));
+    float t = 0;
+    HIP_TRY(hipEventElapsedTime(&t, e0, e1));
+    *ms = t / (float)iters;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
     return RQ_OK;
 }
 

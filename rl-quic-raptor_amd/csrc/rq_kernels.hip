@@ -196,12 +196,22 @@ __global__ void __launch_bounds__(NW * 64) k_encode(EncArgs a) {
         return *reinterpret_cast<const uint32_t*>(gcol + (size_t)isi * T);
     };
     // Descriptor words: readlane from the current page; the cursor is wave-uniform.
-    uint32_t pos = 0;
-    auto pick = [&](uint32_t w) -> uint32_t { return half ? (w >> 16) : (w & 0xFFFFu); };
+    uint32_t pos = 0;  // word index in the current page (wave-uniform)
+    // Slot fields in the stream are LDS dword offsets (slot * sd): this lane's half is extracted
+    // with one per-lane bitfield extract, its address with one shift-add.
+    const uint32_t sh = half << 4;
+    const uint32_t hl4 = hlc << 2;
+    char* const ldsb = reinterpret_cast<char*>(lds);
+    // (non-volatile asm: the compiler otherwise re-associates this into three VALU ops)
+    auto at = [&](uint32_t w) -> uint32_t* {
+        uint32_t b;
+        asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(b) : "v"(__builtin_amdgcn_ubfe(w, sh, 16)), "v"(hl4));
+        return reinterpret_cast<uint32_t*>(ldsb + b);
+    };
     // Lanes past the strip never write real slots: they write the trash slot instead, so the
     // statement loop has no divergent control flow.
     uint32_t* const trash = lds + (a.n_slots - 1) * sd;
-    const uint32_t zero_slot = a.n_slots - 1 - a.p.H;  // WaveProgram: zero slot, then H trash slots
+    const uint32_t zero_off = (a.n_slots - 1 - a.p.H) * sd;  // WaveProgram: zero slot, then H trash
     uint32_t ht = 0;  // Horner running value (kept across continuation pieces)
 
     const uint32_t n_levels = (a.dbg & 2u) ? 0u : a.n_levels;
@@ -210,112 +220,114 @@ __global__ void __launch_bounds__(NW * 64) k_encode(EncArgs a) {
     unsigned long long t_lv = stamping ? __builtin_amdgcn_s_memtime() : 0ull;
     // One segment: its ops, then the NEXT word (bit0 barrier, bit1 page switch).
     auto segment = [&](const uint32_t cur) -> uint32_t {
-        auto fetch = [&]() -> uint32_t {
-            const uint32_t w = __builtin_amdgcn_readlane(cur, __builtin_amdgcn_readfirstlane(pos));
-            ++pos;
-            return w;
-        };
-        const uint32_t nops = fetch();
+        uint32_t p = __builtin_amdgcn_readfirstlane(pos);
+#define RL(i) __builtin_amdgcn_readlane(cur, (i))
+        const uint32_t nops = RL(p);
+        ++p;
         for (uint32_t op = 0; op < nops; ++op) {
-            const uint32_t hdr = fetch();
+            const uint32_t hdr = RL(p), dw = RL(p + 1);
+            p += 2;
             const uint32_t ty = hdr & 7u, n = hdr >> 16;
-            const uint32_t dst = pick(fetch());
-            uint32_t gi = 0xFFFFFFFFu;
-            if (hdr & 32u) {
-                const uint32_t ga = fetch(), gb = fetch();
-                gi = half ? gb : ga;
-            }
-            const uint32_t accm = ((hdr >> (half ? 4 : 3)) & 1u) ? 0xFFFFFFFFu : 0u;
-            uint32_t* D = lds + __umul24(dst, sd) + hlc;
+            uint32_t* D = at(dw);
             uint32_t* Dw = live ? D : trash;
             if (ty == ST_XOR_) {
-                uint32_t v = *D & accm;
-                if (hdr & 32u) v ^= gload(gi == 0xFFFFFFFFu ? K : gi);
-                uint32_t k = 0;
-                for (; k + 4 <= n; k += 4) {
-                    const uint32_t s0 = pick(fetch()), s1 = pick(fetch()), s2 = pick(fetch()), s3 = pick(fetch());
-                    const uint32_t x0 = lds[__umul24(s0, sd) + hlc], x1 = lds[__umul24(s1, sd) + hlc];
-                    const uint32_t x2 = lds[__umul24(s2, sd) + hlc], x3 = lds[__umul24(s3, sd) + hlc];
-                    v ^= (x0 ^ x1) ^ (x2 ^ x3);
+                uint32_t v = 0;
+                if (hdr & 24u) v = *D & (((hdr >> (3 + half)) & 1u) ? 0xFFFFFFFFu : 0u);
+                if (hdr & 32u) {
+                    const uint32_t ga = RL(p), gb = RL(p + 1);
+                    p += 2;
+                    const uint32_t gi = half ? gb : ga;
+                    v ^= gload(gi == 0xFFFFFFFFu ? K : gi);
                 }
-                for (; k < n; ++k) v ^= lds[__umul24(pick(fetch()), sd) + hlc];
+                uint32_t k = 0;
+                for (; k + 8 <= n; k += 8) {
+                    uint32_t x[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) x[u] = *at(RL(p + k + u));
+                    v ^= ((x[0] ^ x[1]) ^ (x[2] ^ x[3])) ^ ((x[4] ^ x[5]) ^ (x[6] ^ x[7]));
+                }
+                for (; k + 4 <= n; k += 4) {
+                    const uint32_t w0 = RL(p + k), w1 = RL(p + k + 1), w2 = RL(p + k + 2), w3 = RL(p + k + 3);
+                    v ^= (*at(w0) ^ *at(w1)) ^ (*at(w2) ^ *at(w3));
+                }
+                for (; k < n; ++k) v ^= *at(RL(p + k));
+                p += n;
                 *Dw = v;
             } else if (ty == ST_MUL_) {
-                uint32_t v = *D & accm;
-                uint32_t k = 0;
-                for (; k + 2 <= n; k += 2) {
-                    const uint32_t sa = pick(fetch()), ca = fetch(), sb = pick(fetch()), cb = fetch();
-                    const uint32_t xa = lds[__umul24(sa, sd) + hlc], xb = lds[__umul24(sb, sd) + hlc];
-                    v ^= gfmul4(xa, half ? (ca >> 8) : ca) ^ gfmul4(xb, half ? (cb >> 8) : cb);
+                uint32_t v = *D & (((hdr >> (3 + half)) & 1u) ? 0xFFFFFFFFu : 0u);
+                for (uint32_t k = 0; k < n; ++k) {
+                    const uint32_t sw = RL(p + 2 * k), cw = RL(p + 2 * k + 1);
+                    v ^= gfmul4(*at(sw), (cw >> (half << 3)) & 0xFFu);
                 }
-                for (; k < n; ++k) {
-                    const uint32_t s = pick(fetch());
-                    const uint32_t cw = fetch();
-                    v ^= gfmul4(lds[__umul24(s, sd) + hlc], half ? (cw >> 8) : cw);
-                }
+                p += 2 * n;
                 *Dw = v;
             } else if (ty == ST_SCALE_) {
-                const uint32_t cw = fetch();
-                *Dw = gfmul4(*D, half ? (cw >> 8) : cw);
+                const uint32_t cw = RL(p);
+                ++p;
+                *Dw = gfmul4(*D, (cw >> (half << 3)) & 0xFFu);
             } else if (ty == ST_HORNER_) {
-                // HDPC chunk: t = alpha*t ^ y_j; partial[h] ^= MT[h][j]*t (fire-and-forget
-                // LDS atomics, no round trip on the chain); finish: partial[h] ^= tau_h * t.
+                // HDPC chunk: t = alpha*t ^ y_j; partial[h] ^= MT[h][j]*t (fire-and-forget LDS
+                // atomics: no round trip on the chain); finish: partial[h] ^= tau_h * t.
                 const uint32_t H = a.p.H;
                 const uint32_t pstride = live ? sd : 0u;  // non-live lanes hit the trash slot
-                uint32_t* P = live ? D : trash;
+                uint32_t* P = Dw;
                 if (hdr & 64u) {
                     ht = 0;
                     for (uint32_t h = 0; h < H; ++h) P[h * pstride] = 0u;
                 }
+                auto col_y = [&](uint32_t e) -> uint32_t {
+                    const uint32_t s = e & 0xFFFFu;
+                    return *reinterpret_cast<const uint32_t*>(ldsb + (((s != SLOT_NONE_ ? s : zero_off) << 2) + hl4));
+                };
+                auto scatter = [&](uint32_t e) {
+                    if ((e >> 26) & 1u) {
+                        for (uint32_t h = 0; h < H; ++h)
+                            __hip_atomic_fetch_xor(P + h * pstride, gfmul4(ht, alpha_pow(h)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    } else {
+                        __hip_atomic_fetch_xor(P + ((e >> 16) & 31u) * pstride, ht, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_fetch_xor(P + ((e >> 21) & 31u) * pstride, ht, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                };
                 uint32_t j = 0;
                 for (; j + 4 <= n; j += 4) {
                     uint32_t e[4], y[4];
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
-                        const uint32_t ea = fetch(), eb = fetch();
+                        const uint32_t ea = RL(p + 2 * (j + u)), eb = RL(p + 2 * (j + u) + 1);
                         e[u] = half ? eb : ea;
-                    }
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const uint32_t sl = e[u] & 0xFFFFu;
-                        y[u] = lds[__umul24(sl != SLOT_NONE_ ? sl : zero_slot, sd) + hlc];  // n_slots-2 = zero slot
+                        y[u] = col_y(e[u]);
                     }
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
                         ht = xtime4(ht) ^ y[u];
-                        if ((e[u] >> 26) & 1u) {
-                            for (uint32_t h = 0; h < H; ++h) __hip_atomic_fetch_xor(P + h * pstride, gfmul4(ht, alpha_pow(h)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        } else {
-                            __hip_atomic_fetch_xor(P + ((e[u] >> 16) & 31u) * pstride, ht, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            __hip_atomic_fetch_xor(P + ((e[u] >> 21) & 31u) * pstride, ht, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        }
+                        scatter(e[u]);
                     }
                 }
                 for (; j < n; ++j) {
-                    const uint32_t ea = fetch(), eb = fetch();
+                    const uint32_t ea = RL(p + 2 * j), eb = RL(p + 2 * j + 1);
                     const uint32_t e = half ? eb : ea;
-                    const uint32_t sl = e & 0xFFFFu;
-                    ht = xtime4(ht) ^ lds[__umul24(sl != SLOT_NONE_ ? sl : zero_slot, sd) + hlc];
-                    if ((e >> 26) & 1u) {
-                        for (uint32_t h = 0; h < H; ++h) __hip_atomic_fetch_xor(P + h * pstride, gfmul4(ht, alpha_pow(h)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    } else {
-                        __hip_atomic_fetch_xor(P + ((e >> 16) & 31u) * pstride, ht, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        __hip_atomic_fetch_xor(P + ((e >> 21) & 31u) * pstride, ht, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    }
+                    ht = xtime4(ht) ^ col_y(e);
+                    scatter(e);
                 }
+                p += 2 * n;
                 if (hdr & 128u) {
                     const uint32_t nt = (H + 3) / 4;
-                    const uint32_t ta0 = fetch(), ta1 = nt > 1 ? fetch() : 0u, ta2 = nt > 2 ? fetch() : 0u, ta3 = nt > 3 ? fetch() : 0u;
-                    const uint32_t tb0 = fetch(), tb1 = nt > 1 ? fetch() : 0u, tb2 = nt > 2 ? fetch() : 0u, tb3 = nt > 3 ? fetch() : 0u;
-                    const uint32_t t0 = half ? tb0 : ta0, t1 = half ? tb1 : ta1, t2 = half ? tb2 : ta2, t3 = half ? tb3 : ta3;
                     for (uint32_t h = 0; h < H; ++h) {
-                        const uint32_t tw = (h < 4) ? t0 : (h < 8) ? t1 : (h < 12) ? t2 : t3;
-                        __hip_atomic_fetch_xor(P + h * pstride, gfmul4(ht, tw >> (8 * (h & 3))), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        // tau words of A, then of B
+                        const uint32_t tw = __builtin_amdgcn_readlane(cur, p + (h >> 2));
+                        const uint32_t twb = __builtin_amdgcn_readlane(cur, p + nt + (h >> 2));
+                        const uint32_t c = ((half ? twb : tw) >> (8 * (h & 3))) & 0xFFu;
+                        __hip_atomic_fetch_xor(P + h * pstride, gfmul4(ht, c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
+                    p += 2 * nt;
                 }
             }
         }
-        return fetch();
+        const uint32_t nx = RL(p);
+        ++p;
+#undef RL
+        pos = p;
+        return nx;
     };
     uint32_t lv = 0;
     auto after = [&](uint32_t nx) -> bool {  // barrier bookkeeping; true when the program is done
@@ -603,20 +615,22 @@ int launch_gather(const DevParams& p, const uint8_t* C, uint32_t T, const uint32
     return (int)hipGetLastError();
 }
 
-constexpr int ENC_WAVES = 8;
-
 int launch_encode(const EncArgs& a, uint32_t n_strips, uint32_t n_blocks, uint32_t /*group*/, void* stream) {
     const uint32_t nebw = a.erased_off ? (a.p.K + 31) / 32 : 0;
     const size_t lds = ((size_t)a.n_slots * a.sd + OUT_BATCH * 6 + nebw) * 4;
-    if (a.n_waves != ENC_WAVES || a.sd > 32 || lds > 160 * 1024) return (int)hipErrorInvalidValue;
+    if ((a.n_waves != 8 && a.n_waves != 16) || a.sd > 32 || lds > 160 * 1024) return (int)hipErrorInvalidValue;
     static bool attr_set = false;  // allow the full 160 KiB of LDS
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)k_encode<ENC_WAVES>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_encode<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_encode<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         (void)hipFuncSetAttribute((const void*)k_solve, hipFuncAttributeMaxDynamicSharedMemorySize, 158 * 1024);
         (void)hipFuncSetAttribute((const void*)k_apply, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_set = true;
     }
-    hipLaunchKernelGGL(k_encode<ENC_WAVES>, dim3(n_strips, n_blocks), dim3(ENC_WAVES * 64), lds, (hipStream_t)stream, a);
+    if (a.n_waves == 16)
+        hipLaunchKernelGGL(k_encode<16>, dim3(n_strips, n_blocks), dim3(16 * 64), lds, (hipStream_t)stream, a);
+    else
+        hipLaunchKernelGGL(k_encode<8>, dim3(n_strips, n_blocks), dim3(8 * 64), lds, (hipStream_t)stream, a);
     return (int)hipGetLastError();
 }
 

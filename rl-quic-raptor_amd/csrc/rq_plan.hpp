@@ -91,12 +91,14 @@ bool compile_encode_plan(const Params& p, Plan* out, std::string* err, const Pla
 //   SCALE     : 1 word coefA | coefB<<8 (n = 0)
 //   HORNER    : n column pairs (wordA, wordB) as in Stmt; [finish] ceil(H/4) tau words of A, of B
 struct WaveProgram {
-    uint32_t n_waves = 0, n_levels = 0, n_slots = 0, zero_slot = 0, trash_slot = 0;
+    uint32_t n_waves = 0, n_levels = 0, n_slots = 0, zero_slot = 0, trash_slot = 0, sd = 0;
     std::vector<uint32_t> words;      // all streams, padded for chunk prefetch
     std::vector<uint32_t> wave_off;   // [n_waves] stream start
     uint32_t max_stream = 0;          // longest stream (words)
 };
-bool build_wave_program(const Plan& plan, uint32_t n_waves, WaveProgram* out, std::string* err);
+// sd > 0: slot fields are emitted as LDS dword offsets (slot * sd) for a strip of sd dwords;
+// sd == 0: raw slot indices (host-side emulation).
+bool build_wave_program(const Plan& plan, uint32_t n_waves, uint32_t sd, WaveProgram* out, std::string* err);
 
 // Encode the output (LT gather) statements for a list of ISIs: per output one word
 // nsrc(8) followed by nsrc slots (C columns mapped through col_slot).  Appended to *words;

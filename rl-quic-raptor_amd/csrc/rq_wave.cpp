@@ -58,13 +58,14 @@ bool decode_stmt(const Plan& pl, uint32_t s, SDesc* d, std::string* err) {
 }
 
 // Emit the op pair (A, B) as one or more pieces of <= MAX_PIECE words.
-void emit_pair(const SDesc& A, const SDesc* Bp, uint32_t H, uint32_t zero, uint32_t trash,
+void emit_pair(const SDesc& A, const SDesc* Bp, uint32_t H, uint32_t zero, uint32_t trash, uint32_t sd,
                std::vector<std::vector<uint32_t>>* pieces) {
+    auto O = [sd](uint32_t slot) { return sd ? slot * sd : slot; };  // LDS dword offset (sd > 0)
     const SDesc nop;
     const SDesc& B = Bp ? *Bp : nop;
     const bool pair = Bp != nullptr;
     const uint32_t n = std::max(A.n, pair ? B.n : 0u);
-    const uint32_t dstw = A.dst | ((pair ? B.dst : trash) << 16);
+    const uint32_t dstw = O(A.dst) | (O(pair ? B.dst : trash) << 16);
     const uint32_t nt = (H + 3) / 4;
     if (A.type == ST_SCALE) {
         pieces->push_back({A.type, dstw, A.coef[0] | ((pair ? B.coef[0] : 0u) << 8)});
@@ -76,8 +77,12 @@ void emit_pair(const SDesc& A, const SDesc* Bp, uint32_t H, uint32_t zero, uint3
         const uint32_t pad_col = 0xFFFFu;
         for (uint32_t k = 0; k < n; ++k) {
             const uint32_t ka = n - A.n, kb = n - (pair ? B.n : 0);
-            cols.push_back(k >= ka ? A.src[k - ka] : pad_col);
-            cols.push_back((pair && k >= kb) ? B.src[k - kb] : pad_col);
+            auto col = [&](uint32_t e) {  // column word: slot field -> offset (NONE stays NONE)
+                const uint32_t s = e & 0xFFFFu;
+                return s == 0xFFFFu ? e : ((e & ~0xFFFFu) | O(s));
+            };
+            cols.push_back(k >= ka ? col(A.src[k - ka]) : pad_col);
+            cols.push_back((pair && k >= kb) ? col(B.src[k - kb]) : pad_col);
         }
         const uint32_t per = (MAX_PIECE - 2 - 2 * nt) / 2;  // columns per piece
         for (uint32_t c0 = 0; c0 < n || c0 == 0; c0 += per) {
@@ -113,8 +118,8 @@ void emit_pair(const SDesc& A, const SDesc* Bp, uint32_t H, uint32_t zero, uint3
         op.push_back(dstw);
         if (g) { op.push_back(A.g); op.push_back(pair ? B.g : 0xFFFFFFFFu); }
         for (uint32_t k = k0; k < k1; ++k) {
-            const uint32_t sa = k < A.n ? A.src[k] : zero;
-            const uint32_t sb = (pair && k < B.n) ? B.src[k] : zero;
+            const uint32_t sa = O(k < A.n ? A.src[k] : zero);
+            const uint32_t sb = O((pair && k < B.n) ? B.src[k] : zero);
             op.push_back(sa | (sb << 16));
             if (mul) {
                 const uint32_t ca = k < A.n ? A.coef[k] : 0;
@@ -130,7 +135,7 @@ void emit_pair(const SDesc& A, const SDesc* Bp, uint32_t H, uint32_t zero, uint3
 
 }  // namespace
 
-bool build_wave_program(const Plan& pl, uint32_t n_waves, WaveProgram* out, std::string* err) {
+bool build_wave_program(const Plan& pl, uint32_t n_waves, uint32_t sd, WaveProgram* out, std::string* err) {
     const uint32_t H = pl.p.H;
     const uint32_t zero = pl.n_slots, trash = pl.n_slots + 1;
     out->n_waves = n_waves;
@@ -138,7 +143,11 @@ bool build_wave_program(const Plan& pl, uint32_t n_waves, WaveProgram* out, std:
     out->zero_slot = zero;
     out->trash_slot = trash;
     out->n_slots = pl.n_slots + 1 + std::max<uint32_t>(H, 1);
-    if (out->n_slots >= 0x8000u) { if (err) *err = "wave: too many slots"; return false; }
+    if (out->n_slots >= 0x8000u || (sd && (uint64_t)out->n_slots * sd >= 0xFFFFu)) {
+        if (err) *err = "wave: slot image too large for 16-bit offsets";
+        return false;
+    }
+    out->sd = sd;
     // per wave: list of segments (word vectors, each <= PAGE words incl. count and NEXT)
     std::vector<std::vector<std::vector<uint32_t>>> segs(n_waves);
     for (uint32_t lv = 0; lv < out->n_levels; ++lv) {
@@ -156,7 +165,7 @@ bool build_wave_program(const Plan& pl, uint32_t n_waves, WaveProgram* out, std:
         for (size_t i = 0; i < st.size();) {
             const bool pair = i + 1 < st.size() && st[i + 1].type == st[i].type;
             std::vector<std::vector<uint32_t>> pieces;
-            emit_pair(st[i], pair ? &st[i + 1] : nullptr, H, zero, trash, &pieces);
+            emit_pair(st[i], pair ? &st[i + 1] : nullptr, H, zero, trash, sd, &pieces);
             const uint32_t n = std::max(st[i].n, pair ? st[i + 1].n : 0u);
             cost.push_back(2 + (st[i].type == ST_HORNER ? 4 * n : n));
             groups.push_back(std::move(pieces));

@@ -39,7 +39,7 @@ EXPORTED = (
     "rq_encoder_symbol_size", "rq_encoder_symbol", "rq_encoder_symbols", "rq_encoder_free",
     "rq_decoder_create", "rq_decoder_k", "rq_decoder_add", "rq_decoder_decode", "rq_decoder_free",
     "rq_encode_batch", "rq_decode_batch", "rq_device_count", "rq_set_device", "rq_plan_stats",
-    "rq_plan_export", "rq_wave_export",
+    "rq_plan_export", "rq_wave_export", "rq_debug_run_wave_program",
 )
 
 
@@ -102,7 +102,10 @@ def lib():
             "rq_set_device": ([ctypes.c_int], ctypes.c_int),
             "rq_plan_stats": ([ctypes.c_uint32, u32p], ctypes.c_int),
             "rq_plan_export": ([ctypes.c_uint32, u32p, u32p, u32p, u32p, u16p, u16p], ctypes.c_int),
-            "rq_wave_export": ([ctypes.c_uint32, u32p, u32p, u32p], ctypes.c_int),
+            "rq_wave_export": ([ctypes.c_uint32, ctypes.c_uint32, u32p, u32p, u32p], ctypes.c_int),
+            "rq_debug_run_wave_program": ([ctypes.c_uint32, ctypes.c_uint32, u32p, ctypes.c_uint32, u32p,
+                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                           ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -161,17 +164,18 @@ def plan_export(K):
     return dict(level_start=lv, stmt_off=so, words=w, load_slot=ls, col_slot=cs, Kp=Kp, L=L)
 
 
-def wave_export(K):
-    """Per-wave instruction streams of the K' plan (numpy) for host-side emulation in tests."""
+def wave_export(K, sd=0):
+    """Per-wave instruction streams of the K' plan (numpy) for host-side emulation in tests.
+    sd > 0 emits slot fields as LDS dword offsets (slot * sd), exactly as the kernel receives them."""
     import numpy as np
     sizes = (ctypes.c_uint32 * 4)()
-    _check(lib().rq_wave_export(K, sizes, None, None))
+    _check(lib().rq_wave_export(K, sd, sizes, None, None))
     n_words, n_waves, n_levels, n_slots = list(sizes)
     w = np.zeros(n_words, np.uint32)
     off = np.zeros(n_waves, np.uint32)
     P32 = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
-    _check(lib().rq_wave_export(K, sizes, P32(w), P32(off)))
-    return dict(words=w, wave_off=off, n_waves=n_waves, n_levels=n_levels, n_slots=n_slots)
+    _check(lib().rq_wave_export(K, sd, sizes, P32(w), P32(off)))
+    return dict(words=w, wave_off=off, n_waves=n_waves, n_levels=n_levels, n_slots=n_slots, sd=sd)
 
 
 def device_count():

@@ -93,6 +93,14 @@ def replay_waves(wave, plan, src_rows, K, H):
     T = src_rows.shape[1]
     Td = T // 4
     words = wave["words"]
+    sd = int(wave.get("sd", 0))  # sd > 0: slot fields are LDS dword offsets (slot * sd)
+
+    def S(f):
+        if not sd:
+            return f
+        assert f % sd == 0, "slot offset not a multiple of the strip width"
+        return f // sd
+
     src32 = np.ascontiguousarray(src_rows).view(np.uint32).reshape(Kp, Td).copy()
     src32[K:] = 0
     slots = np.zeros((wave["n_slots"], Td), np.uint32)
@@ -127,9 +135,9 @@ def replay_waves(wave, plan, src_rows, K, H):
                         nt = (H + 3) // 4
                         taus = ([F() for _ in range(nt)], [F() for _ in range(nt)]) if hdr & 128 else None
                     for half in (0, 1):
-                        dst = (dd >> 16) if half else (dd & 0xFFFF)
+                        dst = S((dd >> 16) if half else (dd & 0xFFFF))
                         acc = (hdr >> (4 if half else 3)) & 1
-                        pk = (lambda x: x >> 16) if half else (lambda x: x & 0xFFFF)
+                        pk = (lambda x: S(x >> 16)) if half else (lambda x: S(x & 0xFFFF))
                         if ty == ST_XOR:
                             v = slots[dst].copy() if acc else np.zeros(Td, np.uint32)
                             gi = g[half]
@@ -153,7 +161,7 @@ def replay_waves(wave, plan, src_rows, K, H):
                             for ea, eb in body:
                                 e = eb if half else ea
                                 sl = e & 0xFFFF
-                                t = xtime4(t) ^ (slots[sl] if sl != 0xFFFF else 0)
+                                t = xtime4(t) ^ (slots[S(sl)] if sl != 0xFFFF else 0)
                                 if (e >> 26) & 1:
                                     for h in range(H):
                                         slots[dst + h] ^= gfmul4(t, ALPHA_POW[h])

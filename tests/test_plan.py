@@ -52,8 +52,8 @@ def test_plan_fits_lds(rq, K):
     assert s["n_slots"] * 4 * 8 <= 160 * 1024  # at least an 8-dword strip fits the LDS
 
 
-@pytest.mark.parametrize("K,T", [(5, 16), (64, 8), (256, 8), (1024, 4)])
-def test_wave_streams_match_oracle(rq, oracle, K, T):
+@pytest.mark.parametrize("K,T,sd", [(5, 16, 0), (64, 8, 0), (256, 8, 0), (1024, 4, 0), (64, 8, 30), (1024, 4, 30)])
+def test_wave_streams_match_oracle(rq, oracle, K, T, sd):
     """The per-wave instruction streams k_encode executes (paired statements, paged segments,
     split Horner pieces) reproduce the oracle's intermediate symbols."""
     from tests.plan_replay import replay_waves
@@ -61,7 +61,7 @@ def test_wave_streams_match_oracle(rq, oracle, K, T):
     data = rng.integers(0, 256, K * T, dtype=np.uint8)
     p = rq.params(len(data), T)
     plan = rq.plan_export(K)
-    wave = rq.wave_export(K)
+    wave = rq.wave_export(K, sd)
     assert wave["words"].size % 64 == 0
     src = np.zeros((p["Kp"], T), np.uint8)
     src.reshape(-1)[:len(data)] = data
