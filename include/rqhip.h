@@ -122,6 +122,9 @@ int rq_wave_export(uint32_t K, uint32_t sd, uint32_t sizes[4], uint32_t* words, 
 
 /* Diagnostics: run k_encode on a caller-supplied wave program (host arrays) over n_blocks
  * synthetic zero blocks of K rows x T bytes; returns the average kernel time in ms via *ms. */
+/* Diagnostics: checks the device's packed GF(256) primitives (xtime, table multiply) against
+ * host arithmetic on 1024 words x 256 coefficients; the counts of mismatching words. */
+int rq_debug_gf_selftest(uint32_t* bad_xtime, uint32_t* bad_mul);
 int rq_debug_run_wave_program(uint32_t K, uint32_t T, const uint32_t* words, uint32_t n_words,
                               const uint32_t* wave_off, uint32_t n_levels, uint32_t n_blocks,
                               uint32_t iters, float* ms);

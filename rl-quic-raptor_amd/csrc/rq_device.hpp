@@ -74,6 +74,7 @@ struct ApplyArgs {
 int launch_encode(const EncArgs& a, uint32_t n_strips, uint32_t n_blocks, uint32_t group, void* stream);
 int launch_solve(const SolveArgs& a, uint32_t n_blocks, uint32_t lds_bytes, void* stream);
 int launch_apply(const ApplyArgs& a, uint32_t n_strips, uint32_t n_blocks, uint32_t lds_bytes, void* stream);
+int launch_gf_selftest(const uint32_t* x, uint32_t n, const uint32_t* tabs, uint32_t* out);
 int launch_gather(const DevParams& p, const uint8_t* C, uint32_t T, const uint32_t* esi, uint32_t n, uint8_t* out,
                   void* stream);
 int upload_tables();  // rand / degree tables to __constant__ memory (once per device)

@@ -55,13 +55,13 @@ struct DevBuf {
     ~DevBuf() { if (p) (void)hipFree(p); }
 };
 
-// Waves per k_encode workgroup (8 or 16; rq_kernels.hip instantiates both).  RQHIP_WAVES
+// Waves per k_encode workgroup (16, or 8; rq_kernels.hip instantiates both).  RQHIP_WAVES
 // overrides the default for experiments; it is read once per process.
 uint32_t enc_waves() {
     static const uint32_t nw = [] {
         const char* e = std::getenv("RQHIP_WAVES");
-        const uint32_t v = e ? (uint32_t)std::atoi(e) : 8u;
-        return (v == 16u) ? 16u : 8u;
+        const uint32_t v = e ? (uint32_t)std::atoi(e) : 16u;
+        return (v == 8u) ? 8u : 16u;
     }();
     return nw;
 }
@@ -121,6 +121,17 @@ int get_ctx(DevCtx** out) {
     return RQ_OK;
 }
 
+// Plan options; RQHIP_PASSB / RQHIP_DEPTH_B override the pass-B strategy for experiments.
+const PlanOptions& plan_options() {
+    static const PlanOptions o = [] {
+        PlanOptions r;
+        if (const char* e = std::getenv("RQHIP_PASSB")) r.passb_mode = (uint32_t)std::atoi(e);
+        if (const char* e = std::getenv("RQHIP_DEPTH_B")) r.depth_b = (uint32_t)std::atoi(e);
+        return r;
+    }();
+    return o;
+}
+
 int host_plan(uint32_t K, const Plan** out) {
     Params p;
     int rc = params_for_K(K, &p);
@@ -130,7 +141,7 @@ int host_plan(uint32_t K, const Plan** out) {
     if (!pl) {
         std::unique_ptr<Plan> np(new Plan());
         std::string err;
-        if (!compile_encode_plan(p, np.get(), &err)) return fail(RQ_ERR_PLAN, err);
+        if (!compile_encode_plan(p, np.get(), &err, plan_options())) return fail(RQ_ERR_PLAN, err);
         pl = std::move(np);
     }
     *out = pl.get();
@@ -195,9 +206,17 @@ struct Geometry {
 };
 int geometry(const DevPlan& dp, uint32_t T, uint32_t K, bool erasures, Geometry* g) {
     const uint32_t Td = T / 4;
-    const size_t budget = 160 * 1024 - 128 * 6 * 4 - (erasures ? ((K + 31) / 32) * 4 : 0);  // - tuple staging
+    // - stream ring / tuple staging, erasure bitmap, 16-byte alignment of the ring
+    const size_t ring = std::max<size_t>((size_t)enc_waves() * 2 * 64, 128 * 6) * 4;
+    const size_t budget = 160 * 1024 - ring - 16 - (erasures ? ((K + 31) / 32) * 4 : 0);
     const size_t per_dword = (size_t)dp.n_slots * 4;
-    uint32_t sd_max = (uint32_t)std::min<size_t>(32, budget / per_dword);
+    // RQHIP_SD_MAX caps the strip width (narrower strips -> several workgroups per CU); experiments
+    static const uint32_t sd_cap = [] {
+        const char* e = std::getenv("RQHIP_SD_MAX");
+        const uint32_t v = e ? (uint32_t)std::atoi(e) : 32u;
+        return v ? std::min<uint32_t>(v, 32u) : 32u;
+    }();
+    uint32_t sd_max = (uint32_t)std::min<size_t>(sd_cap, budget / per_dword);
     if (sd_max == 0) return fail(RQ_ERR_UNSUPPORTED, "K' too large for the LDS-resident plan (n_slots=" +
                                                          std::to_string(dp.n_slots) + ")");
     g->n_strips = (Td + sd_max - 1) / sd_max;
@@ -509,6 +528,37 @@ int rq_wave_export(uint32_t K, uint32_t sd, uint32_t sizes[4], uint32_t* words, 
     sizes[3] = wp.n_slots;
     if (words) std::memcpy(words, wp.words.data(), wp.words.size() * 4);
     if (wave_off) std::memcpy(wave_off, wp.wave_off.data(), wp.wave_off.size() * 4);
+    return RQ_OK;
+}
+
+int rq_debug_gf_selftest(uint32_t* bad_xtime, uint32_t* bad_mul) {
+    if (!bad_xtime || !bad_mul) return fail(RQ_ERR_BAD_ARG, "null output");
+    DevCtx* ctx;
+    int rc;
+    if ((rc = get_ctx(&ctx))) return rc;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    const uint32_t n = 1024;
+    std::vector<uint32_t> x(n), tabs(256 * 5), out((size_t)n * 257);
+    uint32_t s = 0x12345678u;
+    for (uint32_t i = 0; i < n; ++i) { s = s * 1664525u + 1013904223u; x[i] = i < 256 ? i * 0x01010101u : s; }
+    for (uint32_t c = 0; c < 256; ++c) gf_perm_tables((uint8_t)c, &tabs[c * 5]);
+    DevBuf dx, dt, dout;
+    if ((rc = upload(dx, x)) || (rc = upload(dt, tabs)) || (rc = dout.ensure(out.size() * 4))) return rc;
+    HIP_TRY((hipError_t)launch_gf_selftest(dx.as<uint32_t>(), n, dt.as<uint32_t>(), dout.as<uint32_t>()));
+    HIP_TRY(hipMemcpy(out.data(), dout.p, out.size() * 4, hipMemcpyDeviceToHost));
+    const GF& g = gf();
+    auto mul4 = [&](uint32_t v, uint8_t c) {
+        uint32_t r = 0;
+        for (int b = 0; b < 4; ++b) r |= (uint32_t)g.mul((uint8_t)(v >> (8 * b)), c) << (8 * b);
+        return r;
+    };
+    *bad_xtime = 0;
+    *bad_mul = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (out[i] != mul4(x[i], 2)) ++*bad_xtime;
+        for (uint32_t c = 0; c < 256; ++c)
+            if (out[n + (size_t)c * n + i] != mul4(x[i], (uint8_t)c)) ++*bad_mul;
+    }
     return RQ_OK;
 }
 

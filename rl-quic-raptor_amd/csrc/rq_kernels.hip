@@ -15,16 +15,15 @@
 // the requested output rows.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
+#include <type_traits>
 
 #include "rfc6330_tables.h"
 #include "rq_device.hpp"
+#include "rq_wave_format.hpp"
 
 namespace rq {
-
-// must match rq_plan.hpp
-constexpr uint32_t ST_XOR_ = 0, ST_MUL_ = 1, ST_SCALE_ = 3, ST_HORNER_ = 4;
-constexpr uint32_t SLOT_NONE_ = 0xFFFFu;
 
 __constant__ uint32_t c_V[4][256];
 __constant__ uint32_t c_DEG[31];
@@ -58,9 +57,22 @@ __device__ __forceinline__ uint32_t gfmul4(uint32_t x, uint32_t c) {
     }
     return r;
 }
-__device__ __forceinline__ uint32_t alpha_pow(uint32_t h) {  // alpha^h, h < 16
-    constexpr uint32_t tab[16] = {1, 2, 4, 8, 16, 32, 64, 128, 29, 58, 116, 232, 205, 135, 19, 38};
-    return tab[h & 15];
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {  // one v_bitop3_b32
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+// alpha * x per byte without a multiply: v_perm_b32 selectors 8..11 replicate the top bit of
+// bytes 1, 3, 5, 7 of {S0:S1}; with S1 = x, S0 = x << 8 those are the top bits of x's bytes
+// 1, 3, 0, 2, so selector 0x090B080A yields 0xFF in every byte whose top bit is set.
+__device__ __forceinline__ uint32_t xtime4p(uint32_t x) {
+    const uint32_t m = __builtin_amdgcn_perm(x << 8, x, 0x090B080Au);
+    return ((x << 1) & 0xFEFEFEFEu) ^ (m & 0x1D1D1D1Du);
+}
+// c * x per byte from the host-built byte tables of c (rq_core.hpp gf_perm_tables): three
+// v_perm_b32 lookups on the 3/3/2-bit groups of each byte.
+__device__ __forceinline__ uint32_t gfmul4_tab(uint32_t x, uint32_t t0, uint32_t t1, uint32_t t2, uint32_t t3,
+                                               uint32_t t4) {
+    const uint32_t s0 = x & 0x07070707u, s1 = (x >> 3) & 0x07070707u, s2 = (x >> 6) & 0x03030303u;
+    return xor3(__builtin_amdgcn_perm(t1, t0, s0), __builtin_amdgcn_perm(t3, t2, s1), __builtin_amdgcn_perm(t4, t4, s2));
 }
 
 // ------------------------------ LT tuple on device (RQ/params.go:83-112) -------------------
@@ -136,18 +148,23 @@ __global__ void __launch_bounds__(NW * 64) k_encode(EncArgs a) {
     const uint32_t tid = threadIdx.x, nthr = NW * 64;
     const uint32_t K = a.p.K;
     const uint32_t nebw = a.erased_off ? (K + 31) / 32 : 0;
-    uint32_t* tup = lds + a.n_slots * sd;          // OUT_BATCH x 6
-    uint32_t* ebits = tup + OUT_BATCH * 6;
+    // LDS: slot image | R (stream ring during the program, LT-tuple staging after it) | bitmap
+    const uint32_t img = (a.n_slots * sd + 3u) & ~3u;           // dwords, 16-byte aligned
+    const uint32_t rsz = max(NW * 2u * WV_PAGE, OUT_BATCH * 6u);
+    uint32_t* tup = lds + img;                                  // OUT_BATCH x 6 (after the program)
+    uint32_t* ebits = lds + img + rsz;
 
-    // stream pages: prefetch the first two before the prologue
+    // per-wave stream ring: two 64-word pages (current, next) staged from global memory
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t lane = tid & 63u;
     const uint32_t* ws = a.wstream;
-    uint32_t page = __builtin_amdgcn_readfirstlane(a.wave_off[wave]);  // word offset of current page
-    // Two page registers used ping-pong: the segment processor is instantiated once per register
-    // (qa current / qb current), so a refill load always targets the idle register directly and
-    // no register copy of an in-flight load exists (which would force vmcnt(0) on every page).
-    uint32_t qa = ws[page + lane], qb = ws[page + 64 + lane];
+    uint32_t pg = __builtin_amdgcn_readfirstlane(a.wave_off[wave]);  // word offset of the current page
+    uint32_t* ring = lds + img + wave * 2u * WV_PAGE;
+    {
+        const uint32_t p0 = ws[pg + lane], p1 = ws[pg + WV_PAGE + lane];
+        ring[lane] = p0;
+        ring[WV_PAGE + lane] = p1;
+    }
 
     {   // zero the slot image (16-byte stores) and the bitmap
         const uint32_t nw4 = (a.n_slots * sd) >> 2;
@@ -195,184 +212,174 @@ __global__ void __launch_bounds__(NW * 64) k_encode(EncArgs a) {
         if (!inb || isi >= K || erased_row(isi)) return 0u;
         return *reinterpret_cast<const uint32_t*>(gcol + (size_t)isi * T);
     };
-    // Descriptor words: readlane from the current page; the cursor is wave-uniform.
-    uint32_t pos = 0;  // word index in the current page (wave-uniform)
-    // Slot fields in the stream are LDS dword offsets (slot * sd): this lane's half is extracted
-    // with one per-lane bitfield extract, its address with one shift-add.
-    const uint32_t sh = half << 4;
-    const uint32_t hl4 = hlc << 2;
+
+    // ---- the wave's instruction stream (rq_wave_format.hpp) ----
+    // Each half of the wave reads its 4 words of a group with one ds_read_b128; slot fields are
+    // LDS byte offsets, so a source costs one add (the lane's column) and one ds_read_b32.
     char* const ldsb = reinterpret_cast<char*>(lds);
-    // (non-volatile asm: the compiler otherwise re-associates this into three VALU ops)
-    auto at = [&](uint32_t w) -> uint32_t* {
-        uint32_t b;
-        asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(b) : "v"(__builtin_amdgcn_ubfe(w, sh, 16)), "v"(hl4));
-        return reinterpret_cast<uint32_t*>(ldsb + b);
+    const uint32_t hl4 = hlc << 2;
+    const uint32_t ring_b = (uint32_t)((char*)ring - ldsb);
+    const uint32_t hv = ring_b + (half << 4);  // this half's words of a group
+    auto grp_at = [&](uint32_t gpos) -> uint4 {  // gpos: byte offset of a group within the ring
+        return *reinterpret_cast<const uint4*>(ldsb + hv + gpos);
     };
-    // Lanes past the strip never write real slots: they write the trash slot instead, so the
-    // statement loop has no divergent control flow.
-    uint32_t* const trash = lds + (a.n_slots - 1) * sd;
-    const uint32_t zero_off = (a.n_slots - 1 - a.p.H) * sd;  // WaveProgram: zero slot, then H trash
-    uint32_t ht = 0;  // Horner running value (kept across continuation pieces)
+    auto rd = [&](uint32_t off) -> uint32_t { return *reinterpret_cast<const uint32_t*>(ldsb + off + hl4); };
+    // lanes past the strip write the (last) trash slot
+    const uint32_t trash_b = (a.n_slots - 1) * sd * 4 + hl4;
+    auto wr_addr = [&](uint32_t off) -> uint32_t { return live ? off + hl4 : trash_b; };
+    auto wr = [&](uint32_t addr, uint32_t v) { *reinterpret_cast<uint32_t*>(ldsb + addr) = v; };
+    constexpr uint32_t GB = WV_GROUP * 4;  // group bytes
 
     const uint32_t n_levels = (a.dbg & 2u) ? 0u : a.n_levels;
     // diagnostics: per level and wave, [cycles working, cycles at the barrier] of workgroup (0,0)
     const bool stamping = a.stamp && blockIdx.x == 0 && blockIdx.y == 0 && lane == 0;
     unsigned long long t_lv = stamping ? __builtin_amdgcn_s_memtime() : 0ull;
-    // One segment: its ops, then the NEXT word (bit0 barrier, bit1 page switch).
-    auto segment = [&](const uint32_t cur) -> uint32_t {
-        uint32_t p = __builtin_amdgcn_readfirstlane(pos);
-#define RL(i) __builtin_amdgcn_readlane(cur, (i))
-        const uint32_t nops = RL(p);
-        ++p;
-        for (uint32_t op = 0; op < nops; ++op) {
-            const uint32_t hdr = RL(p), dw = RL(p + 1);
-            p += 2;
-            const uint32_t ty = hdr & 7u, n = hdr >> 16;
-            uint32_t* D = at(dw);
-            uint32_t* Dw = live ? D : trash;
-            if (ty == ST_XOR_) {
-                uint32_t v = 0;
-                if (hdr & 24u) v = *D & (((hdr >> (3 + half)) & 1u) ? 0xFFFFFFFFu : 0u);
-                if (hdr & 32u) {
-                    const uint32_t ga = RL(p), gb = RL(p + 1);
-                    p += 2;
-                    const uint32_t gi = half ? gb : ga;
-                    v ^= gload(gi == 0xFFFFFFFFu ? K : gi);
-                }
-                uint32_t k = 0;
-                for (; k + 8 <= n; k += 8) {
-                    uint32_t x[8];
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) x[u] = *at(RL(p + k + u));
-                    v ^= ((x[0] ^ x[1]) ^ (x[2] ^ x[3])) ^ ((x[4] ^ x[5]) ^ (x[6] ^ x[7]));
-                }
-                for (; k + 4 <= n; k += 4) {
-                    const uint32_t w0 = RL(p + k), w1 = RL(p + k + 1), w2 = RL(p + k + 2), w3 = RL(p + k + 3);
-                    v ^= (*at(w0) ^ *at(w1)) ^ (*at(w2) ^ *at(w3));
-                }
-                for (; k < n; ++k) v ^= *at(RL(p + k));
-                p += n;
-                *Dw = v;
-            } else if (ty == ST_MUL_) {
-                uint32_t v = *D & (((hdr >> (3 + half)) & 1u) ? 0xFFFFFFFFu : 0u);
-                for (uint32_t k = 0; k < n; ++k) {
-                    const uint32_t sw = RL(p + 2 * k), cw = RL(p + 2 * k + 1);
-                    v ^= gfmul4(*at(sw), (cw >> (half << 3)) & 0xFFu);
-                }
-                p += 2 * n;
-                *Dw = v;
-            } else if (ty == ST_SCALE_) {
-                const uint32_t cw = RL(p);
-                ++p;
-                *Dw = gfmul4(*D, (cw >> (half << 3)) & 0xFFu);
-            } else if (ty == ST_HORNER_) {
-                // HDPC chunk: t = alpha*t ^ y_j; partial[h] ^= MT[h][j]*t (fire-and-forget LDS
-                // atomics: no round trip on the chain); finish: partial[h] ^= tau_h * t.
-                const uint32_t H = a.p.H;
-                const uint32_t pstride = live ? sd : 0u;  // non-live lanes hit the trash slot
-                uint32_t* P = Dw;
-                if (hdr & 64u) {
-                    ht = 0;
-                    for (uint32_t h = 0; h < H; ++h) P[h * pstride] = 0u;
-                }
-                auto col_y = [&](uint32_t e) -> uint32_t {
-                    const uint32_t s = e & 0xFFFFu;
-                    return *reinterpret_cast<const uint32_t*>(ldsb + (((s != SLOT_NONE_ ? s : zero_off) << 2) + hl4));
-                };
-                auto scatter = [&](uint32_t e) {
-                    if ((e >> 26) & 1u) {
-                        for (uint32_t h = 0; h < H; ++h)
-                            __hip_atomic_fetch_xor(P + h * pstride, gfmul4(ht, alpha_pow(h)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    } else {
-                        __hip_atomic_fetch_xor(P + ((e >> 16) & 31u) * pstride, ht, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        __hip_atomic_fetch_xor(P + ((e >> 21) & 31u) * pstride, ht, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    }
-                };
-                uint32_t j = 0;
-                for (; j + 4 <= n; j += 4) {
-                    uint32_t e[4], y[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const uint32_t ea = RL(p + 2 * (j + u)), eb = RL(p + 2 * (j + u) + 1);
-                        e[u] = half ? eb : ea;
-                        y[u] = col_y(e[u]);
-                    }
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        ht = xtime4(ht) ^ y[u];
-                        scatter(e[u]);
-                    }
-                }
-                for (; j < n; ++j) {
-                    const uint32_t ea = RL(p + 2 * j), eb = RL(p + 2 * j + 1);
-                    const uint32_t e = half ? eb : ea;
-                    ht = xtime4(ht) ^ col_y(e);
-                    scatter(e);
-                }
-                p += 2 * n;
-                if (hdr & 128u) {
-                    const uint32_t nt = (H + 3) / 4;
-                    for (uint32_t h = 0; h < H; ++h) {
-                        // tau words of A, then of B
-                        const uint32_t tw = __builtin_amdgcn_readlane(cur, p + (h >> 2));
-                        const uint32_t twb = __builtin_amdgcn_readlane(cur, p + nt + (h >> 2));
-                        const uint32_t c = ((half ? twb : tw) >> (8 * (h & 3))) & 0xFFu;
-                        __hip_atomic_fetch_xor(P + h * pstride, gfmul4(ht, c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    }
-                    p += 2 * nt;
-                }
-            }
-        }
-        const uint32_t nx = RL(p);
-        ++p;
-#undef RL
-        pos = p;
-        return nx;
-    };
-    uint32_t lv = 0;
-    auto after = [&](uint32_t nx) -> bool {  // barrier bookkeeping; true when the program is done
-        if (nx & 1u) {
-            unsigned long long t_w = 0;
-            if (stamping) t_w = __builtin_amdgcn_s_memtime();
-            // Level barrier: only LDS traffic must be complete (lgkmcnt); page and source-row loads
-            // stay in flight (a __syncthreads() would also drain vmcnt).
-            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-            if (stamping) {
-                const unsigned long long t_b = __builtin_amdgcn_s_memtime();
-                a.stamp[(lv * NW + wave) * 2] = t_w - t_lv;
-                a.stamp[(lv * NW + wave) * 2 + 1] = t_b - t_w;
-                t_lv = t_b;
-            }
-            ++lv;
-        }
-        return lv >= n_levels;
-    };
-    // Page refills are issued as inline-asm loads, invisible to the compiler's wait-count pass
-    // (which otherwise drains vmcnt(0) at every segment for loop-carried loads); the page that
-    // becomes current is waited for explicitly at the switch.  VMEM ops retire in order, so the
-    // compiler's own counted waits for its loads stay correct with these extra loads in flight.
-    auto refill = [&](uint32_t& reg) {
-        const uint32_t* p = ws + page + 64 + lane;
-        asm volatile("global_load_dword %0, %1, off" : "=v"(reg) : "v"(p) : "memory");
-    };
-    // Compiler-visible drain of the prologue's page loads (vmcnt(0), lgkm/exp untouched), so the
-    // wait-count pass sees no VMEM pending at the loop header and inserts no wait there.
+    // Page refills are LDS-DMA (global_load_lds_dword: 64 lanes x 4 B = one page straight into
+    // the freed ring slot, no VGPR).  The compiler does not see them; each is waited for with
+    // vmcnt(0) at the next page switch, which orders the wave's own later ds_reads behind it.
+    // The compiler's counted waits for its own loads stay correct (at worst they wait longer).
+    // compiler-visible drain of the prologue's loads, so no VMEM wait lands inside the loop
     __builtin_amdgcn_s_waitcnt(0x0F70);
-    bool done = n_levels == 0;
-    while (!done) {
-        uint32_t nx;
-        do { nx = segment(qa); done = after(nx); } while (!done && !(nx & 2u));
-        if (done) break;
-        page += 64; pos = 0;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // qb (page + 0) has landed
-        refill(qa);                                         // qa <- page + 1
-        do { nx = segment(qb); done = after(nx); } while (!done && !(nx & 2u));
-        if (done) break;
-        page += 64; pos = 0;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        refill(qb);
+
+    uint32_t cslot = 0;   // ring page slot of the current page
+    // page switch: the next page is staged in the other slot; refill this one with the page after
+    auto advance = [&]() -> uint32_t {
+        const uint32_t old_b = ring_b + cslot * (WV_PAGE * 4);  // wave-uniform LDS address of the freed slot
+        cslot ^= 1u;
+        pg += WV_PAGE;
+        const uint32_t* src = ws + pg + WV_PAGE + lane;        // the page after the new current one
+        uint32_t keep;
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\t"
+                     "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                     "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(src), "s"(old_b) : "memory");
+        return cslot * (WV_PAGE * 4);
+    };
+    // XOR of 4N sources (N payload groups), straight-line: all group reads, then all source reads
+    auto xor_n = [&](auto NC, uint32_t pay) -> uint32_t {
+        constexpr uint32_t N = decltype(NC)::value;
+        uint4 s[N];
+#pragma unroll
+        for (uint32_t q = 0; q < N; ++q) s[q] = grp_at(pay + q * GB);
+        uint32_t v = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < N; ++q) v = xor3(xor3(v, rd(s[q].x), rd(s[q].y)), rd(s[q].z), rd(s[q].w));
+        return v;
+    };
+    auto mul_n = [&](auto NC, uint32_t pay) -> uint32_t {
+        constexpr uint32_t N = decltype(NC)::value;  // sources (2 groups each)
+        uint4 g1[N], g2[N];
+#pragma unroll
+        for (uint32_t q = 0; q < N; ++q) { g1[q] = grp_at(pay + 2 * q * GB); g2[q] = grp_at(pay + (2 * q + 1) * GB); }
+        uint32_t v = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < N; ++q) v ^= gfmul4_tab(rd(g1[q].x), g1[q].y, g1[q].z, g1[q].w, g2[q].x, g2[q].y);
+        return v;
+    };
+    using I1 = std::integral_constant<uint32_t, 1>; using I2 = std::integral_constant<uint32_t, 2>;
+    using I3 = std::integral_constant<uint32_t, 3>; using I4 = std::integral_constant<uint32_t, 4>;
+    using I5 = std::integral_constant<uint32_t, 5>; using I6 = std::integral_constant<uint32_t, 6>;
+    static_assert(WV_MAX_PIECE - 1 == 6, "xor_n cases");
+
+    uint32_t ht = 0;      // HDPC Horner running value (kept across the pieces of a chunk)
+    uint32_t gp = 0;      // byte offset of the current group within the ring
+    uint32_t lv = 0;
+    uint4 g = grp_at(0);
+    while (lv < n_levels) {
+        const uint32_t hdr = __builtin_amdgcn_readfirstlane(g.x);
+        const uint32_t ty = hdr & 7u, n = hdr >> 16;
+        if (ty == OP_END) {
+            gp = (hdr & FLAG_ADVANCE) ? advance() : gp + GB;
+            g = grp_at(gp);
+            if (hdr & FLAG_BARRIER) {
+                unsigned long long t_w = 0;
+                if (stamping) t_w = __builtin_amdgcn_s_memtime();
+                // level barrier: LDS traffic complete (lgkmcnt); the page load stays in flight
+                asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                if (stamping) {
+                    const unsigned long long t_b = __builtin_amdgcn_s_memtime();
+                    a.stamp[(lv * NW + wave) * 2] = t_w - t_lv;
+                    a.stamp[(lv * NW + wave) * 2 + 1] = t_b - t_w;
+                    t_lv = t_b;
+                }
+                ++lv;
+            }
+            continue;
+        }
+        if (ty == OP_HORNER) {
+            // One HDPC chunk piece on the whole wave (row indices are scalars): t = alpha*t ^ y;
+            // partial[a] ^= t; partial[b] ^= t.  Between pieces of a chunk the partials wait in
+            // their destination rows and t in a register.
+            uint32_t hp[16];
+            const uint32_t H = a.p.H;
+            const uint32_t base = wr_addr(g.y), pstride = live ? sd * 4 : 0u;
+            if (hdr & FLAG_HSTART) {
+                ht = 0;
+#pragma unroll
+                for (int h = 0; h < 16; ++h) hp[h] = 0;
+            } else {
+#pragma unroll
+                for (uint32_t h = 0; h < 16; ++h) hp[h] = h < H ? rd(g.y + h * sd * 4) : 0u;
+            }
+            const uint32_t pay = gp + GB;
+            for (uint32_t q = 0; q < n; ++q) {
+                const uint4 gc = grp_at(pay + q * GB);
+                uint32_t e[8], y[8];
+                e[0] = __builtin_amdgcn_readfirstlane(gc.x); e[1] = __builtin_amdgcn_readfirstlane(gc.y);
+                e[2] = __builtin_amdgcn_readfirstlane(gc.z); e[3] = __builtin_amdgcn_readfirstlane(gc.w);
+                e[4] = __builtin_amdgcn_readlane(gc.x, 32); e[5] = __builtin_amdgcn_readlane(gc.y, 32);
+                e[6] = __builtin_amdgcn_readlane(gc.z, 32); e[7] = __builtin_amdgcn_readlane(gc.w, 32);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) y[j] = rd(e[j] & 0x3FFFFu);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    ht = xtime4p(ht) ^ y[j];
+                    hp[(e[j] >> 18) & 15u] ^= ht;
+                    hp[(e[j] >> 22) & 15u] ^= ht;
+                }
+            }
+            const bool fin = (hdr & FLAG_HFINISH) != 0;
+            uint32_t tw[4] = {0, 0, 0, 0};
+            if (fin) {
+                const uint4 gt = grp_at(pay + n * GB);
+                tw[0] = __builtin_amdgcn_readfirstlane(gt.x); tw[1] = __builtin_amdgcn_readfirstlane(gt.y);
+                tw[2] = __builtin_amdgcn_readfirstlane(gt.z); tw[3] = __builtin_amdgcn_readfirstlane(gt.w);
+            }
+#pragma unroll
+            for (uint32_t h = 0; h < 16; ++h)
+                if (h < H) wr(base + h * pstride, fin ? hp[h] ^ gfmul4(ht, (tw[h >> 2] >> (8 * (h & 3))) & 0xFFu) : hp[h]);
+            gp = pay + (n + (fin ? 1u : 0u)) * GB;
+            g = grp_at(gp);
+            continue;
+        }
+        const uint32_t npos = gp + (n + 1u) * GB;
+        const uint4 gn = grp_at(npos);  // next op's header group, in flight during this op
+        const uint32_t pay = gp + GB;
+        uint32_t v = 0;
+        if (hdr & FLAG_G) v = gload(g.z);
+        if (ty == OP_XOR) {
+            switch (n) {
+                case 1: v ^= xor_n(I1{}, pay); break;
+                case 2: v ^= xor_n(I2{}, pay); break;
+                case 3: v ^= xor_n(I3{}, pay); break;
+                case 4: v ^= xor_n(I4{}, pay); break;
+                case 5: v ^= xor_n(I5{}, pay); break;
+                default: v ^= xor_n(I6{}, pay); break;
+            }
+        } else {  // OP_MUL
+            switch (n) {
+                case 2: v ^= mul_n(I1{}, pay); break;
+                case 4: v ^= mul_n(I2{}, pay); break;
+                default: v ^= mul_n(I3{}, pay); break;
+            }
+        }
+        wr(wr_addr(g.y), v);
+        gp = npos;
+        g = gn;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no asm load outlives the program
+    // no ring refill outlives the program: the ring becomes the tuple staging area
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
     // ---- outputs: repair symbols (encodeGen, RQ/params.go:162-182) or syndromes (decode) ----
     if (a.out && !(a.dbg & 4u)) {
         uint32_t o0 = 0, o1 = a.n_out;
@@ -609,6 +616,20 @@ __global__ void __launch_bounds__(256) k_gather(DevParams p, const uint8_t* C, u
     }
 }
 
+// Self-test of the packed GF(256) primitives against host tables (rq_debug_gf_selftest):
+// out[i] = xtime4p(x[i]); out[n + c*n + i] = gfmul4_tab(x[i], tables of c).
+__global__ void __launch_bounds__(256) k_gf_selftest(const uint32_t* x, uint32_t n, const uint32_t* tabs, uint32_t* out) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x, c = blockIdx.y;
+    if (i >= n) return;
+    const uint32_t* t = tabs + c * 5;
+    if (c == 0) out[i] = xtime4p(x[i]);
+    out[n + c * n + i] = gfmul4_tab(x[i], t[0], t[1], t[2], t[3], t[4]);
+}
+int launch_gf_selftest(const uint32_t* x, uint32_t n, const uint32_t* tabs, uint32_t* out) {
+    hipLaunchKernelGGL(k_gf_selftest, dim3((n + 255) / 256, 256), dim3(256), 0, nullptr, x, n, tabs, out);
+    return (int)hipGetLastError();
+}
+
 int launch_gather(const DevParams& p, const uint8_t* C, uint32_t T, const uint32_t* esi, uint32_t n, uint8_t* out,
                   void* stream) {
     hipLaunchKernelGGL(k_gather, dim3(n), dim3(256), 0, (hipStream_t)stream, p, C, T, esi, n, out);
@@ -617,7 +638,9 @@ int launch_gather(const DevParams& p, const uint8_t* C, uint32_t T, const uint32
 
 int launch_encode(const EncArgs& a, uint32_t n_strips, uint32_t n_blocks, uint32_t /*group*/, void* stream) {
     const uint32_t nebw = a.erased_off ? (a.p.K + 31) / 32 : 0;
-    const size_t lds = ((size_t)a.n_slots * a.sd + OUT_BATCH * 6 + nebw) * 4;
+    const size_t img = ((size_t)a.n_slots * a.sd + 3) & ~(size_t)3;
+    const size_t rsz = std::max<size_t>((size_t)a.n_waves * 2 * WV_PAGE, OUT_BATCH * 6);
+    const size_t lds = (img + rsz + nebw) * 4;
     if ((a.n_waves != 8 && a.n_waves != 16) || a.sd > 32 || lds > 160 * 1024) return (int)hipErrorInvalidValue;
     static bool attr_set = false;  // allow the full 160 KiB of LDS
     if (!attr_set) {

@@ -333,15 +333,17 @@ bool compile_encode_plan(const Params& p, Plan* out, std::string* err, const Pla
         Stmt st;
         st.type = ST_HORNER; st.acc = false; st.dst = (uint16_t)(tmp_base + q * H);
         for (uint32_t j = s0; j < e0; ++j) {
+            // The last column (MT[h][KS-1] = alpha^h) scatters nothing (a == b cancels); its
+            // alpha^h * t term is folded into the final chunk's tau below.
             const uint32_t slot = (cstate[j] == PIVOTED) ? j : SLOT_NONE;
-            const uint32_t last = (j == KS - 1) ? 1u : 0u;
-            st.src.push_back((slot & 0xFFFFu) | ((uint32_t)(last ? 0 : ma[j]) << 16) |
-                             ((uint32_t)(last ? 0 : mb[j]) << 21) | (last << 26));
+            const bool last = j == KS - 1;
+            st.src.push_back((slot & 0xFFFFu) | ((uint32_t)(last ? 0 : ma[j]) << 16) | ((uint32_t)(last ? 0 : mb[j]) << 21));
         }
         uint32_t word = 0;
         std::vector<uint32_t> tau;
         for (uint32_t h = 0; h < H; ++h) {
-            word |= (uint32_t)F[(size_t)h * (KS + 1) + e0] << (8 * (h & 3));
+            const uint8_t th = (uint8_t)(F[(size_t)h * (KS + 1) + e0] ^ (e0 == KS ? g.pow_alpha(h) : 0));
+            word |= (uint32_t)th << (8 * (h & 3));
             if ((h & 3) == 3 || h + 1 == H) { tau.push_back(word); word = 0; }
         }
         st.extra = (uint32_t)tau.size();
@@ -494,7 +496,7 @@ bool compile_encode_plan(const Params& p, Plan* out, std::string* err, const Pla
         const uint64_t* wk = wrow(k);
         uint32_t wc = 0;
         for (uint32_t x = 0; x < nw; ++x) wc += (uint32_t)__builtin_popcountll(wk[x]);
-        if (wc <= terms.size()) {
+        if (opt.passb_mode == 1 || wc <= terms.size()) {
             std::vector<uint32_t> s;
             for (uint32_t x = 0; x < nw; ++x) {
                 uint64_t bits = wk[x];

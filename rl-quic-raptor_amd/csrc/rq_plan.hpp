@@ -40,8 +40,9 @@ constexpr uint16_t SLOT_NONE = 0xFFFF;
 // Statement word 0: dst(16) | nsrc(12) | type(3) | ACC(1).  Then (SCALE) one extra word,
 // then nsrc source words: slot(16) | coef(8) | 0, or SRC_GLOBAL | isi for a source row that is
 // re-read from global memory (zero if isi >= K or erased).  HORNER: word0 dst = first of H
-// partial slots, nsrc = chunk length; per column word: slot(16) | a(5) | b(5) | last(1);
-// then ceil(H/4) words of tau coefficients.
+// partial slots, nsrc = chunk length; per column word: slot(16) | a(5) | b(5) -- t is added to
+// partials a and b (a == b: nothing); then ceil(H/4) words of tau coefficients (partial[h] ^=
+// tau_h * t at the end of the chunk; the last chunk's tau includes MT[h][KS-1] = alpha^h).
 struct Stmt {
     uint32_t type = ST_XOR;
     bool acc = false;
@@ -75,29 +76,22 @@ struct PlanOptions {
     uint32_t horner_chunks = 16;  // parallel chunks of the HDPC Horner scan
     uint32_t depth_a = 1u << 30;  // dependency-depth cap of the forward substitution (pass A)
     uint32_t depth_b = 1u << 30;  // dependency-depth cap of the final substitution (pass B)
+    // pass B: 1 = in place only (C_k = y_k ^ W_k C_U: one level, no source re-reads from global
+    // memory); 0 = per row the cheaper of in place / rebuild (fewer XORs, ~90 more levels)
+    uint32_t passb_mode = 1;
 };
 bool compile_encode_plan(const Params& p, Plan* out, std::string* err, const PlanOptions& opt = PlanOptions());
 
 // ---------------------------------------------------------------------------------------
-// Wave program: the level-scheduled statements re-packed for execution by whole wavefronts.
-// Each op runs two statements of the same type side by side (lanes 0-31: A, 32-63: B), so every
-// descriptor word is wave-uniform.  Streams are 64-word pages of segments (rq_wave.cpp):
-//   segment   : count, ops..., NEXT (bit0: barrier = end of level, bit1: next segment on next page)
-//   op header : type(3) | accA<<3 | accB<<4 | hasG<<5 | hornerStart<<6 | hornerFinish<<7 | n<<16
-//   dst word  : dstA | dstB<<16
-//   [hasG]    : isiA, isiB (0xFFFFFFFF = none) -- source rows re-read from global memory
-//   XOR       : n words srcA | srcB<<16
-//   MUL       : n x (srcA | srcB<<16, coefA | coefB<<8)
-//   SCALE     : 1 word coefA | coefB<<8 (n = 0)
-//   HORNER    : n column pairs (wordA, wordB) as in Stmt; [finish] ceil(H/4) tau words of A, of B
+// Wave program: the level-scheduled statements re-packed into per-wave instruction streams for
+// k_encode; the stream format is specified in rq_wave_format.hpp.
 struct WaveProgram {
     uint32_t n_waves = 0, n_levels = 0, n_slots = 0, zero_slot = 0, trash_slot = 0, sd = 0;
     std::vector<uint32_t> words;      // all streams, padded for chunk prefetch
     std::vector<uint32_t> wave_off;   // [n_waves] stream start
     uint32_t max_stream = 0;          // longest stream (words)
 };
-// sd > 0: slot fields are emitted as LDS dword offsets (slot * sd) for a strip of sd dwords;
-// sd == 0: raw slot indices (host-side emulation).
+// Slot fields are LDS byte offsets (slot * sd * 4) for a strip of sd dwords (sd > 0).
 bool build_wave_program(const Plan& plan, uint32_t n_waves, uint32_t sd, WaveProgram* out, std::string* err);
 
 // Encode the output (LT gather) statements for a list of ISIs: per output one word

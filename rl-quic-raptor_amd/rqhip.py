@@ -39,7 +39,7 @@ EXPORTED = (
     "rq_encoder_symbol_size", "rq_encoder_symbol", "rq_encoder_symbols", "rq_encoder_free",
     "rq_decoder_create", "rq_decoder_k", "rq_decoder_add", "rq_decoder_decode", "rq_decoder_free",
     "rq_encode_batch", "rq_decode_batch", "rq_device_count", "rq_set_device", "rq_plan_stats",
-    "rq_plan_export", "rq_wave_export", "rq_debug_run_wave_program",
+    "rq_plan_export", "rq_wave_export", "rq_debug_run_wave_program", "rq_debug_gf_selftest",
 )
 
 
@@ -106,6 +106,7 @@ def lib():
             "rq_debug_run_wave_program": ([ctypes.c_uint32, ctypes.c_uint32, u32p, ctypes.c_uint32, u32p,
                                            ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                            ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
+            "rq_debug_gf_selftest": ([u32p, u32p], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -164,7 +165,7 @@ def plan_export(K):
     return dict(level_start=lv, stmt_off=so, words=w, load_slot=ls, col_slot=cs, Kp=Kp, L=L)
 
 
-def wave_export(K, sd=0):
+def wave_export(K, sd):
     """Per-wave instruction streams of the K' plan (numpy) for host-side emulation in tests.
     sd > 0 emits slot fields as LDS dword offsets (slot * sd), exactly as the kernel receives them."""
     import numpy as np
@@ -176,6 +177,13 @@ def wave_export(K, sd=0):
     P32 = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
     _check(lib().rq_wave_export(K, sd, sizes, P32(w), P32(off)))
     return dict(words=w, wave_off=off, n_waves=n_waves, n_levels=n_levels, n_slots=n_slots, sd=sd)
+
+
+def gf_selftest():
+    """Device GF(256) primitives vs host arithmetic: (bad xtime words, bad table-multiply words)."""
+    a, b = ctypes.c_uint32(0), ctypes.c_uint32(0)
+    _check(lib().rq_debug_gf_selftest(ctypes.byref(a), ctypes.byref(b)))
+    return a.value, b.value
 
 
 def device_count():

@@ -87,19 +87,35 @@ def replay(plan, src_rows, K, H, erased=()):
     return C32.view(np.uint8).reshape(L, T)
 
 
+OP_XOR, OP_MUL, OP_HORNER, OP_END = 0, 1, 4, 7
+FLAG_G, FLAG_HSTART, FLAG_HFINISH, FLAG_BARRIER, FLAG_ADVANCE = 1 << 5, 1 << 6, 1 << 7, 1 << 8, 1 << 9
+
+
+def gfmul4_tab(x, t):
+    """v_perm table multiply (rq_kernels.hip gfmul4_tab) on uint32 arrays."""
+    def perm(hi, lo, sel):
+        tab = np.array([(lo >> (8 * i)) & 0xFF for i in range(4)] + [(hi >> (8 * i)) & 0xFF for i in range(4)], np.uint32)
+        out = np.zeros_like(sel)
+        for b in range(4):
+            out |= tab[(sel >> (8 * b)) & 0xFF] << (8 * b)
+        return out
+    s0, s1, s2 = x & 0x07070707, (x >> 3) & 0x07070707, (x >> 6) & 0x03030303
+    return perm(t[1], t[0], s0) ^ perm(t[3], t[2], s1) ^ perm(t[4], t[4], s2)
+
+
 def replay_waves(wave, plan, src_rows, K, H):
-    """Emulate k_encode's wave streams (paged segments, paired statements A|B, Horner pieces)."""
+    """Emulate k_encode's wave streams (rq_wave_format.hpp): pages of 8-word groups, half A/B
+    words, byte-offset slot fields, END barriers; waves run level by level."""
     Kp, L = plan["Kp"], plan["L"]
     T = src_rows.shape[1]
     Td = T // 4
     words = wave["words"]
-    sd = int(wave.get("sd", 0))  # sd > 0: slot fields are LDS dword offsets (slot * sd)
+    sd = int(wave["sd"])
+    row_bytes = sd * 4
 
-    def S(f):
-        if not sd:
-            return f
-        assert f % sd == 0, "slot offset not a multiple of the strip width"
-        return f // sd
+    def S(off):
+        assert off % row_bytes == 0, "slot offset not a multiple of the strip row"
+        return off // row_bytes
 
     src32 = np.ascontiguousarray(src_rows).view(np.uint32).reshape(Kp, Td).copy()
     src32[K:] = 0
@@ -107,76 +123,61 @@ def replay_waves(wave, plan, src_rows, K, H):
     for i in range(K):
         slots[plan["load_slot"][i]] = src32[i]
     nw = wave["n_waves"]
-    page = [int(o) for o in wave["wave_off"]]
-    pos = [0] * nw
-    ht = [[np.zeros(Td, np.uint32), np.zeros(Td, np.uint32)] for _ in range(nw)]
+    gpos = [int(o) for o in wave["wave_off"]]  # word index of the next group
+    hstate = [None] * nw
     for _lv in range(wave["n_levels"]):
         for w in range(nw):
-            def F():
-                assert pos[w] < 64, "segment crosses a page"
-                v = int(words[page[w] + pos[w]])
-                pos[w] += 1
-                return v
+            def G():
+                g = [int(x) for x in words[gpos[w]:gpos[w] + 8]]
+                gpos[w] += 8
+                return g
             while True:
-                nops = F()
-                for _ in range(nops):
-                    hdr = F()
-                    ty, n = hdr & 7, hdr >> 16
-                    dd = F()
-                    g = (F(), F()) if hdr & 32 else (0xFFFFFFFF, 0xFFFFFFFF)
-                    if ty == ST_XOR:
-                        body = [F() for _ in range(n)]
-                    elif ty == ST_MUL:
-                        body = [(F(), F()) for _ in range(n)]
-                    elif ty == ST_SCALE:
-                        body = F()
+                h = G()
+                hdr = h[0]
+                assert h[4] == hdr
+                ty, n = hdr & 7, hdr >> 16
+                if ty == OP_END:
+                    if hdr & FLAG_ADVANCE:
+                        gpos[w] = (gpos[w] + 63) // 64 * 64
+                    if hdr & FLAG_BARRIER:
+                        break
+                    continue
+                start = gpos[w] - 8
+                span = 8 * (n + 1 + (1 if ty == OP_HORNER and hdr & FLAG_HFINISH else 0))
+                assert start // 64 == (start + span + 8 - 1) // 64, "op (and a closing END) cross a page"
+                body = [G() for _ in range(n)]
+                if ty == OP_HORNER:
+                    tau = G()[:4] if hdr & FLAG_HFINISH else None
+                    dst = S(h[1])
+                    if hdr & FLAG_HSTART:
+                        hstate[w] = [np.zeros(Td, np.uint32), np.zeros((16, Td), np.uint32)]
+                    t, hp = hstate[w]
+                    for g in body:
+                        for e in g:
+                            t = xtime4(t) ^ slots[S(e & 0x3FFFF)]
+                            hp[(e >> 18) & 15] ^= t
+                            hp[(e >> 22) & 15] ^= t
+                    hstate[w] = [t, hp]
+                    if tau is not None:
+                        for hh in range(H):
+                            slots[dst + hh] = hp[hh] ^ gfmul4(t, (tau[hh // 4] >> (8 * (hh & 3))) & 0xFF)
+                    continue
+                res = []
+                for half in (0, 1):
+                    o = 4 * half
+                    v = np.zeros(Td, np.uint32)
+                    gi = h[o + 2]
+                    if hdr & FLAG_G and gi != 0xFFFFFFFF and gi < K:
+                        v ^= src32[gi]
+                    if ty == OP_XOR:
+                        for g in body:
+                            for e in g[o:o + 4]:
+                                v ^= slots[S(e)]
                     else:
-                        body = [(F(), F()) for _ in range(n)]
-                        nt = (H + 3) // 4
-                        taus = ([F() for _ in range(nt)], [F() for _ in range(nt)]) if hdr & 128 else None
-                    for half in (0, 1):
-                        dst = S((dd >> 16) if half else (dd & 0xFFFF))
-                        acc = (hdr >> (4 if half else 3)) & 1
-                        pk = (lambda x: S(x >> 16)) if half else (lambda x: S(x & 0xFFFF))
-                        if ty == ST_XOR:
-                            v = slots[dst].copy() if acc else np.zeros(Td, np.uint32)
-                            gi = g[half]
-                            if gi != 0xFFFFFFFF and gi < K:
-                                v ^= src32[gi]
-                            for x in body:
-                                v ^= slots[pk(x)]
-                            slots[dst] = v
-                        elif ty == ST_MUL:
-                            v = slots[dst].copy() if acc else np.zeros(Td, np.uint32)
-                            for x, c in body:
-                                v ^= gfmul4(slots[pk(x)], (c >> 8) & 0xFF if half else c & 0xFF)
-                            slots[dst] = v
-                        elif ty == ST_SCALE:
-                            slots[dst] = gfmul4(slots[dst], (body >> 8) & 0xFF if half else body & 0xFF)
-                        else:
-                            if hdr & 64:
-                                ht[w][half] = np.zeros(Td, np.uint32)
-                                slots[dst:dst + H] = 0
-                            t = ht[w][half]
-                            for ea, eb in body:
-                                e = eb if half else ea
-                                sl = e & 0xFFFF
-                                t = xtime4(t) ^ (slots[S(sl)] if sl != 0xFFFF else 0)
-                                if (e >> 26) & 1:
-                                    for h in range(H):
-                                        slots[dst + h] ^= gfmul4(t, ALPHA_POW[h])
-                                else:
-                                    slots[dst + ((e >> 16) & 31)] ^= t
-                                    slots[dst + ((e >> 21) & 31)] ^= t
-                            ht[w][half] = t
-                            if taus is not None:
-                                tw = taus[half]
-                                for h in range(H):
-                                    slots[dst + h] ^= gfmul4(t, (tw[h // 4] >> (8 * (h & 3))) & 0xFF)
-                nx = F()
-                if nx & 2:
-                    page[w] += 64
-                    pos[w] = 0
-                if nx & 1:
-                    break
+                        for k in range(0, n, 2):
+                            g1, g2 = body[k], body[k + 1]
+                            v ^= gfmul4_tab(slots[S(g1[o])], (g1[o + 1], g1[o + 2], g1[o + 3], g2[o], g2[o + 1]))
+                    res.append((S(h[o + 1]), v))
+                for d, v in res:
+                    slots[d] = v
     return slots[plan["col_slot"].astype(np.int64)].view(np.uint8).reshape(L, T)
