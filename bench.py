@@ -56,6 +56,16 @@ def erasure_pattern(K, N, n_blocks, n_erase, seed):
     return er, rep
 
 
+def pmc_traffic(K, T, N, B):
+    """HBM bytes per encode launch from the newest committed rocprofv3 PMC summary of this exact
+    workload (profiles/rNN_traffic.json, written from tools/gpu_profile.sh); None if absent."""
+    for path in sorted((ROOT / "profiles").glob("r*_traffic.json"), reverse=True):
+        t = json.loads(path.read_text())
+        if t.get("workload") == {"K": K, "T": T, "N": N, "blocks": B}:
+            return t["traffic_bytes"], path.name
+    return None, None
+
+
 def cpu_baseline(K, T, N, n_erase, n_blocks):
     """Oracle (C restatement, 1 thread) on a bounded sample of the same workload."""
     from oracle import oracle as O
@@ -112,9 +122,9 @@ def main():
     # correctness of one full step before timing
     rqhip.encode_batch(src, K, T, esis, rep, stream=stream)
     recv = rep.view(B, R, T)[rb, rr].contiguous()
-    for b in range(B):
-        for i in er[b]:
-            data[b, i * T:(i + 1) * T] = 0
+    eb = torch.tensor([b for b in range(B) for _ in er[b]], device=dev, dtype=torch.long)
+    ei = torch.tensor([i for b in range(B) for i in er[b]], device=dev, dtype=torch.long)
+    data.view(B, K, T)[eb, ei] = 0  # erased source rows (one indexing kernel)
     st = db.run(data, recv, stream=stream)
     torch.cuda.synchronize()
     ok_frac = float((st == 1).mean())
@@ -152,6 +162,7 @@ def main():
     value = src_bytes * args.steps / dt / 1e9
     if rank == 0:
         achieved = B * K * T / (enc_ms * 1e-3) / 1e9
+        traffic, traffic_src = pmc_traffic(K, T, N, B)
         line = {
             "metric": "RaptorQ encode+decode GB/s device-resident, K=1024 T=1200B, 1/2/4/8 MI355X",
             "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
@@ -161,9 +172,9 @@ def main():
             "config": {"workload": "encode+decode K=%d T=%d N=%d erase=%d/%d symbols" % (K, T, N, n_erase, N),
                        "blocks_per_gpu": B, "bytes_per_gpu": B * K * T, "parallelism": "block-sharded x%d" % world,
                        "decode_ok_fraction": ok_frac},
-            "roofline": {"bound": "hbm", "kernel": "k_encode (encode batch)", "achieved": round(achieved, 2),
+            "roofline": {"bound": "hbm", "kernel": "rq::k_encode<16, false> (encode batch)", "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": None, "encode_ms_per_launch": round(enc_ms, 4),
+                         "traffic": traffic, "traffic_source": traffic_src, "encode_ms_per_launch": round(enc_ms, 4),
                          "algorithmic_bytes_per_launch": B * K * T},
         }
         if args.cpu_sample > 0 and world == 1:

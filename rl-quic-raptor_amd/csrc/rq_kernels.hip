@@ -137,7 +137,9 @@ __device__ __forceinline__ uint32_t d_degree(uint32_t v, uint32_t W) {
 // statement A, lanes 32-63 statement B, one strip dword per lane); a workgroup barrier closes
 // each dependency level.  Descriptor words are wave-uniform and live in two VGPR pages (current
 // and prefetched next), extracted with v_readlane: no memory latency inside a segment.
-template <int NW>
+// ERASE: decode's syndrome pass (erased source rows read as zero); a separate instantiation so
+// the encode path carries no erasure checks and profiles name the two passes apart.
+template <int NW, bool ERASE>
 __global__ void __launch_bounds__(NW * 64) k_encode(EncArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t sd = a.sd, T = a.T, Td = T >> 2;
@@ -147,7 +149,7 @@ __global__ void __launch_bounds__(NW * 64) k_encode(EncArgs a) {
     const uint32_t width = min(sd, Td - c0);
     const uint32_t tid = threadIdx.x, nthr = NW * 64;
     const uint32_t K = a.p.K;
-    const uint32_t nebw = a.erased_off ? (K + 31) / 32 : 0;
+    const uint32_t nebw = ERASE ? (K + 31) / 32 : 0;
     // LDS: slot image | R (stream ring during the program, LT-tuple staging after it) | bitmap
     const uint32_t img = (a.n_slots * sd + 3u) & ~3u;           // dwords, 16-byte aligned
     const uint32_t rsz = max(NW * 2u * WV_PAGE, OUT_BATCH * 6u);
@@ -188,7 +190,7 @@ __global__ void __launch_bounds__(NW * 64) k_encode(EncArgs a) {
     const bool inb = hl < width;
     const uint8_t* blk = a.src + (size_t)b * a.src_stride;
     const uint8_t* gcol = blk + (size_t)(c0 + hlc) * 4;
-    auto erased_row = [&](uint32_t r) -> bool { return nebw && ((ebits[r >> 5] >> (r & 31)) & 1u); };
+    auto erased_row = [&](uint32_t r) -> bool { return ERASE && ((ebits[r >> 5] >> (r & 31)) & 1u); };
     if (!(a.dbg & 1u)) {   // source strip -> slots: one 32-lane group per row, 4 rows in flight per group
         uint32_t r = grp;
         for (; r + 3 * ngrp < K; r += 4 * ngrp) {
@@ -644,16 +646,23 @@ int launch_encode(const EncArgs& a, uint32_t n_strips, uint32_t n_blocks, uint32
     if ((a.n_waves != 8 && a.n_waves != 16) || a.sd > 32 || lds > 160 * 1024) return (int)hipErrorInvalidValue;
     static bool attr_set = false;  // allow the full 160 KiB of LDS
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)k_encode<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute((const void*)k_encode<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_encode<8, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_encode<16, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_encode<8, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_encode<16, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         (void)hipFuncSetAttribute((const void*)k_solve, hipFuncAttributeMaxDynamicSharedMemorySize, 158 * 1024);
         (void)hipFuncSetAttribute((const void*)k_apply, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_set = true;
     }
-    if (a.n_waves == 16)
-        hipLaunchKernelGGL(k_encode<16>, dim3(n_strips, n_blocks), dim3(16 * 64), lds, (hipStream_t)stream, a);
-    else
-        hipLaunchKernelGGL(k_encode<8>, dim3(n_strips, n_blocks), dim3(8 * 64), lds, (hipStream_t)stream, a);
+    const dim3 grid(n_strips, n_blocks);
+    const bool erase = a.erased_off != nullptr;
+    if (a.n_waves == 16) {
+        if (erase) hipLaunchKernelGGL((k_encode<16, true>), grid, dim3(16 * 64), lds, (hipStream_t)stream, a);
+        else hipLaunchKernelGGL((k_encode<16, false>), grid, dim3(16 * 64), lds, (hipStream_t)stream, a);
+    } else {
+        if (erase) hipLaunchKernelGGL((k_encode<8, true>), grid, dim3(8 * 64), lds, (hipStream_t)stream, a);
+        else hipLaunchKernelGGL((k_encode<8, false>), grid, dim3(8 * 64), lds, (hipStream_t)stream, a);
+    }
     return (int)hipGetLastError();
 }
 
