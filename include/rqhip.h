@@ -125,6 +125,20 @@ int rq_wave_export(uint32_t K, uint32_t sd, uint32_t sizes[4], uint32_t* words, 
 /* Diagnostics: checks the device's packed GF(256) primitives (xtime, table multiply) against
  * host arithmetic on 1024 words x 256 coefficients; the counts of mismatching words. */
 int rq_debug_gf_selftest(uint32_t* bad_xtime, uint32_t* bad_mul);
+/* Diagnostics (host only): build the column program for (K, output ESIs; esi = NULL -> all L
+ * intermediate symbols) and, if src/out are given, evaluate its IR on one block on the host
+ * (src: K x T, out: n_out x T).  stats[0..11] = {nodes, xor2, xor3, xt, xtx, load, store, zero,
+ * u, n_pivots, n_remaining_rows, n_out}. */
+int rq_debug_colprog_eval(uint32_t K, uint32_t T, const uint32_t* esi, uint32_t n_out, const uint8_t* src,
+                          uint8_t* out, uint32_t stats[12]);
+/* Diagnostics (host only): allocate the column program (opts = {n_vgpr, n_agpr, la_load,
+ * la_reload, max_vmem}, 0 = default), emulate the machine program on one block when src/out are
+ * given (checks vmcnt waits and scratch ordering), and optionally return its gfx950 assembly.
+ * stats[0..13] = {instructions, valu, src loads, out stores, spill stores, spill loads, accw,
+ * accr, waits, nops, unprefetched reloads, scratch slots, ir nodes, xtimes}. */
+int rq_debug_colprog_emulate(uint32_t K, uint32_t T, const uint32_t* esi, uint32_t n_out, const uint8_t* src,
+                             uint8_t* out, const uint32_t opts[5], uint32_t stats[16], char* asm_buf, size_t asm_cap,
+                             size_t* asm_len);
 int rq_debug_run_wave_program(uint32_t K, uint32_t T, const uint32_t* words, uint32_t n_words,
                               const uint32_t* wave_off, uint32_t n_levels, uint32_t n_blocks,
                               uint32_t iters, float* ms);

@@ -1,0 +1,575 @@
+// rq_colasm.cpp -- allocation, emission and emulation of the column program (rq_colasm.hpp).
+#include "rq_colasm.hpp"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <deque>
+#include <queue>
+
+namespace rq {
+
+namespace {
+
+constexpr uint32_t INF = 0xFFFFFFFFu;
+inline bool is_agpr(int r) { return r >= REG_A0; }
+
+struct Allocator {
+    const ColIR& ir;
+    const AllocOpts& o;
+    MProg* mp;
+    std::string* err;
+    uint32_t nv = 0;                                // IR nodes
+    std::vector<std::vector<uint32_t>> uses;        // value -> use positions (ascending)
+    std::vector<uint32_t> uptr;
+    std::vector<int16_t> reg;                       // value -> register or -1
+    std::vector<int32_t> slot;                      // value -> scratch slot with a valid copy or -1
+    std::vector<uint8_t> issued;                    // LOAD value already issued
+    int32_t owner[512];
+    uint64_t inflight[512];
+    uint8_t pinned[512];
+    int last_accw[512];                             // instruction index of the last ACCW into an AGPR
+    std::vector<int> freeV, freeA;
+    std::vector<int32_t> free_slots;
+    std::vector<uint64_t> slot_st, slot_ld;         // last store / load seq per slot
+    uint64_t seq = 0, retired = 0;
+    std::deque<std::pair<uint64_t, int>> pend_loads;  // (seq, reg)
+    using HE = std::pair<uint32_t, uint32_t>;       // (next use, value)
+    std::priority_queue<HE, std::vector<HE>, std::greater<HE>> reload_q;
+    bool failed = false;
+
+    Allocator(const ColIR& i, const AllocOpts& op, MProg* m, std::string* e) : ir(i), o(op), mp(m), err(e) {}
+
+    uint32_t nu(uint32_t v) const { return uptr[v] < uses[v].size() ? uses[v][uptr[v]] : INF; }
+
+    void emit(uint8_t op, int d = -1, int a = -1, int b = -1, int c = -1, uint32_t imm = 0) {
+        MInst m;
+        m.op = op; m.d = (int16_t)d; m.a = (int16_t)a; m.b = (int16_t)b; m.c = (int16_t)c; m.imm = imm;
+        mp->ins.push_back(m);
+    }
+    void fail(const char* m) {
+        if (!failed && err) *err = m;
+        failed = true;
+    }
+
+    // ---- vector-memory counters ----
+    void retire_to(uint64_t s) {
+        if (s <= retired) return;
+        retired = s;
+        while (!pend_loads.empty() && pend_loads.front().first <= retired) {
+            const int r = pend_loads.front().second;
+            if (inflight[r] == pend_loads.front().first) inflight[r] = 0;
+            pend_loads.pop_front();
+        }
+    }
+    void wait_seq(uint64_t s) {  // make op `s` complete
+        if (s == 0 || s <= retired) return;
+        const uint64_t n = std::min<uint64_t>(seq - s, 63);
+        emit(MI_WAIT, -1, -1, -1, -1, (uint32_t)n);
+        mp->st.wait++;
+        retire_to(seq - n);
+    }
+    uint64_t issue_vmem() {  // call before emitting a VMEM instruction; returns its seq
+        if (seq - retired >= o.max_vmem) {
+            const uint64_t n = o.max_vmem - 1;
+            emit(MI_WAIT, -1, -1, -1, -1, (uint32_t)n);
+            mp->st.wait++;
+            retire_to(seq - n);
+        }
+        return ++seq;
+    }
+
+    // ---- scratch ----
+    int32_t new_slot() {
+        int32_t s;
+        if (!free_slots.empty()) { s = free_slots.back(); free_slots.pop_back(); }
+        else { s = (int32_t)mp->n_slots++; slot_st.push_back(0); slot_ld.push_back(0); }
+        wait_seq(slot_ld[s]);  // WAR: an older reload of this slot must have read it
+        wait_seq(slot_st[s]);  // WAW
+        return s;
+    }
+    // value in register r -> scratch copy (if none); r becomes free (not pushed to a free list)
+    void spill_out(int r) {
+        const int32_t v = owner[r];
+        if (slot[v] < 0) {
+            const int32_t s = new_slot();
+            const uint64_t q = issue_vmem();
+            emit(MI_SPST, -1, r, -1, -1, (uint32_t)s);
+            mp->st.spst++;
+            slot_st[s] = q;
+            slot[v] = s;
+        }
+        reg[v] = -1;
+        owner[r] = -1;
+        reload_q.push({nu((uint32_t)v), (uint32_t)v});
+    }
+    int victim(int lo, int hi) const {  // max-next-use resident value in [lo, hi), unpinned, not in flight
+        int best = -1;
+        uint32_t bn = 0;
+        for (int r = lo; r < hi; ++r) {
+            const int32_t v = owner[r];
+            if (v < 0 || pinned[r] || inflight[r]) continue;
+            const uint32_t n = nu((uint32_t)v);
+            if (best < 0 || n > bn) { best = r; bn = n; }
+        }
+        return best;
+    }
+    // a VGPR for an operand / result
+    int take_vgpr() {
+        if (!freeV.empty()) { const int r = freeV.back(); freeV.pop_back(); return r; }
+        const int r = victim(0, (int)o.n_vgpr);
+        if (r < 0) { fail("colasm: no evictable VGPR"); return 0; }
+        const uint32_t n = nu((uint32_t)owner[r]);
+        int a = -1;
+        if (!freeA.empty()) { a = freeA.back(); freeA.pop_back(); }
+        else {
+            const int ra = victim(REG_A0, REG_A0 + (int)o.n_agpr);
+            if (ra >= 0 && nu((uint32_t)owner[ra]) > n) { spill_out(ra); a = ra; }
+        }
+        if (a >= 0) {
+            const int32_t v = owner[r];
+            emit(MI_ACCW, a, r);
+            mp->st.accw++;
+            last_accw[a] = (int)mp->ins.size() - 1;
+            owner[a] = v; reg[v] = (int16_t)a; owner[r] = -1;
+        } else {
+            spill_out(r);
+        }
+        return r;
+    }
+    // any register for a value first needed at `need` (prefetch); -1 if not worth it
+    int take_any(uint32_t need) {
+        if (!freeV.empty()) { const int r = freeV.back(); freeV.pop_back(); return r; }
+        if (!freeA.empty()) { const int r = freeA.back(); freeA.pop_back(); return r; }
+        const int rv = victim(0, (int)o.n_vgpr), ra = victim(REG_A0, REG_A0 + (int)o.n_agpr);
+        int r = rv;
+        if (r < 0 || (ra >= 0 && nu((uint32_t)owner[ra]) >= nu((uint32_t)owner[rv]))) r = ra;
+        if (r < 0 || nu((uint32_t)owner[r]) <= need) return -1;
+        spill_out(r);
+        return r;
+    }
+    void release(int r) {
+        owner[r] = -1;
+        (is_agpr(r) ? freeA : freeV).push_back(r);
+    }
+    void kill(uint32_t v) {  // value dead: free register and scratch slot
+        if (reg[v] >= 0) { release(reg[v]); reg[v] = -1; }
+        if (slot[v] >= 0) { free_slots.push_back(slot[v]); slot[v] = -1; }
+    }
+    void reload_into(uint32_t v, int r) {
+        const int32_t s = slot[v];
+        wait_seq(slot_st[s]);
+        const uint64_t q = issue_vmem();
+        emit(MI_SPLD, r, -1, -1, -1, (uint32_t)s);
+        mp->st.spld++;
+        slot_ld[s] = q;
+        inflight[r] = q;
+        pend_loads.push_back({q, r});
+        owner[r] = (int32_t)v; reg[v] = (int16_t)r;
+    }
+    void issue_load(uint32_t v, int r) {
+        const uint64_t q = issue_vmem();
+        emit(MI_LDSRC, r, -1, -1, -1, ir.nodes[v].imm);
+        mp->st.ldsrc++;
+        inflight[r] = q;
+        pend_loads.push_back({q, r});
+        owner[r] = (int32_t)v; reg[v] = (int16_t)r;
+        issued[v] = 1;
+    }
+    // operand v into a VGPR (pinned by the caller)
+    int to_vgpr(uint32_t v) {
+        int r = reg[v];
+        if (r < 0) {  // not prefetched: synchronous reload
+            if (slot[v] < 0) { fail("colasm: value lost"); return 0; }
+            const int t = take_vgpr();
+            reload_into(v, t);
+            mp->st.sync_reload++;
+            r = t;
+        }
+        if (inflight[r]) wait_seq(inflight[r]);
+        if (is_agpr(r)) {
+            pinned[r] = 1;
+            const int t = take_vgpr();
+            pinned[r] = 0;
+            if (last_accw[r] >= (int)mp->ins.size() - 2) emit(MI_NOP, -1, -1, -1, -1, 1);
+            emit(MI_ACCR, t, r);
+            mp->st.accr++;
+            release(r);
+            owner[t] = (int32_t)v; reg[v] = (int16_t)t;
+            r = t;
+        }
+        return r;
+    }
+
+    bool run() {
+        nv = (uint32_t)ir.nodes.size();
+        uses.assign(nv, {});
+        for (uint32_t i = 0; i < nv; ++i) {
+            const IrNode& n = ir.nodes[i];
+            for (uint32_t x : {n.a, n.b, n.c})
+                if (x != NOVAL) uses[x].push_back(i);
+        }
+        uptr.assign(nv, 0);
+        reg.assign(nv, -1);
+        slot.assign(nv, -1);
+        issued.assign(nv, 0);
+        for (int r = 0; r < 512; ++r) { owner[r] = -1; inflight[r] = 0; pinned[r] = 0; last_accw[r] = -100; }
+        for (int r = (int)o.n_vgpr - 1; r >= 0; --r) freeV.push_back(r);
+        for (int r = REG_A0 + (int)o.n_agpr - 1; r >= REG_A0; --r) freeA.push_back(r);
+        std::vector<uint32_t> loads;
+        for (uint32_t i = 0; i < nv; ++i)
+            if (ir.nodes[i].k == IR_LOAD) loads.push_back(i);
+        size_t lp = 0;
+        mp->ins.clear();
+        mp->n_slots = 0;
+        mp->n_out = ir.n_out;
+        mp->K = ir.p.K;
+
+        for (uint32_t i = 0; i < nv && !failed; ++i) {
+            // -- prefetch source rows
+            while (lp < loads.size() && loads[lp] <= i + o.la_load) {
+                const uint32_t v = loads[lp];
+                if (issued[v]) { ++lp; continue; }
+                if (uses[v].empty()) { issued[v] = 1; ++lp; continue; }
+                if (seq - retired >= o.max_vmem && loads[lp] > i) break;
+                const int r = take_any(uses[v][0]);
+                if (r < 0) break;
+                issue_load(v, r);
+                ++lp;
+            }
+            // -- prefetch scratch reloads
+            while (!reload_q.empty() && reload_q.top().first <= i + o.la_reload) {
+                const HE e = reload_q.top();
+                const uint32_t v = e.second;
+                if (reg[v] >= 0 || slot[v] < 0 || nu(v) != e.first) { reload_q.pop(); continue; }
+                if (seq - retired >= o.max_vmem && e.first > i + 8) break;
+                const int r = take_any(e.first);
+                if (r < 0) break;
+                reload_q.pop();
+                reload_into(v, r);
+            }
+            const IrNode& n = ir.nodes[i];
+            switch (n.k) {
+                case IR_LOAD: {
+                    if (!issued[i] && !uses[i].empty()) {
+                        const int r = take_vgpr();
+                        issue_load(i, r);
+                    }
+                    break;
+                }
+                case IR_STORE: {
+                    const uint32_t v = n.a;
+                    int r = reg[v];
+                    if (r < 0) {
+                        if (slot[v] < 0) { fail("colasm: store of a lost value"); break; }
+                        r = take_vgpr();
+                        reload_into(v, r);
+                        mp->st.sync_reload++;
+                    }
+                    if (inflight[r]) wait_seq(inflight[r]);
+                    const uint64_t q = issue_vmem();
+                    (void)q;
+                    emit(MI_STOUT, -1, r, -1, -1, n.imm);
+                    mp->st.stout++;
+                    uptr[v]++;
+                    if (nu(v) == INF) kill(v);
+                    break;
+                }
+                default: {
+                    uint32_t ops[3] = {n.a, n.b, n.c};
+                    int nops = (n.k == IR_ZERO) ? 0 : (n.k == IR_XOR3 ? 3 : (n.k == IR_XT ? 1 : 2));
+                    int rr[3] = {-1, -1, -1};
+                    for (int q = 0; q < nops; ++q)
+                        if (reg[ops[q]] >= 0) pinned[reg[ops[q]]] = 1;
+                    for (int q = 0; q < nops; ++q) {
+                        rr[q] = to_vgpr(ops[q]);
+                        pinned[rr[q]] = 1;
+                    }
+                    // consume uses; find a dying operand register to reuse for the result
+                    int dst = -1;
+                    for (int q = 0; q < nops; ++q) {
+                        const uint32_t v = ops[q];
+                        bool dup = false;
+                        for (int p = 0; p < q; ++p) dup |= (ops[p] == v);
+                        if (dup) continue;
+                        while (uptr[v] < uses[v].size() && uses[v][uptr[v]] == i) uptr[v]++;
+                    }
+                    for (int q = 0; q < nops && dst < 0; ++q)
+                        if (nu(ops[q]) == INF) dst = rr[q];
+                    if (dst < 0) dst = take_vgpr();
+                    pinned[dst] = 1;
+                    uint8_t op = MI_XOR2;
+                    switch (n.k) {
+                        case IR_ZERO: op = MI_ZERO; break;
+                        case IR_XOR2: op = MI_XOR2; break;
+                        case IR_XOR3: op = MI_XOR3; break;
+                        case IR_XT: op = MI_XT; break;
+                        case IR_XTX: op = MI_XTX; break;
+                    }
+                    emit(op, dst, rr[0], rr[1], rr[2]);
+                    mp->st.valu++;
+                    for (int q = 0; q < nops; ++q) {
+                        const uint32_t v = ops[q];
+                        pinned[rr[q]] = 0;
+                        if (nu(v) == INF && reg[v] >= 0) {
+                            if (reg[v] == dst) { reg[v] = -1; owner[dst] = -1; if (slot[v] >= 0) { free_slots.push_back(slot[v]); slot[v] = -1; } }
+                            else kill(v);
+                        }
+                    }
+                    pinned[dst] = 0;
+                    owner[dst] = (int32_t)i; reg[i] = (int16_t)dst;
+                    if (uses[i].empty()) kill(i);
+                    break;
+                }
+            }
+        }
+        return !failed;
+    }
+};
+
+}  // namespace
+
+bool allocate_colprog(const ColIR& ir, const AllocOpts& o, MProg* mp, std::string* err) {
+    *mp = MProg();
+    Allocator a(ir, o, mp, err);
+    return a.run();
+}
+
+bool divmagic(uint32_t d, uint32_t limit, uint32_t* magic, uint32_t* shift) {
+    if (d == 0) return false;
+    for (uint32_t s = 0; s < 32; ++s) {
+        const uint64_t m = (((uint64_t)1 << (32 + s)) + d - 1) / d;
+        if (m > 0xFFFFFFFFull) break;
+        // exact for g < limit if the error term stays below one step
+        const uint64_t e = m * d - ((uint64_t)1 << (32 + s));
+        if ((uint64_t)limit * e < ((uint64_t)1 << (32 + s))) {
+            *magic = (uint32_t)m;
+            *shift = s;
+            return true;
+        }
+    }
+    return false;
+}
+
+// ------------------------------------------------------------------------------------------
+std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
+    std::string s;
+    s.reserve(mp.ins.size() * 48 + 8192);
+    char buf[256];
+    auto R = [&](int r) {
+        static thread_local char b[2][16];
+        static thread_local int k = 0;
+        k ^= 1;
+        std::snprintf(b[k], sizeof b[k], is_agpr(r) ? "a%d" : "v%d", is_agpr(r) ? r - REG_A0 : r);
+        return b[k];
+    };
+    auto line = [&](const char* t) { s += '\t'; s += t; s += '\n'; };
+    s += "\t.amdgcn_target \"amdgcn-amd-amdhsa--gfx950\"\n\t.amdhsa_code_object_version 6\n\t.text\n";
+    s += "\t.globl " + kname + "\n\t.p2align 8\n\t.type " + kname + ",@function\n" + kname + ":\n";
+    const char* pro[] = {
+        "s_load_dwordx8 s[4:11], s[0:1], 0x0",
+        "s_load_dwordx8 s[12:19], s[0:1], 0x20",
+        "s_waitcnt lgkmcnt(0)",
+        "s_lshl_b32 s20, s2, 6",
+        "v_add_u32_e32 v1, s20, v0",
+        "v_cmp_gt_u32_e64 s[22:23], s13, v1",
+        "s_and_b64 exec, exec, s[22:23]",
+        "v_mul_hi_u32 v2, v1, s14",
+        "v_lshrrev_b32_e32 v2, s15, v2",
+        "s_lshr_b32 s21, s12, 2",
+        "v_mul_lo_u32 v3, v2, s21",
+        "v_sub_u32_e32 v3, v1, v3",
+        "v_lshlrev_b32_e32 v3, 2, v3",
+        "v_mul_lo_u32 v4, v2, s10",
+        "v_add_u32_e32 v255, v4, v3",
+        "v_mul_lo_u32 v4, v2, s11",
+        "v_add_u32_e32 v254, v4, v3",
+        "v_lshlrev_b32_e32 v253, 2, v0",
+        "s_mov_b32 s24, s4",
+        "s_and_b32 s25, s5, 0xffff",
+        "s_mov_b32 s26, -1",
+        "s_mov_b32 s27, 0x20000",
+        "s_mov_b32 s28, s6",
+        "s_and_b32 s29, s7, 0xffff",
+        "s_mov_b32 s30, -1",
+        "s_mov_b32 s31, 0x20000",
+        "s_mul_i32 s32, s2, s16",
+        "s_mul_hi_u32 s33, s2, s16",
+        "s_add_u32 s32, s8, s32",
+        "s_addc_u32 s33, s9, s33",
+        "s_and_b32 s33, s33, 0xffff",
+        "s_mov_b32 s34, -1",
+        "s_mov_b32 s35, 0x20000",
+        "s_mov_b32 s36, 0x090b080a",
+        "s_mov_b32 s37, 0xfefefefe",
+        "s_mov_b32 s38, 0x1d1d1d1d",
+    };
+    for (const char* p : pro) line(p);
+    int sr = 0;
+    auto srot = [&]() { sr = (sr + 1) & 7; return 40 + sr; };
+    for (const MInst& m : mp.ins) {
+        switch (m.op) {
+            case MI_XOR2:
+                std::snprintf(buf, sizeof buf, "v_xor_b32_e32 v%d, v%d, v%d", m.d, m.a, m.b); line(buf); break;
+            case MI_XOR3:
+                std::snprintf(buf, sizeof buf, "v_bitop3_b32 v%d, v%d, v%d, v%d bitop3:0x96", m.d, m.a, m.b, m.c); line(buf); break;
+            case MI_XT:
+            case MI_XTX:
+                std::snprintf(buf, sizeof buf, "v_lshlrev_b32_e32 v%d, 8, v%d", V_T1, m.a); line(buf);
+                std::snprintf(buf, sizeof buf, "v_perm_b32 v%d, v%d, v%d, s36", V_T1, V_T1, m.a); line(buf);
+                std::snprintf(buf, sizeof buf, "v_and_b32_e32 v%d, s38, v%d", V_T1, V_T1); line(buf);
+                std::snprintf(buf, sizeof buf, "v_lshlrev_b32_e32 v%d, 1, v%d", V_T2, m.a); line(buf);
+                std::snprintf(buf, sizeof buf, "v_and_b32_e32 v%d, s37, v%d", V_T2, V_T2); line(buf);
+                if (m.op == MI_XT) std::snprintf(buf, sizeof buf, "v_xor_b32_e32 v%d, v%d, v%d", m.d, V_T1, V_T2);
+                else std::snprintf(buf, sizeof buf, "v_bitop3_b32 v%d, v%d, v%d, v%d bitop3:0x96", m.d, V_T1, V_T2, m.b);
+                line(buf);
+                break;
+            case MI_ZERO:
+                std::snprintf(buf, sizeof buf, "v_mov_b32_e32 v%d, 0", m.d); line(buf); break;
+            case MI_LDSRC: {
+                const int q = srot();
+                std::snprintf(buf, sizeof buf, "s_mul_i32 s%d, s12, %u", q, m.imm); line(buf);
+                std::snprintf(buf, sizeof buf, "buffer_load_dword %s, v%d, s[24:27], s%d offen", R(m.d), V_SRCOFF, q); line(buf);
+                break;
+            }
+            case MI_STOUT: {
+                const int q = srot();
+                std::snprintf(buf, sizeof buf, "s_mul_i32 s%d, s12, %u", q, m.imm); line(buf);
+                std::snprintf(buf, sizeof buf, "buffer_store_dword %s, v%d, s[28:31], s%d offen", R(m.a), V_OUTOFF, q); line(buf);
+                break;
+            }
+            case MI_SPST: {
+                const int q = srot();
+                std::snprintf(buf, sizeof buf, "s_mov_b32 s%d, %u", q, m.imm * 256u); line(buf);
+                std::snprintf(buf, sizeof buf, "buffer_store_dword %s, v%d, s[32:35], s%d offen", R(m.a), V_SCROFF, q); line(buf);
+                break;
+            }
+            case MI_SPLD: {
+                const int q = srot();
+                std::snprintf(buf, sizeof buf, "s_mov_b32 s%d, %u", q, m.imm * 256u); line(buf);
+                std::snprintf(buf, sizeof buf, "buffer_load_dword %s, v%d, s[32:35], s%d offen sc1", R(m.d), V_SCROFF, q); line(buf);
+                break;
+            }
+            case MI_ACCW:
+                std::snprintf(buf, sizeof buf, "v_accvgpr_write_b32 %s, v%d", R(m.d), m.a); line(buf); break;
+            case MI_ACCR:
+                std::snprintf(buf, sizeof buf, "v_accvgpr_read_b32 v%d, %s", m.d, R(m.a)); line(buf); break;
+            case MI_WAIT:
+                std::snprintf(buf, sizeof buf, "s_waitcnt vmcnt(%u)", m.imm); line(buf); break;
+            case MI_NOP:
+                std::snprintf(buf, sizeof buf, "s_nop %u", m.imm); line(buf); break;
+        }
+    }
+    s += ".Lend:\n\ts_endpgm\n";
+    s += ".Lfunc_end:\n\t.size " + kname + ", .Lfunc_end-" + kname + "\n";
+    s += "\t.p2alignl 6, 3212836864\n\t.fill 256, 4, 3212836864\n";
+    s += "\t.section .rodata,\"a\",@progbits\n\t.p2align 6, 0x0\n\t.amdhsa_kernel " + kname + "\n";
+    s += "\t\t.amdhsa_group_segment_fixed_size 0\n\t\t.amdhsa_private_segment_fixed_size 0\n";
+    s += "\t\t.amdhsa_kernarg_size 64\n\t\t.amdhsa_user_sgpr_count 2\n";
+    s += "\t\t.amdhsa_user_sgpr_kernarg_segment_ptr 1\n\t\t.amdhsa_system_sgpr_workgroup_id_x 1\n";
+    s += "\t\t.amdhsa_system_vgpr_workitem_id 0\n\t\t.amdhsa_next_free_vgpr 512\n";
+    s += "\t\t.amdhsa_next_free_sgpr 56\n\t\t.amdhsa_accum_offset 256\n\t\t.amdhsa_reserve_vcc 0\n";
+    s += "\t\t.amdhsa_ieee_mode 0\n\t\t.amdhsa_dx10_clamp 0\n\t.end_amdhsa_kernel\n\t.text\n";
+    s += "\t.amdgpu_metadata\n---\namdhsa.kernels:\n  - .agpr_count: 256\n    .args:\n";
+    s += "      - .offset: 0\n        .size: 64\n        .value_kind: by_value\n";
+    s += "    .group_segment_fixed_size: 0\n    .kernarg_segment_align: 8\n    .kernarg_segment_size: 64\n";
+    s += "    .max_flat_workgroup_size: 64\n    .name: " + kname + "\n    .private_segment_fixed_size: 0\n";
+    s += "    .sgpr_count: 56\n    .symbol: " + kname + ".kd\n    .vgpr_count: 512\n    .wavefront_size: 64\n";
+    s += "amdhsa.target: amdgcn-amd-amdhsa--gfx950\namdhsa.version:\n  - 1\n  - 2\n...\n\t.end_amdgpu_metadata\n";
+    return s;
+}
+
+// ------------------------------------------------------------------------------------------
+namespace {
+inline uint32_t xtime4(uint32_t x) {
+    const uint32_t hi = (x >> 7) & 0x01010101u;
+    return ((x & 0x7F7F7F7Fu) << 1) ^ (hi * 0x1Du);
+}
+}  // namespace
+
+bool emulate_colprog(const MProg& mp, const uint8_t* src, uint32_t T, uint8_t* out, std::string* err) {
+    const uint32_t Td = T / 4;
+    std::vector<std::vector<uint32_t>> R(512, std::vector<uint32_t>(Td, 0));
+    std::vector<std::vector<uint32_t>> scr(mp.n_slots, std::vector<uint32_t>(Td, 0));
+    std::vector<uint64_t> pend(512, 0), slot_st(mp.n_slots, 0);
+    uint64_t seq = 0, retired = 0;
+    char buf[160];
+    auto bad = [&](size_t i, const char* what) {
+        std::snprintf(buf, sizeof buf, "emulate: instruction %zu: %s", i, what);
+        if (err) *err = buf;
+        return false;
+    };
+    for (size_t i = 0; i < mp.ins.size(); ++i) {
+        const MInst& m = mp.ins[i];
+        auto ready = [&](int r) { return r < 0 || pend[r] == 0 || pend[r] <= retired; };
+        if (!ready(m.a) || !ready(m.b) || !ready(m.c)) return bad(i, "operand read before its load completed");
+        if (m.d >= 0 && !ready(m.d)) return bad(i, "register overwritten while a load into it is pending");
+        auto vmem = [&]() {
+            ++seq;
+            if (seq - retired > 63) return false;
+            return true;
+        };
+        switch (m.op) {
+            case MI_XOR2:
+                for (uint32_t c = 0; c < Td; ++c) R[m.d][c] = R[m.a][c] ^ R[m.b][c];
+                break;
+            case MI_XOR3:
+                for (uint32_t c = 0; c < Td; ++c) R[m.d][c] = R[m.a][c] ^ R[m.b][c] ^ R[m.c][c];
+                break;
+            case MI_XT:
+                for (uint32_t c = 0; c < Td; ++c) R[m.d][c] = xtime4(R[m.a][c]);
+                break;
+            case MI_XTX: {
+                for (uint32_t c = 0; c < Td; ++c) R[m.d][c] = xtime4(R[m.a][c]) ^ R[m.b][c];
+                break;
+            }
+            case MI_ZERO:
+                std::fill(R[m.d].begin(), R[m.d].end(), 0u);
+                break;
+            case MI_LDSRC:
+                if (m.imm >= mp.K) return bad(i, "source row >= K");
+                std::memcpy(R[m.d].data(), src + (size_t)m.imm * T, (size_t)Td * 4);
+                if (!vmem()) return bad(i, "more than 63 vector-memory operations outstanding");
+                pend[m.d] = seq;
+                break;
+            case MI_STOUT:
+                if (m.imm >= mp.n_out) return bad(i, "output index out of range");
+                std::memcpy(out + (size_t)m.imm * T, R[m.a].data(), (size_t)Td * 4);
+                if (!vmem()) return bad(i, "more than 63 vector-memory operations outstanding");
+                break;
+            case MI_SPST:
+                scr[m.imm] = R[m.a];
+                if (!vmem()) return bad(i, "more than 63 vector-memory operations outstanding");
+                slot_st[m.imm] = seq;
+                break;
+            case MI_SPLD:
+                if (slot_st[m.imm] > retired) return bad(i, "reload of a slot whose store is still in flight");
+                R[m.d] = scr[m.imm];
+                if (!vmem()) return bad(i, "more than 63 vector-memory operations outstanding");
+                pend[m.d] = seq;
+                break;
+            case MI_ACCW:
+                if (m.d < REG_A0 || m.a >= REG_A0) return bad(i, "accvgpr_write operands");
+                R[m.d] = R[m.a];
+                break;
+            case MI_ACCR:
+                if (m.d >= REG_A0 || m.a < REG_A0) return bad(i, "accvgpr_read operands");
+                R[m.d] = R[m.a];
+                break;
+            case MI_WAIT:
+                if (seq > m.imm) retired = std::max(retired, seq - m.imm);
+                break;
+            case MI_NOP:
+                break;
+        }
+        if ((m.op == MI_XOR2 || m.op == MI_XOR3 || m.op == MI_XT || m.op == MI_XTX || m.op == MI_ZERO) &&
+            (m.d >= REG_A0 || m.a >= REG_A0 || m.b >= REG_A0 || m.c >= REG_A0))
+            return bad(i, "VALU operand in an AGPR");
+        if ((m.op <= MI_ZERO) && (m.d >= V_ALLOC || (m.a >= V_ALLOC && m.a < REG_A0) || (m.b >= V_ALLOC && m.b < REG_A0) ||
+                                  (m.c >= V_ALLOC && m.c < REG_A0)))
+            return bad(i, "VALU operand in a reserved VGPR");
+    }
+    return true;
+}
+
+}  // namespace rq

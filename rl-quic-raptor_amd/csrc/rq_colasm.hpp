@@ -1,0 +1,88 @@
+// rq_colasm.hpp -- register allocation, gfx950 assembly emission and CPU emulation of the
+// column program (rq_colprog.hpp).
+//
+// Storage tiers of a value (one dword per lane): arch VGPR (operand of a VALU op), AGPR (one
+// v_accvgpr_read/write away; also a direct target/source of buffer loads/stores), and a per-wave
+// global scratch slot (256 B per value, L2/MALL-resident in practice).  Allocation is Belady's
+// furthest-next-use rule over the straight-line program; source-row loads and scratch reloads
+// are issued ahead of their use (look-ahead windows) and waited for with exact vmcnt counts.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "rq_colprog.hpp"
+
+namespace rq {
+
+enum MOp : uint8_t {
+    MI_XOR2 = 0, MI_XOR3, MI_XT, MI_XTX, MI_ZERO,
+    MI_LDSRC,   // d <- source row imm (buffer_load; d is a VGPR or an AGPR)
+    MI_STOUT,   // output row imm <- a
+    MI_SPST,    // scratch slot imm <- a
+    MI_SPLD,    // d <- scratch slot imm
+    MI_ACCW,    // AGPR d <- VGPR a
+    MI_ACCR,    // VGPR d <- AGPR a
+    MI_WAIT,    // s_waitcnt vmcnt(imm)
+    MI_NOP,     // s_nop imm
+};
+
+constexpr int REG_A0 = 256;       // register ids: 0..255 VGPR, 256..511 AGPR
+constexpr int V_SRCOFF = 255, V_OUTOFF = 254, V_SCROFF = 253, V_T1 = 252, V_T2 = 251;
+constexpr int V_ALLOC = 251;      // v0..v250 are allocatable
+
+struct MInst {
+    uint8_t op = MI_NOP;
+    int16_t d = -1, a = -1, b = -1, c = -1;
+    uint32_t imm = 0;
+};
+
+struct AllocOpts {
+    uint32_t n_vgpr = V_ALLOC;   // allocatable VGPRs (<= V_ALLOC)
+    uint32_t n_agpr = 256;       // allocatable AGPRs
+    uint32_t la_load = 320;      // look-ahead (IR nodes) for source-row loads
+    uint32_t la_reload = 160;    // look-ahead (IR nodes) for scratch reloads
+    uint32_t max_vmem = 56;      // outstanding vector-memory operations per wave
+};
+
+struct MProg {
+    std::vector<MInst> ins;
+    uint32_t n_slots = 0;        // scratch slots per wave (256 B each)
+    uint32_t n_out = 0;
+    uint32_t K = 0;
+    struct Stats {
+        uint32_t valu = 0, ldsrc = 0, stout = 0, spst = 0, spld = 0, accw = 0, accr = 0, wait = 0, nop = 0;
+        uint32_t sync_reload = 0;  // reloads that were not prefetched
+    } st;
+};
+
+bool allocate_colprog(const ColIR& ir, const AllocOpts& o, MProg* mp, std::string* err);
+
+// Kernel argument block of the emitted kernel (must match the prologue in emit_colprog_asm).
+struct ColKernArgs {
+    uint64_t src;         // block b row i at src + b*src_stride + i*T
+    uint64_t out;         // output r of block b at out + b*out_stride + r*T
+    uint64_t scratch;     // per-wave scratch: n_slots * 256 bytes per workgroup
+    uint32_t src_stride;  // bytes (< 4 GiB spans: the host splits larger batches)
+    uint32_t out_stride;
+    uint32_t T;           // bytes, multiple of 4
+    uint32_t n_cols;      // n_blocks * T/4
+    uint32_t magic, shift;  // b = mulhi(g, magic) >> shift == g / (T/4) for g < n_cols
+    uint32_t scr_per_wave;  // bytes
+    uint32_t pad[3];
+};
+static_assert(sizeof(ColKernArgs) == 64, "kernarg layout");
+
+std::string emit_colprog_asm(const MProg& mp, const std::string& kname);
+
+// Executes the machine program on the host for one block (T/4 lanes), checking vmcnt waits and
+// scratch ordering as it goes.  Test infrastructure for the allocator, not a product path.
+bool emulate_colprog(const MProg& mp, const uint8_t* src, uint32_t T, uint8_t* out, std::string* err);
+
+// In-process assembly (amd_comgr, rq_comgr.cpp): assembly text -> gfx950 code object.
+bool comgr_assemble(const std::string& src, std::vector<char>* co, std::string* err);
+
+// magic/shift such that (uint64(g) * magic) >> (32 + shift) == g / d for all g < limit.
+bool divmagic(uint32_t d, uint32_t limit, uint32_t* magic, uint32_t* shift);
+
+}  // namespace rq

@@ -1,0 +1,545 @@
+// rq_colprog.cpp -- builds the column program IR (see rq_colprog.hpp).
+//
+// Constraint system (RQ/solver.go:25-65, RQ/params.go:116-160):
+//   S LDPC rows (circulant B part, identity on B..B+S-1, two PI columns), rhs 0
+//   K' LT rows (ISI 0..K'-1), rhs = zero-padded source symbol
+//   H HDPC rows [MT*Gamma | I_H], rhs 0
+// Elimination: peeling with inactivation over the sparse GF(2) rows (cf. RQ/inactivate.go:25-170),
+// then a dense solve on the u inactive columns (replaces RQ/discmath/gauss.go:7-45).
+#include "rq_colprog.hpp"
+
+#include <algorithm>
+#include <cstring>
+
+namespace rq {
+
+namespace {
+
+using Bits = std::vector<uint64_t>;
+
+struct Elim {
+    uint32_t L = 0, S = 0, H = 0, Kp = 0, W = 0, P = 0, KS = 0, NR = 0;
+    std::vector<std::vector<uint32_t>> rows;    // GF(2) rows: LDPC 0..S-1, LT S..S+K'-1
+    std::vector<uint8_t> cstate;                // 1 pivoted, 2 inactive
+    std::vector<uint32_t> piv_row, piv_col;     // peeling order
+    std::vector<int32_t> col_order;             // column -> pivot index or -1
+    std::vector<std::vector<uint32_t>> deps;    // pivot -> earlier pivots in its row
+    std::vector<uint32_t> ucols;                // inactive columns
+    std::vector<int32_t> uidx;                  // column -> index in ucols or -1
+    std::vector<uint32_t> rem;                  // remaining (unpeeled) GF(2) rows
+    uint32_t u = 0, nw = 0;
+    std::vector<uint64_t> Wb;                   // npiv x nw: C[c_k] = y_k ^ W_k * C_U
+    const uint64_t* wrow(uint32_t k) const { return &Wb[(size_t)k * nw]; }
+    // HDPC: G[h][j] = sum_{i>=j} MT[h][i] alpha^(i-j); ma/mb = the two ones of MT column j
+    std::vector<uint8_t> G, ma, mb;
+    // dense solve
+    uint32_t n2 = 0;
+    std::vector<int32_t> pc_of_row;             // rem row i -> U index of its pivot column
+    std::vector<uint32_t> fcols;                // H free U indices
+    std::vector<Bits> E2, R;                    // n2 x n2, n2 x H (GF(2))
+    std::vector<uint8_t> Zi;                    // H x H GF(256)
+    std::vector<uint8_t> Q;                     // H x n2 GF(256): C_F = Zi*bh ^ Q*b2
+};
+
+inline bool bit(const uint64_t* b, uint32_t i) { return (b[i >> 6] >> (i & 63)) & 1; }
+inline void flip(uint64_t* b, uint32_t i) { b[i >> 6] ^= 1ull << (i & 63); }
+
+bool eliminate(const Params& p, Elim* e, std::string* err) {
+    const GF& g = gf();
+    e->L = p.L; e->S = p.S; e->H = p.H; e->Kp = p.Kp; e->W = p.W; e->P = p.P;
+    const uint32_t L = p.L, S = p.S, H = p.H, W = p.W, P = p.P, KS = p.Kp + p.S, NR = p.S + p.Kp;
+    e->KS = KS; e->NR = NR;
+    auto& rows = e->rows;
+    rows.assign(NR, {});
+    for (uint32_t i = 0; i < p.B; ++i) {
+        const uint32_t a = 1 + i / S;
+        uint32_t r = i % S;
+        rows[r].push_back(i);
+        r = (r + a) % S; rows[r].push_back(i);
+        r = (r + a) % S; rows[r].push_back(i);
+    }
+    for (uint32_t i = 0; i < S; ++i) {
+        rows[i].push_back(p.B + i);
+        rows[i].push_back(W + (i % P));
+        rows[i].push_back(W + ((i + 1) % P));
+    }
+    uint32_t cols[64];
+    for (uint32_t i = 0; i < p.Kp; ++i) {
+        const int n = lt_cols(p, i, cols);
+        rows[S + i].assign(cols, cols + n);
+    }
+    for (auto& r : rows) {  // Set(...,1) semantics: duplicates are idempotent
+        std::sort(r.begin(), r.end());
+        r.erase(std::unique(r.begin(), r.end()), r.end());
+    }
+    std::vector<std::vector<uint32_t>> col_rows(L);
+    for (uint32_t r = 0; r < NR; ++r)
+        for (uint32_t c : rows[r]) col_rows[c].push_back(r);
+
+    // ---- peeling with inactivation: take a row of minimum active degree (FIFO per degree);
+    // its pivot is the active column with the most unfinished rows, the others go inactive.
+    enum : uint8_t { ACTIVE = 0, PIVOTED = 1, INACTIVE = 2 };
+    auto& cstate = e->cstate;
+    cstate.assign(L, ACTIVE);
+    for (uint32_t c = W; c < L; ++c) cstate[c] = INACTIVE;  // PI columns start inactive
+    std::vector<uint32_t> cnt(NR, 0);
+    std::vector<uint8_t> rdone(NR, 0);
+    for (uint32_t r = 0; r < NR; ++r)
+        for (uint32_t c : rows[r]) cnt[r] += (cstate[c] == ACTIVE);
+    std::vector<uint32_t> live_deg(L, 0);
+    for (uint32_t c = 0; c < L; ++c) live_deg[c] = (uint32_t)col_rows[c].size();
+    std::vector<std::vector<uint32_t>> bucket(64);
+    std::vector<size_t> bhead(64, 0);
+    for (uint32_t r = 0; r < NR; ++r) bucket[std::min<uint32_t>(cnt[r], 63)].push_back(r);
+    e->ucols.clear();
+    for (uint32_t c = W; c < L; ++c) e->ucols.push_back(c);
+    e->col_order.assign(L, -1);
+    auto drop_col = [&](uint32_t c, uint32_t except_row) {
+        for (uint32_t r : col_rows[c]) {
+            if (rdone[r] || r == except_row) continue;
+            --cnt[r];
+            bucket[std::min<uint32_t>(cnt[r], 63)].push_back(r);
+        }
+    };
+    for (;;) {
+        int32_t r = -1;
+        for (uint32_t b = 1; b < 64 && r < 0; ++b) {
+            auto& bk = bucket[b];
+            while (bhead[b] < bk.size()) {
+                const uint32_t x = bk[bhead[b]++];
+                if (!rdone[x] && std::min<uint32_t>(cnt[x], 63) == b) { r = (int32_t)x; break; }
+            }
+        }
+        if (r < 0) break;
+        uint32_t best = UINT32_MAX, best_deg = 0;
+        for (uint32_t c : rows[r])
+            if (cstate[c] == ACTIVE && (best == UINT32_MAX || live_deg[c] > best_deg)) { best = c; best_deg = live_deg[c]; }
+        for (uint32_t c : rows[r]) {
+            if (cstate[c] != ACTIVE || c == best) continue;
+            cstate[c] = INACTIVE;
+            e->ucols.push_back(c);
+            drop_col(c, UINT32_MAX);
+        }
+        cstate[best] = PIVOTED;
+        e->col_order[best] = (int32_t)e->piv_col.size();
+        e->piv_row.push_back((uint32_t)r);
+        e->piv_col.push_back(best);
+        rdone[r] = 1;
+        drop_col(best, (uint32_t)r);
+        for (uint32_t c : rows[r]) --live_deg[c];
+    }
+    for (uint32_t c = 0; c < L; ++c)
+        if (cstate[c] == ACTIVE) { cstate[c] = INACTIVE; e->ucols.push_back(c); }
+    const uint32_t u = e->u = (uint32_t)e->ucols.size();
+    const uint32_t npiv = (uint32_t)e->piv_col.size();
+    for (uint32_t r = 0; r < NR; ++r)
+        if (!rdone[r]) e->rem.push_back(r);
+    const uint32_t n2 = e->n2 = (uint32_t)e->rem.size();
+    if (n2 + H != u) { if (err) *err = "colprog: remaining rows != inactive columns"; return false; }
+    e->uidx.assign(L, -1);
+    for (uint32_t j = 0; j < u; ++j) e->uidx[e->ucols[j]] = (int32_t)j;
+
+    // ---- forward-substitution structure and W (C[c_k] = y_k ^ W_k C_U)
+    const uint32_t nw = e->nw = (u + 63) / 64;
+    e->Wb.assign((size_t)npiv * nw, 0);
+    e->deps.assign(npiv, {});
+    for (uint32_t k = 0; k < npiv; ++k) {
+        uint64_t* wk = &e->Wb[(size_t)k * nw];
+        for (uint32_t c : rows[e->piv_row[k]]) {
+            if (c == e->piv_col[k]) continue;
+            if (cstate[c] == PIVOTED) {
+                const uint32_t j = (uint32_t)e->col_order[c];
+                e->deps[k].push_back(j);
+                const uint64_t* wd = e->wrow(j);
+                for (uint32_t x = 0; x < nw; ++x) wk[x] ^= wd[x];
+            } else {
+                flip(wk, (uint32_t)e->uidx[c]);
+            }
+        }
+    }
+
+    // ---- HDPC coefficients
+    e->ma.assign(KS, 0); e->mb.assign(KS, 0);
+    for (uint32_t j = 0; j + 1 < KS; ++j) {
+        const uint32_t a = rand_(j + 1, 6, H);
+        e->ma[j] = (uint8_t)a;
+        e->mb[j] = (uint8_t)((a + rand_(j + 1, 7, H - 1) + 1) % H);
+    }
+    auto MT = [&](uint32_t h, uint32_t j) -> uint8_t {
+        if (j == KS - 1) return g.pow_alpha(h);
+        return (e->ma[j] == h || e->mb[j] == h) ? 1 : 0;
+    };
+    e->G.assign((size_t)H * KS, 0);
+    for (uint32_t h = 0; h < H; ++h) {
+        uint8_t acc = 0;
+        for (int64_t j = (int64_t)KS - 1; j >= 0; --j) {
+            acc = (uint8_t)(g.mul(acc, 2) ^ MT(h, (uint32_t)j));
+            e->G[(size_t)h * KS + j] = acc;
+        }
+    }
+
+    // ---- dense matrix Mu (u x u): rem rows (GF(2)) then HDPC rows (GF(256))
+    std::vector<uint8_t> Mu((size_t)u * u, 0);
+    for (uint32_t i = 0; i < n2; ++i) {
+        std::vector<uint64_t> acc(nw, 0);
+        for (uint32_t c : rows[e->rem[i]]) {
+            if (cstate[c] == PIVOTED) {
+                const uint64_t* wd = e->wrow((uint32_t)e->col_order[c]);
+                for (uint32_t x = 0; x < nw; ++x) acc[x] ^= wd[x];
+            } else {
+                flip(acc.data(), (uint32_t)e->uidx[c]);
+            }
+        }
+        for (uint32_t j = 0; j < u; ++j) Mu[(size_t)i * u + j] = bit(acc.data(), j);
+    }
+    for (uint32_t h = 0; h < H; ++h) {
+        uint8_t* mrow = &Mu[(size_t)(n2 + h) * u];
+        for (uint32_t j = 0; j < u; ++j) {
+            const uint32_t c = e->ucols[j];
+            uint8_t v = (c < KS) ? e->G[(size_t)h * KS + c] : 0;
+            if (c == KS + h) v ^= 1;
+            mrow[j] = v;
+        }
+        for (uint32_t k = 0; k < npiv; ++k) {
+            const uint8_t gc = e->G[(size_t)h * KS + e->piv_col[k]];
+            if (!gc) continue;
+            const uint64_t* wk = e->wrow(k);
+            for (uint32_t j = 0; j < u; ++j)
+                if (bit(wk, j)) mrow[j] ^= gc;
+        }
+    }
+    auto mu = [&](uint32_t r, uint32_t c) -> uint8_t { return Mu[(size_t)r * u + c]; };
+
+    // ---- GF(2) Gauss-Jordan on [Mu2 | I]: pivot columns Pc, E2 = Mu2[:,Pc]^-1, R = E2 Mu2[:,Fc]
+    const uint32_t bw = (u + n2 + 63) / 64;
+    std::vector<uint64_t> aug((size_t)n2 * bw, 0);
+    for (uint32_t i = 0; i < n2; ++i) {
+        uint64_t* ar = &aug[(size_t)i * bw];
+        for (uint32_t j = 0; j < u; ++j)
+            if (mu(i, j)) flip(ar, j);
+        flip(ar, u + i);
+    }
+    e->pc_of_row.assign(n2, -1);
+    std::vector<uint8_t> is_pc(u, 0);
+    for (uint32_t i = 0; i < n2; ++i) {
+        uint64_t* ai = &aug[(size_t)i * bw];
+        int32_t jc = -1;
+        for (uint32_t j = 0; j < u; ++j)
+            if (!is_pc[j] && bit(ai, j)) { jc = (int32_t)j; break; }
+        if (jc < 0) { if (err) *err = "colprog: singular GF(2) block"; return false; }
+        e->pc_of_row[i] = jc;
+        is_pc[jc] = 1;
+        for (uint32_t q = 0; q < n2; ++q) {
+            uint64_t* aq = &aug[(size_t)q * bw];
+            if (q != i && bit(aq, (uint32_t)jc))
+                for (uint32_t x = 0; x < bw; ++x) aq[x] ^= ai[x];
+        }
+    }
+    for (uint32_t j = 0; j < u; ++j)
+        if (!is_pc[j]) e->fcols.push_back(j);
+    if (e->fcols.size() != H) { if (err) *err = "colprog: free column count != H"; return false; }
+    const uint32_t nb2 = (n2 + 63) / 64, nbh = (H + 63) / 64;
+    e->E2.assign(n2, Bits(nb2, 0));
+    e->R.assign(n2, Bits(nbh, 0));
+    for (uint32_t i = 0; i < n2; ++i) {
+        const uint64_t* ai = &aug[(size_t)i * bw];
+        for (uint32_t m = 0; m < n2; ++m)
+            if (bit(ai, u + m)) flip(e->E2[i].data(), m);
+        for (uint32_t f = 0; f < H; ++f)
+            if (bit(ai, e->fcols[f])) flip(e->R[i].data(), f);
+    }
+    // Z = Mh[:,Fc] ^ Mh[:,Pc] R, Zi = Z^-1 (GF(256) Gauss-Jordan)
+    std::vector<uint8_t> Z((size_t)H * H, 0), Zi((size_t)H * H, 0);
+    for (uint32_t h = 0; h < H; ++h)
+        for (uint32_t f = 0; f < H; ++f) {
+            uint8_t z = mu(n2 + h, e->fcols[f]);
+            for (uint32_t i = 0; i < n2; ++i)
+                if (bit(e->R[i].data(), f)) z ^= mu(n2 + h, (uint32_t)e->pc_of_row[i]);
+            Z[(size_t)h * H + f] = z;
+        }
+    for (uint32_t i = 0; i < H; ++i) Zi[(size_t)i * H + i] = 1;
+    for (uint32_t c = 0; c < H; ++c) {
+        uint32_t pr = H;
+        for (uint32_t r = c; r < H; ++r)
+            if (Z[(size_t)r * H + c]) { pr = r; break; }
+        if (pr == H) { if (err) *err = "colprog: singular HDPC block"; return false; }
+        for (uint32_t x = 0; x < H; ++x) {
+            std::swap(Z[(size_t)pr * H + x], Z[(size_t)c * H + x]);
+            std::swap(Zi[(size_t)pr * H + x], Zi[(size_t)c * H + x]);
+        }
+        const uint8_t inv = g.inv(Z[(size_t)c * H + c]);
+        for (uint32_t x = 0; x < H; ++x) {
+            Z[(size_t)c * H + x] = g.mul(Z[(size_t)c * H + x], inv);
+            Zi[(size_t)c * H + x] = g.mul(Zi[(size_t)c * H + x], inv);
+        }
+        for (uint32_t r = 0; r < H; ++r) {
+            const uint8_t f = Z[(size_t)r * H + c];
+            if (r == c || !f) continue;
+            for (uint32_t x = 0; x < H; ++x) {
+                Z[(size_t)r * H + x] ^= g.mul(f, Z[(size_t)c * H + x]);
+                Zi[(size_t)r * H + x] ^= g.mul(f, Zi[(size_t)c * H + x]);
+            }
+        }
+    }
+    e->Zi = Zi;
+    // Q = Zi * Mh[:,Pc] * E2  (H x n2)
+    std::vector<uint8_t> MP((size_t)H * n2, 0);  // Mh[:,Pc] E2
+    for (uint32_t h = 0; h < H; ++h)
+        for (uint32_t m = 0; m < n2; ++m) {
+            uint8_t v = 0;
+            for (uint32_t i = 0; i < n2; ++i)
+                if (bit(e->E2[i].data(), m)) v ^= mu(n2 + h, (uint32_t)e->pc_of_row[i]);
+            MP[(size_t)h * n2 + m] = v;
+        }
+    e->Q.assign((size_t)H * n2, 0);
+    for (uint32_t f = 0; f < H; ++f)
+        for (uint32_t m = 0; m < n2; ++m) {
+            uint8_t v = 0;
+            for (uint32_t h = 0; h < H; ++h) v ^= g.mul(Zi[(size_t)f * H + h], MP[(size_t)h * n2 + m]);
+            e->Q[(size_t)f * n2 + m] = v;
+        }
+    return true;
+}
+
+// ---- IR construction helpers ----
+struct Builder {
+    ColIR* ir;
+    uint32_t add(uint8_t k, uint32_t a = NOVAL, uint32_t b = NOVAL, uint32_t c = NOVAL, uint32_t imm = 0) {
+        IrNode n;
+        n.k = k; n.a = a; n.b = b; n.c = c; n.imm = imm;
+        ir->nodes.push_back(n);
+        return (uint32_t)ir->nodes.size() - 1;
+    }
+    // XOR of a term list (NOVAL = zero terms are skipped); NOVAL if every term is zero.
+    uint32_t xsum(const std::vector<uint32_t>& terms) {
+        uint32_t acc = NOVAL;
+        std::vector<uint32_t> t;
+        for (uint32_t v : terms)
+            if (v != NOVAL) t.push_back(v);
+        size_t i = 0;
+        if (t.empty()) return NOVAL;
+        if (t.size() == 1) return t[0];
+        if (t.size() % 2 == 0) { acc = add(IR_XOR2, t[0], t[1]); i = 2; }
+        else { acc = t[0]; i = 1; }
+        for (; i < t.size(); i += 2) acc = add(IR_XOR3, acc, t[i], t[i + 1]);
+        return acc;
+    }
+    uint32_t xt(uint32_t a, uint32_t b = NOVAL) {  // alpha*a ^ b
+        if (a == NOVAL) return b;
+        return b == NOVAL ? add(IR_XT, a) : add(IR_XTX, a, b);
+    }
+};
+
+// Accumulator: pushes are XORed in pairs (one XOR3 per two pushes).
+struct Acc {
+    uint32_t val = NOVAL, pend = NOVAL;
+    void push(Builder& B, uint32_t v) {
+        if (v == NOVAL) return;
+        if (val == NOVAL) { val = v; return; }
+        if (pend == NOVAL) { pend = v; return; }
+        val = B.add(IR_XOR3, val, pend, v);
+        pend = NOVAL;
+    }
+    uint32_t get(Builder& B) {
+        if (pend != NOVAL) { val = B.add(IR_XOR2, val, pend); pend = NOVAL; }
+        return val;
+    }
+};
+
+// Output specification: the set of C columns XORed (XOR semantics) or a source row.
+struct OutDesc {
+    bool source = false;
+    uint32_t row = 0;
+    std::vector<uint32_t> cols;
+};
+
+bool build(const Params& p, const std::vector<OutDesc>& outs, ColIR* ir, std::string* err) {
+    Elim e;
+    if (!eliminate(p, &e, err)) return false;
+    *ir = ColIR();
+    ir->p = p;
+    ir->n_out = (uint32_t)outs.size();
+    Builder B{ir};
+    const uint32_t npiv = (uint32_t)e.piv_col.size(), u = e.u, n2 = e.n2, H = e.H, S = e.S, KS = e.KS;
+    const uint32_t K = p.K;
+    auto D = [&](uint32_t row) -> uint32_t {  // rhs of GF(2) row `row` (LT rows: source ISI row - S)
+        if (row < S) return NOVAL;
+        const uint32_t isi = row - S;
+        return isi < K ? B.add(IR_LOAD, NOVAL, NOVAL, NOVAL, isi) : NOVAL;
+    };
+    // ---- forward pass (peeling order)
+    ir->phase_start[0] = 0;
+    std::vector<uint32_t> y(npiv, NOVAL);
+    for (uint32_t k = 0; k < npiv; ++k) {
+        std::vector<uint32_t> t;
+        t.push_back(D(e.piv_row[k]));
+        for (uint32_t j : e.deps[k]) t.push_back(y[j]);
+        y[k] = B.xsum(t);
+    }
+    // ---- per output: y-part (pivoted columns) and W-hat (U part) -> V1 (n2 bits), V2 (H bits)
+    const uint32_t no = (uint32_t)outs.size();
+    std::vector<std::vector<uint32_t>> col_outs(e.L);  // column -> outputs using it (odd multiplicity)
+    std::vector<Bits> V1(no, Bits((n2 + 63) / 64, 0)), V2(no, Bits((H + 63) / 64, 0));
+    for (uint32_t o = 0; o < no; ++o) {
+        if (outs[o].source) continue;
+        std::vector<uint32_t> cs = outs[o].cols;
+        std::sort(cs.begin(), cs.end());
+        std::vector<uint32_t> kept;
+        for (size_t i = 0; i < cs.size();) {
+            size_t j = i;
+            while (j < cs.size() && cs[j] == cs[i]) ++j;
+            if ((j - i) & 1) kept.push_back(cs[i]);
+            i = j;
+        }
+        Bits what(e.nw, 0);
+        for (uint32_t c : kept) {
+            if (e.cstate[c] == 1) {
+                col_outs[c].push_back(o);
+                const uint64_t* wk = e.wrow((uint32_t)e.col_order[c]);
+                for (uint32_t x = 0; x < e.nw; ++x) what[x] ^= wk[x];
+            } else {
+                flip(what.data(), (uint32_t)e.uidx[c]);
+            }
+        }
+        for (uint32_t i = 0; i < n2; ++i) {
+            if (!bit(what.data(), (uint32_t)e.pc_of_row[i])) continue;
+            for (uint32_t x = 0; x < V1[o].size(); ++x) V1[o][x] ^= e.E2[i][x];
+            for (uint32_t x = 0; x < V2[o].size(); ++x) V2[o][x] ^= e.R[i][x];
+        }
+        for (uint32_t f = 0; f < H; ++f)
+            if (bit(what.data(), e.fcols[f])) flip(V2[o].data(), f);
+    }
+    // rem rows per column
+    std::vector<std::vector<uint32_t>> col_rem(e.L);
+    for (uint32_t i = 0; i < n2; ++i)
+        for (uint32_t c : e.rows[e.rem[i]])
+            if (e.cstate[c] == 1) col_rem[c].push_back(i);
+
+    // ---- column scan: Horner for the HDPC sums and the pushes into b2 / output sums
+    ir->phase_start[1] = (uint32_t)ir->nodes.size();
+    std::vector<Acc> b2acc(n2), oacc(no), part(H);
+    for (uint32_t i = 0; i < n2; ++i) b2acc[i].push(B, D(e.rem[i]));
+    uint32_t t = NOVAL;
+    for (uint32_t j = 0; j < KS; ++j) {
+        const uint32_t yj = (e.cstate[j] == 1) ? y[(uint32_t)e.col_order[j]] : NOVAL;
+        t = B.xt(t, yj);
+        if (j + 1 < KS && t != NOVAL) {
+            part[e.ma[j]].push(B, t);
+            part[e.mb[j]].push(B, t);
+        }
+        if (yj != NOVAL) {
+            for (uint32_t i : col_rem[j]) b2acc[i].push(B, yj);
+            for (uint32_t o : col_outs[j]) oacc[o].push(B, yj);
+        }
+    }
+    for (uint32_t c = KS; c < e.L; ++c) {  // pivoted columns past the HDPC range (none in practice)
+        if (e.cstate[c] != 1) continue;
+        const uint32_t yc = y[(uint32_t)e.col_order[c]];
+        for (uint32_t i : col_rem[c]) b2acc[i].push(B, yc);
+        for (uint32_t o : col_outs[c]) oacc[o].push(B, yc);
+    }
+    // bh_h = part_h ^ alpha^h * t_(KS-1)
+    std::vector<uint32_t> bh(H), b2(n2);
+    {
+        uint32_t s = t;
+        for (uint32_t h = 0; h < H; ++h) {
+            if (h) s = B.xt(s);
+            std::vector<uint32_t> v{part[h].get(B), s};
+            bh[h] = B.xsum(v);
+        }
+    }
+    for (uint32_t i = 0; i < n2; ++i) b2[i] = b2acc[i].get(B);
+
+    // ---- dense part: C_F[f] = sum_bit alpha^bit X_bit[f], X_bit[f] = bits of Zi[f]*bh ^ Q[f]*b2
+    ir->phase_start[2] = (uint32_t)ir->nodes.size();
+    std::vector<uint32_t> CF(H, NOVAL);
+    for (uint32_t f = 0; f < H; ++f) {
+        uint32_t acc = NOVAL;
+        for (int bt = 7; bt >= 0; --bt) {
+            std::vector<uint32_t> terms;
+            for (uint32_t h = 0; h < H; ++h)
+                if ((e.Zi[(size_t)f * H + h] >> bt) & 1) terms.push_back(bh[h]);
+            for (uint32_t m = 0; m < n2; ++m)
+                if ((e.Q[(size_t)f * n2 + m] >> bt) & 1) terms.push_back(b2[m]);
+            const uint32_t x = B.xsum(terms);
+            acc = B.xt(acc, x);
+        }
+        CF[f] = acc;
+    }
+    // ---- outputs
+    ir->phase_start[3] = (uint32_t)ir->nodes.size();
+    for (uint32_t o = 0; o < no; ++o) {
+        uint32_t v;
+        if (outs[o].source) {
+            v = outs[o].row < K ? B.add(IR_LOAD, NOVAL, NOVAL, NOVAL, outs[o].row) : NOVAL;
+        } else {
+            std::vector<uint32_t> terms{oacc[o].get(B)};
+            for (uint32_t m = 0; m < n2; ++m)
+                if (bit(V1[o].data(), m)) terms.push_back(b2[m]);
+            for (uint32_t f = 0; f < H; ++f)
+                if (bit(V2[o].data(), f)) terms.push_back(CF[f]);
+            v = B.xsum(terms);
+        }
+        if (v == NOVAL) v = B.add(IR_ZERO);
+        B.add(IR_STORE, v, NOVAL, NOVAL, o);
+    }
+    auto& st = ir->st;
+    for (const IrNode& n : ir->nodes) {
+        switch (n.k) {
+            case IR_LOAD: ++st.load; break;
+            case IR_ZERO: ++st.zero; break;
+            case IR_XOR2: ++st.xor2; break;
+            case IR_XOR3: ++st.xor3; break;
+            case IR_XT: ++st.xt; break;
+            case IR_XTX: ++st.xtx; break;
+            case IR_STORE: ++st.store; break;
+        }
+    }
+    st.u = u; st.npiv = npiv; st.n2 = n2;
+    return true;
+}
+
+inline uint32_t xtime4(uint32_t x) {
+    const uint32_t hi = (x >> 7) & 0x01010101u;
+    return ((x & 0x7F7F7F7Fu) << 1) ^ (hi * 0x1Du);
+}
+
+}  // namespace
+
+bool build_colprog(const Params& p, const uint32_t* esi, uint32_t n_out, ColIR* ir, std::string* err) {
+    std::vector<OutDesc> outs(n_out);
+    uint32_t cols[64];
+    for (uint32_t o = 0; o < n_out; ++o) {
+        if (esi[o] < p.K) { outs[o].source = true; outs[o].row = esi[o]; continue; }
+        const int n = lt_cols(p, esi[o] + p.Kp - p.K, cols);
+        outs[o].cols.assign(cols, cols + n);
+    }
+    return build(p, outs, ir, err);
+}
+
+bool build_colprog_C(const Params& p, ColIR* ir, std::string* err) {
+    std::vector<OutDesc> outs(p.L);
+    for (uint32_t c = 0; c < p.L; ++c) outs[c].cols = {c};
+    return build(p, outs, ir, err);
+}
+
+void eval_colprog(const ColIR& ir, const uint8_t* src, uint32_t T, uint8_t* out) {
+    const uint32_t Td = T / 4;
+    std::vector<uint32_t> v((size_t)ir.nodes.size() * Td, 0);
+    auto V = [&](uint32_t i) { return &v[(size_t)i * Td]; };
+    for (uint32_t i = 0; i < ir.nodes.size(); ++i) {
+        const IrNode& n = ir.nodes[i];
+        uint32_t* d = V(i);
+        switch (n.k) {
+            case IR_LOAD: std::memcpy(d, src + (size_t)n.imm * T, (size_t)Td * 4); break;
+            case IR_ZERO: break;
+            case IR_XOR2: for (uint32_t c = 0; c < Td; ++c) d[c] = V(n.a)[c] ^ V(n.b)[c]; break;
+            case IR_XOR3: for (uint32_t c = 0; c < Td; ++c) d[c] = V(n.a)[c] ^ V(n.b)[c] ^ V(n.c)[c]; break;
+            case IR_XT: for (uint32_t c = 0; c < Td; ++c) d[c] = xtime4(V(n.a)[c]); break;
+            case IR_XTX: for (uint32_t c = 0; c < Td; ++c) d[c] = xtime4(V(n.a)[c]) ^ V(n.b)[c]; break;
+            case IR_STORE: std::memcpy(out + (size_t)n.imm * T, V(n.a), (size_t)Td * 4); break;
+        }
+    }
+}
+
+}  // namespace rq

@@ -1,0 +1,64 @@
+// rq_colprog.hpp -- the "column program": RaptorQ encode compiled to straight-line gfx950 code.
+//
+// One GPU lane owns one dword column (4 bytes) of one source block; all lanes run the same
+// program, which depends only on (K', K, the requested output symbols).  The program computes
+// the requested repair symbols of the constraint system A*C = D that xssnick's Solve handles per
+// block (RQ/solver.go:25-185), without ever materialising C:
+//
+//   forward pass  y_k = D_row(k) ^ XOR_{j in deps(k)} y_j       (peeling order, RQ/inactivate.go)
+//   Horner scan   bh = G_HDPC * y  (MT * Gamma, RQ/params.go:116-133) in column order, which also
+//                 pushes every y into the remaining-row sums b2 and the output sums
+//   dense part    C_F = Zi*bh ^ Q*b2  (H values; GF(256) by bit-decomposed Horner: xtime + XOR)
+//   outputs       out_j = XOR_{c in LT(j), pivoted} y_c ^ V1_j*b2 ^ V2_j*C_F   (encodeGen,
+//                 RQ/params.go:162-182, with C = y ^ W*C_U folded in)
+//
+// C is the unique solution of a full-rank system, so the outputs are
+// bit-exact with the reference whatever elimination order is used here.  Every operation is an
+// XOR of 2-3 values or a multiply by alpha (xtime) -- no general GF(256) multiply survives.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "rq_core.hpp"
+
+namespace rq {
+
+enum IrKind : uint8_t {
+    IR_LOAD = 0,  // imm = source row (< K)
+    IR_ZERO = 1,
+    IR_XOR2 = 2,  // a ^ b
+    IR_XOR3 = 3,  // a ^ b ^ c
+    IR_XT = 4,    // alpha * a (per byte, GF(256) poly 0x11D)
+    IR_XTX = 5,   // alpha * a ^ b
+    IR_STORE = 6  // output imm <- a
+};
+constexpr uint32_t NOVAL = 0xFFFFFFFFu;
+
+struct IrNode {
+    uint8_t k = IR_ZERO;
+    uint32_t a = NOVAL, b = NOVAL, c = NOVAL;  // operand value ids (node indices)
+    uint32_t imm = 0;
+};
+
+struct ColIR {
+    Params p{};
+    std::vector<IrNode> nodes;     // program order; node i defines value i (except STORE)
+    uint32_t n_out = 0;
+    uint32_t phase_start[4] = {0, 0, 0, 0};  // forward, scan, dense, outputs
+    struct Stats {
+        uint32_t xor2 = 0, xor3 = 0, xt = 0, xtx = 0, load = 0, store = 0, zero = 0;
+        uint32_t u = 0, npiv = 0, n2 = 0;
+    } st;
+};
+
+// Outputs are ESIs with the library's GenSymbol meaning (RQ/encoder.go:36-41): esi < K is the
+// zero-padded source row, otherwise the LT symbol of ISI esi + K' - K.  p.K is the library K.
+bool build_colprog(const Params& p, const uint32_t* esi, uint32_t n_out, ColIR* ir, std::string* err);
+// Outputs are the L intermediate symbols C[0..L-1] (per-object encoder: GenSymbol gathers).
+bool build_colprog_C(const Params& p, ColIR* ir, std::string* err);
+// Host evaluation of the IR on one block (test reference for the compiler, not a product path):
+// src = K rows x T bytes, out = n_out rows x T bytes.
+void eval_colprog(const ColIR& ir, const uint8_t* src, uint32_t T, uint8_t* out);
+
+}  // namespace rq

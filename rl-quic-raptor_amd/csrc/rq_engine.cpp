@@ -17,6 +17,8 @@
 #include <vector>
 
 #include "../../include/rqhip.h"
+#include "rq_colasm.hpp"
+#include "rq_colprog.hpp"
 #include "rq_device.hpp"
 #include "rq_plan.hpp"
 
@@ -81,12 +83,25 @@ struct DevPlan {
     bool cid_ready = false;
 };
 
+// A compiled column program (rq_colprog.hpp / rq_colasm.hpp) loaded on one device.
+struct ColKernel {
+    hipModule_t mod = nullptr;
+    hipFunction_t fn = nullptr;
+    Params p{};
+    std::vector<uint32_t> esi;     // outputs (empty: all L intermediate symbols)
+    uint32_t n_out = 0, n_slots = 0;
+    MProg::Stats st{};
+    uint32_t n_ins = 0;
+    ~ColKernel() { if (mod) (void)hipModuleUnload(mod); }
+};
+
 struct DevCtx {
     int device = -1;
     std::mutex mu;
     bool tables = false;
     std::map<uint32_t, std::unique_ptr<DevPlan>> plans;  // keyed by K'
-    DevBuf ws_idx, ws_sigma, ws_x, ws_xp, ws_status, ws_esi;
+    std::map<std::string, std::unique_ptr<ColKernel>> colk;  // keyed by (K', K, outputs)
+    DevBuf ws_idx, ws_sigma, ws_x, ws_xp, ws_status, ws_esi, ws_scratch;
 };
 
 std::mutex g_ctx_mu;
@@ -286,6 +301,81 @@ int encode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, c
                 std::fclose(f);
             }
         }
+    }
+    return RQ_OK;
+}
+
+// ---------------- column programs (the encode hot path) ----------------
+// Compile (once per device and (K', K, outputs)) the straight-line gfx950 program for the given
+// outputs: IR (rq_colprog.cpp) -> registers/scratch (rq_colasm.cpp) -> assembly -> code object
+// (amd_comgr, in process) -> hipModuleLoadData.  Caller holds ctx->mu.
+int get_col_kernel(DevCtx* ctx, const Params& p, const uint32_t* esi, uint32_t n_esi, bool all_C, ColKernel** out) {
+    std::string key = std::to_string(p.Kp) + ":" + std::to_string(p.K) + (all_C ? ":C" : ":E");
+    if (!all_C) {
+        key.reserve(key.size() + n_esi * 6);
+        for (uint32_t i = 0; i < n_esi; ++i) key += "," + std::to_string(esi[i]);
+    }
+    auto& slot = ctx->colk[key];
+    if (!slot) {
+        std::unique_ptr<ColKernel> k(new ColKernel());
+        k->p = p;
+        if (!all_C) k->esi.assign(esi, esi + n_esi);
+        ColIR ir;
+        std::string err;
+        const bool ok = all_C ? build_colprog_C(p, &ir, &err) : build_colprog(p, esi, n_esi, &ir, &err);
+        if (!ok) return fail(RQ_ERR_PLAN, err);
+        AllocOpts o;
+        MProg mp;
+        if (!allocate_colprog(ir, o, &mp, &err)) return fail(RQ_ERR_PLAN, err);
+        const std::string src = emit_colprog_asm(mp, "rq_colprog");
+        std::vector<char> co;
+        if (!comgr_assemble(src, &co, &err)) return fail(RQ_ERR_PLAN, err);
+        HIP_TRY(hipModuleLoadData(&k->mod, co.data()));
+        HIP_TRY(hipModuleGetFunction(&k->fn, k->mod, "rq_colprog"));
+        k->n_out = ir.n_out;
+        k->n_slots = mp.n_slots;
+        k->st = mp.st;
+        k->n_ins = (uint32_t)mp.ins.size();
+        slot = std::move(k);
+    }
+    *out = slot.get();
+    return RQ_OK;
+}
+
+// Run a column program over n_blocks device-resident blocks.  Caller holds ctx->mu.
+int launch_col(DevCtx* ctx, ColKernel* k, uint32_t T, uint32_t n_blocks, const void* src, uint64_t src_stride,
+               void* out, uint64_t out_stride, void* stream) {
+    if (T == 0 || T % 4) return fail(RQ_ERR_BAD_ARG, "T must be a positive multiple of 4");
+    const uint32_t Td = T / 4;
+    // every buffer offset is 32-bit: split so that each launch spans < 4 GiB per buffer
+    const uint64_t lim = 0xFFFFFFFFull - (uint64_t)std::max(k->p.K, k->n_out) * T;
+    uint32_t per = n_blocks;
+    while (per > 1 && ((uint64_t)per * src_stride > lim || (uint64_t)per * out_stride > lim)) per = (per + 1) / 2;
+    if ((uint64_t)per * src_stride > lim || (uint64_t)per * out_stride > lim)
+        return fail(RQ_ERR_UNSUPPORTED, "block stride beyond the 4 GiB buffer-offset range");
+    const uint64_t max_cols = (uint64_t)per * Td;
+    if (max_cols > 0x7FFFFFFFull) return fail(RQ_ERR_UNSUPPORTED, "batch too large");
+    const uint32_t max_waves = (uint32_t)((max_cols + 63) / 64);
+    const size_t spw = (size_t)std::max<uint32_t>(k->n_slots, 1) * 256;
+    int rc;
+    if ((rc = ctx->ws_scratch.ensure(spw * max_waves))) return rc;
+    for (uint32_t b0 = 0; b0 < n_blocks; b0 += per) {
+        const uint32_t nb = std::min(per, n_blocks - b0);
+        ColKernArgs a;
+        std::memset(&a, 0, sizeof a);
+        a.src = (uint64_t)(uintptr_t)src + (uint64_t)b0 * src_stride;
+        a.out = (uint64_t)(uintptr_t)out + (uint64_t)b0 * out_stride;
+        a.scratch = (uint64_t)(uintptr_t)ctx->ws_scratch.p;
+        a.src_stride = (uint32_t)src_stride;
+        a.out_stride = (uint32_t)out_stride;
+        a.T = T;
+        a.n_cols = nb * Td;
+        a.scr_per_wave = (uint32_t)spw;
+        if (!divmagic(Td, a.n_cols, &a.magic, &a.shift)) return fail(RQ_ERR_UNSUPPORTED, "no division magic");
+        size_t sz = sizeof a;
+        void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+        const uint32_t waves = (a.n_cols + 63) / 64;
+        HIP_TRY(hipModuleLaunchKernel(k->fn, waves, 1, 1, 64, 1, 1, 0, (hipStream_t)stream, nullptr, cfg));
     }
     return RQ_OK;
 }
@@ -531,6 +621,62 @@ int rq_wave_export(uint32_t K, uint32_t sd, uint32_t sizes[4], uint32_t* words, 
     return RQ_OK;
 }
 
+int rq_debug_colprog_eval(uint32_t K, uint32_t T, const uint32_t* esi, uint32_t n_out, const uint8_t* src,
+                          uint8_t* out, uint32_t stats[12]) {
+    Params p;
+    int rc = params_for_K(K, &p);
+    if (rc) return fail(rc, "k is too big");
+    if (T == 0 || T % 4) return fail(RQ_ERR_BAD_ARG, "T must be a positive multiple of 4");
+    ColIR ir;
+    std::string err;
+    const bool ok = esi ? build_colprog(p, esi, n_out, &ir, &err) : build_colprog_C(p, &ir, &err);
+    if (!ok) return fail(RQ_ERR_PLAN, err);
+    if (src && out) eval_colprog(ir, src, T, out);
+    if (stats) {
+        const auto& s = ir.st;
+        const uint32_t v[12] = {(uint32_t)ir.nodes.size(), s.xor2, s.xor3, s.xt, s.xtx, s.load, s.store, s.zero,
+                                s.u, s.npiv, s.n2, ir.n_out};
+        std::memcpy(stats, v, sizeof v);
+    }
+    return RQ_OK;
+}
+
+int rq_debug_colprog_emulate(uint32_t K, uint32_t T, const uint32_t* esi, uint32_t n_out, const uint8_t* src,
+                             uint8_t* out, const uint32_t opts[5], uint32_t stats[16], char* asm_buf, size_t asm_cap,
+                             size_t* asm_len) {
+    Params p;
+    int rc = params_for_K(K, &p);
+    if (rc) return fail(rc, "k is too big");
+    if (T == 0 || T % 4) return fail(RQ_ERR_BAD_ARG, "T must be a positive multiple of 4");
+    ColIR ir;
+    std::string err;
+    const bool ok = esi ? build_colprog(p, esi, n_out, &ir, &err) : build_colprog_C(p, &ir, &err);
+    if (!ok) return fail(RQ_ERR_PLAN, err);
+    AllocOpts o;
+    if (opts) {
+        if (opts[0]) o.n_vgpr = std::min<uint32_t>(opts[0], V_ALLOC);
+        if (opts[1]) o.n_agpr = std::min<uint32_t>(opts[1], 256);
+        if (opts[2]) o.la_load = opts[2];
+        if (opts[3]) o.la_reload = opts[3];
+        if (opts[4]) o.max_vmem = std::min<uint32_t>(opts[4], 60);
+    }
+    MProg mp;
+    if (!allocate_colprog(ir, o, &mp, &err)) return fail(RQ_ERR_PLAN, err);
+    if (src && out && !emulate_colprog(mp, src, T, out, &err)) return fail(RQ_ERR_PLAN, err);
+    if (stats) {
+        const auto& s = mp.st;
+        const uint32_t v[16] = {(uint32_t)mp.ins.size(), s.valu, s.ldsrc, s.stout, s.spst, s.spld, s.accw, s.accr,
+                                s.wait, s.nop, s.sync_reload, mp.n_slots, (uint32_t)ir.nodes.size(), ir.st.xt + ir.st.xtx, 0, 0};
+        std::memcpy(stats, v, sizeof v);
+    }
+    if (asm_len) {
+        const std::string a = emit_colprog_asm(mp, "rq_colprog");
+        *asm_len = a.size();
+        if (asm_buf && asm_cap >= a.size()) std::memcpy(asm_buf, a.data(), a.size());
+    }
+    return RQ_OK;
+}
+
 int rq_debug_gf_selftest(uint32_t* bad_xtime, uint32_t* bad_mul) {
     if (!bad_xtime || !bad_mul) return fail(RQ_ERR_BAD_ARG, "null output");
     DevCtx* ctx;
@@ -618,6 +764,12 @@ int rq_encode_batch(const rq_encode_desc* d) {
     DevCtx* ctx;
     if ((rc = get_ctx(&ctx))) return rc;
     std::lock_guard<std::mutex> lk(ctx->mu);
+    if (!d->c_out) {
+        if (!d->n_esi) return RQ_OK;
+        ColKernel* k;
+        if ((rc = get_col_kernel(ctx, p, d->esi, d->n_esi, false, &k))) return rc;
+        return launch_col(ctx, k, d->T, d->n_blocks, d->src, d->src_stride, d->out, d->out_stride, d->stream);
+    }
     const uint32_t* d_esi = nullptr;
     if (d->n_esi) {
         if ((rc = ctx->ws_esi.ensure(d->n_esi * 4))) return rc;
