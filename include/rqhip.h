@@ -103,45 +103,31 @@ typedef struct {
 } rq_decode_desc;
 int rq_decode_batch(const rq_decode_desc* d);
 
-/* ---------------- device / plan control ---------------- */
+/* ---------------- device control ---------------- */
 int rq_device_count(void);
 int rq_set_device(int device);      /* selects the HIP device for subsequent calls on this thread */
-/* Compile (and cache) the encode schedule for the K' row of K; returns its statistics:
- * stats[0..10] = {n_stmts, n_levels, n_src_xor, n_src_mul, n_global, u, inactivated,
- *                 n_pivots, n_slots, passB_inplace, passB_rebuild}.  Host only. */
-int rq_plan_stats(uint32_t K, uint32_t stats[11]);
-/* Export the compiled program for host-side verification (tests): sizes first with NULL
- * buffers.  sizes[0..4] = {n_levels+1, n_stmts+1, n_words, K', L}. */
-int rq_plan_export(uint32_t K, uint32_t sizes[5], uint32_t* level_start, uint32_t* stmt_off,
-                   uint32_t* words, uint16_t* load_slot, uint16_t* col_slot);
 
-/* Export the per-wave instruction streams k_encode executes (tests).  sd = strip width in
- * dwords (slot fields become LDS dword offsets slot*sd), or 0 for raw slot indices.
- * sizes[0..3] = {n_words, n_waves, n_levels, n_slots}; wave_off receives n_waves offsets. */
-int rq_wave_export(uint32_t K, uint32_t sd, uint32_t sizes[4], uint32_t* words, uint32_t* wave_off);
-
-/* Diagnostics: run k_encode on a caller-supplied wave program (host arrays) over n_blocks
- * synthetic zero blocks of K rows x T bytes; returns the average kernel time in ms via *ms. */
-/* Diagnostics: checks the device's packed GF(256) primitives (xtime, table multiply) against
- * host arithmetic on 1024 words x 256 coefficients; the counts of mismatching words. */
-int rq_debug_gf_selftest(uint32_t* bad_xtime, uint32_t* bad_mul);
-/* Diagnostics (host only): build the column program for (K, output ESIs; esi = NULL -> all L
- * intermediate symbols) and, if src/out are given, evaluate its IR on one block on the host
- * (src: K x T, out: n_out x T).  stats[0..11] = {nodes, xor2, xor3, xt, xtx, load, store, zero,
- * u, n_pivots, n_remaining_rows, n_out}. */
+/* ---------------- diagnostics (host only; tests and tools) ----------------
+ * The encode hot path is a straight-line gfx950 program generated per (K', K, outputs): the
+ * "column program" (rl-quic-raptor_amd/csrc/rq_colprog.hpp).  These entry points expose its
+ * stages for verification without a GPU.
+ *
+ * Build the column program for (K, output ESIs; esi = NULL -> all L intermediate symbols) and,
+ * if src/out are given, evaluate its IR on one block on the host (src: K x T, out: n_out x T).
+ * stats[0..11] = {nodes, xor2, xor3, xt, xtx, load, store, zero, u, n_pivots,
+ *                 n_remaining_rows, n_out}. */
 int rq_debug_colprog_eval(uint32_t K, uint32_t T, const uint32_t* esi, uint32_t n_out, const uint8_t* src,
                           uint8_t* out, uint32_t stats[12]);
-/* Diagnostics (host only): allocate the column program (opts = {n_vgpr, n_agpr, la_load,
- * la_reload, max_vmem}, 0 = default), emulate the machine program on one block when src/out are
- * given (checks vmcnt waits and scratch ordering), and optionally return its gfx950 assembly.
+/* Allocate the column program (opts = {n_vgpr, n_agpr, la_load, la_reload, max_vmem}, 0 =
+ * default), emulate the machine program on one block when src/out are given (checks vmcnt waits
+ * and scratch ordering), and optionally return its gfx950 assembly (size first with NULL).
  * stats[0..13] = {instructions, valu, src loads, out stores, spill stores, spill loads, accw,
  * accr, waits, nops, unprefetched reloads, scratch slots, ir nodes, xtimes}. */
 int rq_debug_colprog_emulate(uint32_t K, uint32_t T, const uint32_t* esi, uint32_t n_out, const uint8_t* src,
                              uint8_t* out, const uint32_t opts[5], uint32_t stats[16], char* asm_buf, size_t asm_cap,
                              size_t* asm_len);
-int rq_debug_run_wave_program(uint32_t K, uint32_t T, const uint32_t* words, uint32_t n_words,
-                              const uint32_t* wave_off, uint32_t n_levels, uint32_t n_blocks,
-                              uint32_t iters, float* ms);
+/* Assemble the column program in process (amd_comgr) and return the code object size. */
+int rq_debug_colprog_assemble(uint32_t K, const uint32_t* esi, uint32_t n_out, size_t* code_bytes);
 
 #ifdef __cplusplus
 }

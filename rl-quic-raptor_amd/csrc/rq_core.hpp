@@ -120,18 +120,4 @@ struct GF {
 };
 const GF& gf();
 
-// Byte-lookup tables for c * x on packed bytes with v_perm_b32 (rq_kernels.hip gfmul4_tab):
-// x = (x & 7) ^ (x & 0x38) ^ (x & 0xC0) per byte, so c*x = T0[x & 7] ^ T1[(x >> 3) & 7] ^ T2[x >> 6]
-// with T0[i] = c*i, T1[i] = c*(i << 3), T2[i] = c*(i << 6).  Words: T0 bytes 0-3, 4-7, T1 bytes
-// 0-3, 4-7, T2 bytes 0-3.
-inline void gf_perm_tables(uint8_t c, uint32_t w[5]) {
-    const GF& g = gf();
-    auto pack = [&](uint32_t base, uint32_t shift) {
-        uint32_t v = 0;
-        for (uint32_t i = 0; i < 4; ++i) v |= (uint32_t)g.mul(c, (uint8_t)((base + i) << shift)) << (8 * i);
-        return v;
-    };
-    w[0] = pack(0, 0); w[1] = pack(4, 0); w[2] = pack(0, 3); w[3] = pack(4, 3); w[4] = pack(0, 6);
-}
-
 }  // namespace rq

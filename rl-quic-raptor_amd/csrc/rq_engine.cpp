@@ -1,9 +1,10 @@
-// rq_engine.cpp -- host runtime of librqhip.so: device contexts, per-K' plan cache, the
-// batched device-resident encode/decode entry points, and the per-object Encoder/Decoder API
-// that mirrors xssnick/raptorq as wrapped by go/fec/raptorq_wrap.go.
+// rq_engine.cpp -- host runtime of librqhip.so: device contexts, the cache of compiled column
+// programs, the batched device-resident encode/decode entry points, and the per-object
+// Encoder/Decoder API that mirrors xssnick/raptorq as wrapped by go/fec/raptorq_wrap.go.
 //
-// There is no CPU fallback: every symbol the engine returns is computed by the HIP kernels in
-// rq_kernels.hip; without a usable gfx950 device the calls fail with RQ_ERR_DEVICE.
+// There is no CPU fallback: every symbol the engine returns is computed on the GPU, by a
+// generated gfx950 code object (rq_colprog / rq_colasm) or by the kernels in rq_kernels.hip;
+// without a usable gfx950 device the calls fail with RQ_ERR_DEVICE.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -20,9 +21,14 @@
 #include "rq_colasm.hpp"
 #include "rq_colprog.hpp"
 #include "rq_device.hpp"
-#include "rq_plan.hpp"
 
 namespace rq {
+
+const GF& gf() {
+    static const GF g;
+    return g;
+}
+
 namespace {
 
 thread_local std::string g_err;
@@ -39,7 +45,7 @@ int fail(int code, const std::string& msg) {
         if (e_ != hipSuccess) return fail(RQ_ERR_DEVICE, std::string(#expr ": ") + hipGetErrorString(e_)); \
     } while (0)
 
-// Growable device buffer (allocation happens outside any timed/captured region after warmup).
+// Growable device buffer (allocation happens outside any timed region after warmup).
 struct DevBuf {
     void* p = nullptr;
     size_t cap = 0;
@@ -57,41 +63,16 @@ struct DevBuf {
     ~DevBuf() { if (p) (void)hipFree(p); }
 };
 
-// Waves per k_encode workgroup (16, or 8; rq_kernels.hip instantiates both).  RQHIP_WAVES
-// overrides the default for experiments; it is read once per process.
-uint32_t enc_waves() {
-    static const uint32_t nw = [] {
-        const char* e = std::getenv("RQHIP_WAVES");
-        const uint32_t v = e ? (uint32_t)std::atoi(e) : 16u;
-        return (v == 8u) ? 8u : 16u;
-    }();
-    return nw;
-}
-
-struct DevWave {  // the wave program for one strip width (slot fields are LDS dword offsets)
-    WaveProgram wp;
-    DevBuf wstream, wave_off;
-};
-
-struct DevPlan {
-    Plan host;
-    uint32_t n_slots = 0;  // slot image rows: plan slots + zero slot + H trash slots
-    std::map<uint32_t, std::unique_ptr<DevWave>> waves;  // keyed by strip width sd
-    DevBuf load_slot, col_slot;
-    DevBuf cid;            // A^-1 restricted to source columns (decode), L x cid_stride bytes
-    uint32_t cid_stride = 0;
-    bool cid_ready = false;
-};
-
-// A compiled column program (rq_colprog.hpp / rq_colasm.hpp) loaded on one device.
+// A compiled column program loaded on one device.
 struct ColKernel {
     hipModule_t mod = nullptr;
     hipFunction_t fn = nullptr;
     Params p{};
     std::vector<uint32_t> esi;     // outputs (empty: all L intermediate symbols)
-    uint32_t n_out = 0, n_slots = 0;
+    uint32_t n_out = 0, n_slots = 0, n_ins = 0;
     MProg::Stats st{};
-    uint32_t n_ins = 0;
+    DevBuf mrep;                   // decode: outputs on the identity payload
+    uint32_t mrep_stride = 0;
     ~ColKernel() { if (mod) (void)hipModuleUnload(mod); }
 };
 
@@ -99,15 +80,12 @@ struct DevCtx {
     int device = -1;
     std::mutex mu;
     bool tables = false;
-    std::map<uint32_t, std::unique_ptr<DevPlan>> plans;  // keyed by K'
     std::map<std::string, std::unique_ptr<ColKernel>> colk;  // keyed by (K', K, outputs)
-    DevBuf ws_idx, ws_sigma, ws_x, ws_xp, ws_status, ws_esi, ws_scratch;
+    DevBuf ws_idx, ws_r0, ws_xb, ws_xp, ws_scratch;
 };
 
 std::mutex g_ctx_mu;
 std::map<int, std::unique_ptr<DevCtx>> g_ctx;
-std::mutex g_hplan_mu;
-std::map<uint32_t, std::unique_ptr<Plan>> g_hplans;  // host-only plans (tests, stats)
 
 int current_device(int* dev) {
     if (g_device < 0) {
@@ -136,61 +114,11 @@ int get_ctx(DevCtx** out) {
     return RQ_OK;
 }
 
-// Plan options; RQHIP_PASSB / RQHIP_DEPTH_B override the pass-B strategy for experiments.
-const PlanOptions& plan_options() {
-    static const PlanOptions o = [] {
-        PlanOptions r;
-        if (const char* e = std::getenv("RQHIP_PASSB")) r.passb_mode = (uint32_t)std::atoi(e);
-        if (const char* e = std::getenv("RQHIP_DEPTH_B")) r.depth_b = (uint32_t)std::atoi(e);
-        return r;
-    }();
-    return o;
-}
-
-int host_plan(uint32_t K, const Plan** out) {
-    Params p;
-    int rc = params_for_K(K, &p);
-    if (rc) return fail(rc, "k is too big");
-    std::lock_guard<std::mutex> lk(g_hplan_mu);
-    auto& pl = g_hplans[p.Kp];
-    if (!pl) {
-        std::unique_ptr<Plan> np(new Plan());
-        std::string err;
-        if (!compile_encode_plan(p, np.get(), &err, plan_options())) return fail(RQ_ERR_PLAN, err);
-        pl = std::move(np);
-    }
-    *out = pl.get();
-    return RQ_OK;
-}
-
 template <class T>
-int upload(DevBuf& b, const std::vector<T>& v) {
-    int rc = b.ensure(v.size() * sizeof(T));
+int upload(DevBuf& b, const std::vector<T>& v, void* stream) {
+    int rc = b.ensure(std::max<size_t>(v.size(), 1) * sizeof(T));
     if (rc) return rc;
-    HIP_TRY(hipMemcpy(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
-    return RQ_OK;
-}
-
-// Caller holds ctx->mu.
-int get_dev_plan(DevCtx* ctx, const Params& p, DevPlan** out) {
-    if (!ctx->tables) {
-        const int e = upload_tables();
-        if (e) return fail(RQ_ERR_DEVICE, "upload_tables failed");
-        ctx->tables = true;
-    }
-    auto& dp = ctx->plans[p.Kp];
-    if (!dp) {
-        const Plan* hp;
-        int rc = host_plan(p.K, &hp);
-        if (rc) return rc;
-        std::unique_ptr<DevPlan> n(new DevPlan());
-        n->host = *hp;
-        n->n_slots = n->host.n_slots + 1 + std::max<uint32_t>(n->host.p.H, 1);
-        if ((rc = upload(n->load_slot, n->host.load_slot))) return rc;
-        if ((rc = upload(n->col_slot, n->host.col_slot))) return rc;
-        dp = std::move(n);
-    }
-    *out = dp.get();
+    if (!v.empty()) HIP_TRY(hipMemcpyAsync(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, (hipStream_t)stream));
     return RQ_OK;
 }
 
@@ -200,109 +128,29 @@ DevParams dev_params(const Params& p) {
     return d;
 }
 
-int get_dev_wave(DevPlan* dp, uint32_t sd, DevWave** out) {
-    auto& dw = dp->waves[sd];
-    if (!dw) {
-        std::unique_ptr<DevWave> n(new DevWave());
-        std::string err;
-        if (!build_wave_program(dp->host, enc_waves(), sd, &n->wp, &err)) return fail(RQ_ERR_PLAN, err);
-        int rc;
-        if ((rc = upload(n->wstream, n->wp.words))) return rc;
-        if ((rc = upload(n->wave_off, n->wp.wave_off))) return rc;
-        dw = std::move(n);
-    }
-    *out = dw.get();
+int ensure_tables(DevCtx* ctx) {
+    if (ctx->tables) return RQ_OK;
+    if (upload_tables()) return fail(RQ_ERR_DEVICE, "upload_tables failed");
+    ctx->tables = true;
     return RQ_OK;
 }
 
-// Strip geometry: the widest strip (<= 32 dwords) whose n_slots x sd image fits the LDS.
-struct Geometry {
-    uint32_t sd, n_strips, group;
-};
-int geometry(const DevPlan& dp, uint32_t T, uint32_t K, bool erasures, Geometry* g) {
-    const uint32_t Td = T / 4;
-    // - stream ring / tuple staging, erasure bitmap, 16-byte alignment of the ring
-    const size_t ring = std::max<size_t>((size_t)enc_waves() * 2 * 64, 128 * 6) * 4;
-    const size_t budget = 160 * 1024 - ring - 16 - (erasures ? ((K + 31) / 32) * 4 : 0);
-    const size_t per_dword = (size_t)dp.n_slots * 4;
-    // RQHIP_SD_MAX caps the strip width (narrower strips -> several workgroups per CU); experiments
-    static const uint32_t sd_cap = [] {
-        const char* e = std::getenv("RQHIP_SD_MAX");
-        const uint32_t v = e ? (uint32_t)std::atoi(e) : 32u;
-        return v ? std::min<uint32_t>(v, 32u) : 32u;
-    }();
-    uint32_t sd_max = (uint32_t)std::min<size_t>(sd_cap, budget / per_dword);
-    if (sd_max == 0) return fail(RQ_ERR_UNSUPPORTED, "K' too large for the LDS-resident plan (n_slots=" +
-                                                         std::to_string(dp.n_slots) + ")");
-    g->n_strips = (Td + sd_max - 1) / sd_max;
-    g->sd = (Td + g->n_strips - 1) / g->n_strips;
-    g->group = 8;
-    while (g->group < g->sd) g->group <<= 1;
-    return RQ_OK;
-}
-
-EncArgs base_args(const DevPlan& dp, const DevWave& dw, const Params& p, uint32_t T, uint32_t sd) {
-    EncArgs a;
-    std::memset(&a, 0, sizeof a);
-    a.p = dev_params(p);
-    a.T = T;
-    a.n_slots = dw.wp.n_slots;
-    a.sd = sd;
-    a.n_levels = dw.wp.n_levels;
-    a.load_slot = dp.load_slot.as<uint16_t>();
-    a.wstream = dw.wstream.as<uint32_t>();
-    a.wave_off = dw.wave_off.as<uint32_t>();
-    a.n_waves = dw.wp.n_waves;
-    a.col_slot = dp.col_slot.as<uint16_t>();
-    static const uint32_t dbg = [] {  // timing ablations only (tools/ablate.py)
-        const char* s = std::getenv("RQHIP_DBG");
-        return s ? (uint32_t)std::strtoul(s, nullptr, 0) : 0u;
-    }();
-    a.dbg = dbg;
-    return a;
-}
-
-// Encode `n_blocks` blocks already on the device.  Caller holds ctx->mu.
-int encode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, const void* src, uint64_t src_stride,
-                  uint32_t n_esi, const uint32_t* d_esi, void* out, uint64_t out_stride, void* c_out,
-                  uint64_t c_stride, void* stream) {
-    DevPlan* dp;
-    int rc = get_dev_plan(ctx, p, &dp);
-    if (rc) return rc;
-    Geometry g;
-    if ((rc = geometry(*dp, T, p.K, false, &g))) return rc;
-    DevWave* dw;
-    if ((rc = get_dev_wave(dp, g.sd, &dw))) return rc;
-    EncArgs a = base_args(*dp, *dw, p, T, g.sd);
-    a.src = static_cast<const uint8_t*>(src);
-    a.src_stride = src_stride;
-    a.out_esi = d_esi;
-    a.n_out = n_esi;
-    a.out = static_cast<uint8_t*>(out);
-    a.out_stride = out_stride;
-    a.c_out = static_cast<uint8_t*>(c_out);
-    a.c_stride = c_stride;
-    static const char* stamp_file = std::getenv("RQHIP_STAMP_FILE");  // diagnostics only
-    DevBuf stamps;
-    if (stamp_file && stamps.ensure((size_t)a.n_levels * a.n_waves * 16) == RQ_OK) a.stamp = stamps.as<unsigned long long>();
-    const int e = launch_encode(a, g.n_strips, n_blocks, g.group, stream);
-    if (e) return fail(RQ_ERR_DEVICE, std::string("k_encode launch: ") + hipGetErrorString((hipError_t)e));
-    if (a.stamp) {
-        std::vector<unsigned long long> h((size_t)a.n_levels * a.n_waves * 2);
-        if (hipStreamSynchronize((hipStream_t)stream) == hipSuccess &&
-            hipMemcpy(h.data(), a.stamp, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
-            if (FILE* f = std::fopen(stamp_file, "w")) {
-                for (uint32_t l = 0; l < a.n_levels; ++l) {
-                    std::fprintf(f, "%u", l);
-                    for (uint32_t w = 0; w < a.n_waves; ++w)
-                        std::fprintf(f, " %llu:%llu", h[((size_t)l * a.n_waves + w) * 2], h[((size_t)l * a.n_waves + w) * 2 + 1]);
-                    std::fprintf(f, "\n");
-                }
-                std::fclose(f);
-            }
+// Allocation options; RQHIP_ALLOC="v,a,la_load,la_reload,max_vmem" overrides them for experiments.
+const AllocOpts& alloc_options() {
+    static const AllocOpts o = [] {
+        AllocOpts r;
+        if (const char* e = std::getenv("RQHIP_ALLOC")) {
+            unsigned v[5] = {0, 0, 0, 0, 0};
+            std::sscanf(e, "%u,%u,%u,%u,%u", &v[0], &v[1], &v[2], &v[3], &v[4]);
+            if (v[0]) r.n_vgpr = std::min<uint32_t>(v[0], V_ALLOC);
+            if (v[1]) r.n_agpr = std::min<uint32_t>(v[1], 256);
+            if (v[2]) r.la_load = v[2];
+            if (v[3]) r.la_reload = v[3];
+            if (v[4]) r.max_vmem = std::min<uint32_t>(v[4], 60);
         }
-    }
-    return RQ_OK;
+        return r;
+    }();
+    return o;
 }
 
 // ---------------- column programs (the encode hot path) ----------------
@@ -323,15 +171,17 @@ int get_col_kernel(DevCtx* ctx, const Params& p, const uint32_t* esi, uint32_t n
         ColIR ir;
         std::string err;
         const bool ok = all_C ? build_colprog_C(p, &ir, &err) : build_colprog(p, esi, n_esi, &ir, &err);
-        if (!ok) return fail(RQ_ERR_PLAN, err);
-        AllocOpts o;
+        if (!ok) { ctx->colk.erase(key); return fail(RQ_ERR_PLAN, err); }
         MProg mp;
-        if (!allocate_colprog(ir, o, &mp, &err)) return fail(RQ_ERR_PLAN, err);
+        if (!allocate_colprog(ir, alloc_options(), &mp, &err)) { ctx->colk.erase(key); return fail(RQ_ERR_PLAN, err); }
         const std::string src = emit_colprog_asm(mp, "rq_colprog");
         std::vector<char> co;
-        if (!comgr_assemble(src, &co, &err)) return fail(RQ_ERR_PLAN, err);
-        HIP_TRY(hipModuleLoadData(&k->mod, co.data()));
-        HIP_TRY(hipModuleGetFunction(&k->fn, k->mod, "rq_colprog"));
+        if (!comgr_assemble(src, &co, &err)) { ctx->colk.erase(key); return fail(RQ_ERR_PLAN, err); }
+        if (hipModuleLoadData(&k->mod, co.data()) != hipSuccess ||
+            hipModuleGetFunction(&k->fn, k->mod, "rq_colprog") != hipSuccess) {
+            ctx->colk.erase(key);
+            return fail(RQ_ERR_DEVICE, "hipModuleLoadData/GetFunction failed for the column program");
+        }
         k->n_out = ir.n_out;
         k->n_slots = mp.n_slots;
         k->st = mp.st;
@@ -346,6 +196,7 @@ int get_col_kernel(DevCtx* ctx, const Params& p, const uint32_t* esi, uint32_t n
 int launch_col(DevCtx* ctx, ColKernel* k, uint32_t T, uint32_t n_blocks, const void* src, uint64_t src_stride,
                void* out, uint64_t out_stride, void* stream) {
     if (T == 0 || T % 4) return fail(RQ_ERR_BAD_ARG, "T must be a positive multiple of 4");
+    if (n_blocks == 0) return RQ_OK;
     const uint32_t Td = T / 4;
     // every buffer offset is 32-bit: split so that each launch spans < 4 GiB per buffer
     const uint64_t lim = 0xFFFFFFFFull - (uint64_t)std::max(k->p.K, k->n_out) * T;
@@ -353,9 +204,8 @@ int launch_col(DevCtx* ctx, ColKernel* k, uint32_t T, uint32_t n_blocks, const v
     while (per > 1 && ((uint64_t)per * src_stride > lim || (uint64_t)per * out_stride > lim)) per = (per + 1) / 2;
     if ((uint64_t)per * src_stride > lim || (uint64_t)per * out_stride > lim)
         return fail(RQ_ERR_UNSUPPORTED, "block stride beyond the 4 GiB buffer-offset range");
-    const uint64_t max_cols = (uint64_t)per * Td;
-    if (max_cols > 0x7FFFFFFFull) return fail(RQ_ERR_UNSUPPORTED, "batch too large");
-    const uint32_t max_waves = (uint32_t)((max_cols + 63) / 64);
+    if ((uint64_t)per * Td > 0x7FFFFFFFull) return fail(RQ_ERR_UNSUPPORTED, "batch too large");
+    const uint32_t max_waves = (uint32_t)(((uint64_t)per * Td + 63) / 64);
     const size_t spw = (size_t)std::max<uint32_t>(k->n_slots, 1) * 256;
     int rc;
     if ((rc = ctx->ws_scratch.ensure(spw * max_waves))) return rc;
@@ -380,24 +230,46 @@ int launch_col(DevCtx* ctx, ColKernel* k, uint32_t T, uint32_t n_blocks, const v
     return RQ_OK;
 }
 
-// A^-1 restricted to the K' source columns: run the plan on the identity payload (T = K' bytes).
-int ensure_cid(DevCtx* ctx, DevPlan* dp, void* stream) {
-    if (dp->cid_ready) return RQ_OK;
-    const Params& p0 = dp->host.p;
-    Params p = p0;
-    p.K = p.Kp;  // every source row present
-    const uint32_t Tc = (p.Kp + 3) & ~3u;
-    std::vector<uint8_t> id((size_t)p.Kp * Tc, 0);
-    for (uint32_t i = 0; i < p.Kp; ++i) id[(size_t)i * Tc + i] = 1;
-    DevBuf src;
-    int rc = src.ensure(id.size());
+// Encode `n_blocks` device-resident blocks: outputs esi[0..n_esi) of every block.
+int encode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, const void* src, uint64_t src_stride,
+                  const uint32_t* esi, uint32_t n_esi, void* out, uint64_t out_stride, void* stream) {
+    if (!n_esi || !n_blocks) return RQ_OK;
+    ColKernel* k;
+    int rc = get_col_kernel(ctx, p, esi, n_esi, false, &k);
     if (rc) return rc;
-    HIP_TRY(hipMemcpy(src.p, id.data(), id.size(), hipMemcpyHostToDevice));
-    if ((rc = dp->cid.ensure((size_t)p.L * Tc))) return rc;
-    if ((rc = encode_locked(ctx, p, Tc, 1, src.p, id.size(), 0, nullptr, nullptr, 0, dp->cid.p, 0, stream))) return rc;
+    return launch_col(ctx, k, T, n_blocks, src, src_stride, out, out_stride, stream);
+}
+
+// Decode output set: every candidate repair ESI the batch holds.  A dense range [K, K+R) (R a
+// multiple of 16) when the received ESIs are not too sparse -- one compiled program then serves
+// every erasure pattern of that range -- otherwise the exact sorted set.
+std::vector<uint32_t> decode_union(uint32_t K, const std::vector<uint32_t>& rep) {
+    std::vector<uint32_t> u(rep);
+    std::sort(u.begin(), u.end());
+    u.erase(std::unique(u.begin(), u.end()), u.end());
+    if (u.empty()) return u;
+    const uint64_t span = ((uint64_t)u.back() - K + 16) & ~(uint64_t)15;
+    if (span <= 4 * u.size() + 64) {
+        std::vector<uint32_t> r((size_t)span);
+        for (uint32_t i = 0; i < span; ++i) r[i] = K + i;
+        return r;
+    }
+    return u;
+}
+
+// Coefficients of every output over the source rows: the program on the identity payload.
+int ensure_mrep(DevCtx* ctx, ColKernel* k, void* stream) {
+    if (k->mrep_stride) return RQ_OK;
+    const uint32_t K = k->p.K, Tid = (K + 3) & ~3u;
+    std::vector<uint8_t> id((size_t)K * Tid, 0);
+    for (uint32_t i = 0; i < K; ++i) id[(size_t)i * Tid + i] = 1;
+    DevBuf src;
+    int rc;
+    if ((rc = src.ensure(id.size())) || (rc = k->mrep.ensure((size_t)k->n_out * Tid))) return rc;
+    HIP_TRY(hipMemcpyAsync(src.p, id.data(), id.size(), hipMemcpyHostToDevice, (hipStream_t)stream));
+    if ((rc = launch_col(ctx, k, Tid, 1, src.p, id.size(), k->mrep.p, (uint64_t)k->n_out * Tid, stream))) return rc;
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
-    dp->cid_stride = Tc;
-    dp->cid_ready = true;
+    k->mrep_stride = Tid;
     return RQ_OK;
 }
 
@@ -407,33 +279,44 @@ constexpr uint32_t MAX_E = 255;  // decode-solve limits (LDS-resident [M | I])
 int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, void* data, uint64_t data_stride,
                   const uint32_t* n_erased, const uint32_t* erased, const uint32_t* n_repair,
                   const uint32_t* repair_esi, const void* repair, int32_t* status, void* stream) {
-    DevPlan* dp;
-    int rc = get_dev_plan(ctx, p, &dp);
-    if (rc) return rc;
-    if ((rc = ensure_cid(ctx, dp, stream))) return rc;
-    // per-block bookkeeping (host, O(n_blocks))
+    int rc;
     std::vector<uint32_t> blk_map, eoff(n_blocks + 1, 0), roff(n_blocks + 1, 0);
     size_t max_lds_solve = 0;
     uint32_t max_e = 0;
     for (uint32_t b = 0; b < n_blocks; ++b) {
         eoff[b + 1] = eoff[b] + n_erased[b];
         roff[b + 1] = roff[b] + n_repair[b];
+    }
+    std::vector<uint32_t> cand;
+    for (uint32_t b = 0; b < n_blocks; ++b) {
         const uint32_t e = n_erased[b], nr = n_repair[b];
+        for (uint32_t i = eoff[b]; i < eoff[b + 1]; ++i)
+            if (erased[i] >= p.K) return fail(RQ_ERR_BAD_ARG, "erased ESI >= K");
+        for (uint32_t i = roff[b]; i < roff[b + 1]; ++i)
+            if (repair_esi[i] < p.K) return fail(RQ_ERR_BAD_ARG, "repair ESI < K");
         if ((p.K - e) + nr < p.K) { status[b] = RQ_ERR_NOT_ENOUGH; continue; }
         if (e == 0) { status[b] = 1; continue; }
-        const size_t need = (((size_t)nr * (e + nr) + 15) & ~size_t(15)) + (size_t)nr * 24;  // [M | I] + tuples
-        if (e > MAX_E || nr > 255 || need > 150 * 1024) { status[b] = RQ_ERR_UNSUPPORTED; continue; }
+        const size_t need = (size_t)nr * (e + nr);
+        if (e > MAX_E || nr > 255 || need > 140 * 1024) { status[b] = RQ_ERR_UNSUPPORTED; continue; }
         status[b] = -100;  // pending
         blk_map.push_back(b);
         max_lds_solve = std::max(max_lds_solve, need);
         max_e = std::max(max_e, e);
+        cand.insert(cand.end(), repair_esi + roff[b], repair_esi + roff[b + 1]);
     }
     const uint32_t nw = (uint32_t)blk_map.size();
     if (nw == 0) return RQ_OK;
+    const std::vector<uint32_t> uni = decode_union(p.K, cand);
+    ColKernel* k;
+    if ((rc = get_col_kernel(ctx, p, uni.data(), (uint32_t)uni.size(), false, &k))) return rc;
+    if ((rc = ensure_mrep(ctx, k, stream))) return rc;
+    // union index of every received repair
+    std::map<uint32_t, uint32_t> upos;
+    for (uint32_t i = 0; i < uni.size(); ++i) upos[uni[i]] = i;
     const size_t n_er = eoff[n_blocks], n_rep = roff[n_blocks];
-    // index workspace: blk_map | eoff | roff | erased | rep_esi | status
+    // index workspace: blk_map | eoff | roff | erased | rep_uidx | status | zero (blk, row) lists
     std::vector<uint32_t> idx;
-    idx.reserve(nw + 2 * (n_blocks + 1) + n_er + n_rep + n_blocks);
+    idx.reserve(nw + 2 * (n_blocks + 1) + n_er * 3 + n_rep + n_blocks);
     const size_t o_map = 0;
     idx.insert(idx.end(), blk_map.begin(), blk_map.end());
     const size_t o_eoff = idx.size();
@@ -442,68 +325,66 @@ int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, v
     idx.insert(idx.end(), roff.begin(), roff.end());
     const size_t o_er = idx.size();
     idx.insert(idx.end(), erased, erased + n_er);
-    const size_t o_rep = idx.size();
-    idx.insert(idx.end(), repair_esi, repair_esi + n_rep);
+    const size_t o_ru = idx.size();
+    for (size_t i = 0; i < n_rep; ++i) {
+        auto it = upos.find(repair_esi[i]);
+        idx.push_back(it == upos.end() ? 0u : it->second);
+    }
     const size_t o_st = idx.size();
     idx.resize(idx.size() + n_blocks, 0);
-    if ((rc = ctx->ws_idx.ensure(idx.size() * 4))) return rc;
-    HIP_TRY(hipMemcpyAsync(ctx->ws_idx.p, idx.data(), idx.size() * 4, hipMemcpyHostToDevice, (hipStream_t)stream));
+    const size_t o_zb = idx.size();
+    uint32_t nz = 0;
+    for (uint32_t b : blk_map)
+        for (uint32_t i = eoff[b]; i < eoff[b + 1]; ++i, ++nz) idx.push_back(b);
+    const size_t o_zr = idx.size();
+    for (uint32_t b : blk_map)
+        for (uint32_t i = eoff[b]; i < eoff[b + 1]; ++i) idx.push_back(erased[i]);
+    if ((rc = upload(ctx->ws_idx, idx, stream))) return rc;
     const uint32_t* di = ctx->ws_idx.as<uint32_t>();
-    if ((rc = ctx->ws_sigma.ensure(std::max<size_t>(n_rep, 1) * T))) return rc;
-    if ((rc = ctx->ws_x.ensure((size_t)nw * max_e * max_e))) return rc;
+    const uint32_t nkc = (max_e + 63) / 64;
+    if ((rc = ctx->ws_r0.ensure((size_t)n_blocks * uni.size() * T))) return rc;
+    if ((rc = ctx->ws_xb.ensure((size_t)nw * nkc * max_e * 8 * 8))) return rc;
     if ((rc = ctx->ws_xp.ensure((size_t)nw * max_e * 2))) return rc;
 
-    // 1) syndromes: sigma_j = r_j ^ G_j A^-1 D(S with erased rows zeroed)
-    Geometry g;
-    if ((rc = geometry(*dp, T, p.K, true, &g))) return rc;
-    DevWave* dw;
-    if ((rc = get_dev_wave(dp, g.sd, &dw))) return rc;
-    EncArgs a = base_args(*dp, *dw, p, T, g.sd);
-    a.src = static_cast<const uint8_t*>(data);
-    a.src_stride = data_stride;
-    a.blk_map = di + o_map;
-    a.erased_off = di + o_eoff;
-    a.erased = di + o_er;
-    a.out_esi = di + o_rep;
-    a.out_off = di + o_roff;
-    a.out = ctx->ws_sigma.as<uint8_t>();
-    a.xor_in = static_cast<const uint8_t*>(repair);
-    int e = launch_encode(a, g.n_strips, nw, g.group, stream);
-    if (e) return fail(RQ_ERR_DEVICE, std::string("k_encode(decode) launch: ") + hipGetErrorString((hipError_t)e));
+    // 1) erased rows := 0, then r0 = the column program on every block (syndromes s = r ^ r0)
+    ZeroArgs z;
+    z.blk = di + o_zb; z.row = di + o_zr; z.data = static_cast<uint8_t*>(data); z.data_stride = data_stride;
+    z.T = T; z.n = nz;
+    if (launch_zero_rows(z, stream)) return fail(RQ_ERR_DEVICE, "k_zero_rows launch failed");
+    if ((rc = launch_col(ctx, k, T, n_blocks, data, data_stride, ctx->ws_r0.p, (uint64_t)uni.size() * T, stream)))
+        return rc;
     // 2) per-block solve
     SolveArgs s;
-    s.p = dev_params(p);
     s.blk_map = di + o_map;
     s.erased_off = di + o_eoff;
     s.erased = di + o_er;
     s.rep_off = di + o_roff;
-    s.rep_esi = di + o_rep;
-    s.cid = dp->cid.as<uint8_t>();
-    s.cid_stride = dp->cid_stride;
-    s.xmat = ctx->ws_x.as<uint8_t>();
+    s.rep_uidx = di + o_ru;
+    s.mrep = k->mrep.as<uint8_t>();
+    s.mrep_stride = k->mrep_stride;
+    s.xbits = ctx->ws_xb.as<uint64_t>();
     s.xpiv = ctx->ws_xp.as<uint16_t>();
     s.status = reinterpret_cast<int32_t*>(ctx->ws_idx.as<uint32_t>() + o_st);
     s.max_e = max_e;
-    e = launch_solve(s, nw, (uint32_t)((max_lds_solve + 15) & ~size_t(15)), stream);
-    if (e) return fail(RQ_ERR_DEVICE, std::string("k_solve launch: ") + hipGetErrorString((hipError_t)e));
-    // 3) apply
+    if (launch_solve(s, nw, (uint32_t)((max_lds_solve + 15) & ~size_t(15)), stream)) return fail(RQ_ERR_DEVICE, "k_solve launch failed");
+    // 3) apply: x_E = X * s
     ApplyArgs ap;
     ap.blk_map = di + o_map;
     ap.erased_off = di + o_eoff;
     ap.erased = di + o_er;
     ap.rep_off = di + o_roff;
-    ap.sigma = ctx->ws_sigma.as<uint8_t>();
-    ap.xmat = s.xmat;
+    ap.rep_uidx = di + o_ru;
+    ap.recv = static_cast<const uint8_t*>(repair);
+    ap.r0 = ctx->ws_r0.as<uint8_t>();
+    ap.n_union = (uint32_t)uni.size();
+    ap.xbits = s.xbits;
     ap.xpiv = s.xpiv;
     ap.status = s.status;
     ap.data = static_cast<uint8_t*>(data);
     ap.data_stride = data_stride;
     ap.T = T;
     ap.max_e = max_e;
-    const uint32_t n_strips = (T / 4 + 63) / 64;
-    const uint32_t lds = max_e * 64 * 4 + ((max_e * max_e + 15) & ~15u);
-    e = launch_apply(ap, n_strips, nw, lds, stream);
-    if (e) return fail(RQ_ERR_DEVICE, std::string("k_apply launch: ") + hipGetErrorString((hipError_t)e));
+    if (launch_apply(ap, (T / 4 + 63) / 64, nw, 0, stream)) return fail(RQ_ERR_DEVICE, "k_apply launch failed");
     std::vector<int32_t> st(n_blocks);
     HIP_TRY(hipMemcpyAsync(st.data(), ctx->ws_idx.as<uint32_t>() + o_st, n_blocks * 4, hipMemcpyDeviceToHost,
                            (hipStream_t)stream));
@@ -521,7 +402,7 @@ using namespace rq;
 struct rq_enc {
     Params p{};
     uint32_t T = 0, Tp = 0;
-    std::vector<uint8_t> src;  // K x Tp, zero padded (GenSymbol for esi < K aliases this)
+    std::vector<uint8_t> src;  // K x Tp, zero padded (GenSymbol for esi < K)
     DevBuf d_src, d_C, d_esi, d_out;
 };
 
@@ -547,7 +428,7 @@ const char* rq_strerror(int code) {
         case RQ_ERR_BAD_ARG: return "bad argument";
         case RQ_ERR_DEVICE: return "device error";
         case RQ_ERR_UNSUPPORTED: return "unsupported shape";
-        case RQ_ERR_PLAN: return "plan compilation failed";
+        case RQ_ERR_PLAN: return "program compilation failed";
         default: return "unknown error";
     }
 }
@@ -573,51 +454,6 @@ int rq_set_device(int device) {
     if (device < 0 || device >= n) return fail(RQ_ERR_DEVICE, "bad device index");
     g_device = device;
     HIP_TRY(hipSetDevice(device));
-    return RQ_OK;
-}
-
-int rq_plan_stats(uint32_t K, uint32_t stats[11]) {
-    const Plan* pl;
-    int rc = host_plan(K, &pl);
-    if (rc) return rc;
-    const PlanStats& s = pl->stats;
-    const uint32_t v[11] = {s.n_stmts, s.n_levels, s.n_src_xor, s.n_src_mul, s.n_reload, s.u,
-                            s.inactivated, s.n_pivots, s.n_slots, s.passB_inplace, s.passB_reload};
-    std::memcpy(stats, v, sizeof v);
-    return RQ_OK;
-}
-
-int rq_plan_export(uint32_t K, uint32_t sizes[5], uint32_t* level_start, uint32_t* stmt_off, uint32_t* words,
-                   uint16_t* load_slot, uint16_t* col_slot) {
-    const Plan* pl;
-    int rc = host_plan(K, &pl);
-    if (rc) return rc;
-    sizes[0] = (uint32_t)pl->level_start.size();
-    sizes[1] = (uint32_t)pl->stmt_off.size();
-    sizes[2] = (uint32_t)pl->words.size();
-    sizes[3] = pl->p.Kp;
-    sizes[4] = pl->p.L;
-    if (level_start) std::memcpy(level_start, pl->level_start.data(), pl->level_start.size() * 4);
-    if (stmt_off) std::memcpy(stmt_off, pl->stmt_off.data(), pl->stmt_off.size() * 4);
-    if (words) std::memcpy(words, pl->words.data(), pl->words.size() * 4);
-    if (load_slot) std::memcpy(load_slot, pl->load_slot.data(), pl->load_slot.size() * 2);
-    if (col_slot) std::memcpy(col_slot, pl->col_slot.data(), pl->col_slot.size() * 2);
-    return RQ_OK;
-}
-
-int rq_wave_export(uint32_t K, uint32_t sd, uint32_t sizes[4], uint32_t* words, uint32_t* wave_off) {
-    const Plan* pl;
-    int rc = host_plan(K, &pl);
-    if (rc) return rc;
-    WaveProgram wp;
-    std::string err;
-    if (!build_wave_program(*pl, enc_waves(), sd, &wp, &err)) return fail(RQ_ERR_PLAN, err);
-    sizes[0] = (uint32_t)wp.words.size();
-    sizes[1] = wp.n_waves;
-    sizes[2] = wp.n_levels;
-    sizes[3] = wp.n_slots;
-    if (words) std::memcpy(words, wp.words.data(), wp.words.size() * 4);
-    if (wave_off) std::memcpy(wave_off, wp.wave_off.data(), wp.wave_off.size() * 4);
     return RQ_OK;
 }
 
@@ -652,7 +488,7 @@ int rq_debug_colprog_emulate(uint32_t K, uint32_t T, const uint32_t* esi, uint32
     std::string err;
     const bool ok = esi ? build_colprog(p, esi, n_out, &ir, &err) : build_colprog_C(p, &ir, &err);
     if (!ok) return fail(RQ_ERR_PLAN, err);
-    AllocOpts o;
+    AllocOpts o = alloc_options();
     if (opts) {
         if (opts[0]) o.n_vgpr = std::min<uint32_t>(opts[0], V_ALLOC);
         if (opts[1]) o.n_agpr = std::min<uint32_t>(opts[1], 256);
@@ -666,7 +502,8 @@ int rq_debug_colprog_emulate(uint32_t K, uint32_t T, const uint32_t* esi, uint32
     if (stats) {
         const auto& s = mp.st;
         const uint32_t v[16] = {(uint32_t)mp.ins.size(), s.valu, s.ldsrc, s.stout, s.spst, s.spld, s.accw, s.accr,
-                                s.wait, s.nop, s.sync_reload, mp.n_slots, (uint32_t)ir.nodes.size(), ir.st.xt + ir.st.xtx, 0, 0};
+                                s.wait, s.nop, s.sync_reload, mp.n_slots, (uint32_t)ir.nodes.size(), ir.st.xt + ir.st.xtx,
+                                0, 0};
         std::memcpy(stats, v, sizeof v);
     }
     if (asm_len) {
@@ -677,107 +514,37 @@ int rq_debug_colprog_emulate(uint32_t K, uint32_t T, const uint32_t* esi, uint32
     return RQ_OK;
 }
 
-int rq_debug_gf_selftest(uint32_t* bad_xtime, uint32_t* bad_mul) {
-    if (!bad_xtime || !bad_mul) return fail(RQ_ERR_BAD_ARG, "null output");
-    DevCtx* ctx;
-    int rc;
-    if ((rc = get_ctx(&ctx))) return rc;
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    const uint32_t n = 1024;
-    std::vector<uint32_t> x(n), tabs(256 * 5), out((size_t)n * 257);
-    uint32_t s = 0x12345678u;
-    for (uint32_t i = 0; i < n; ++i) { s = s * 1664525u + 1013904223u; x[i] = i < 256 ? i * 0x01010101u : s; }
-    for (uint32_t c = 0; c < 256; ++c) gf_perm_tables((uint8_t)c, &tabs[c * 5]);
-    DevBuf dx, dt, dout;
-    if ((rc = upload(dx, x)) || (rc = upload(dt, tabs)) || (rc = dout.ensure(out.size() * 4))) return rc;
-    HIP_TRY((hipError_t)launch_gf_selftest(dx.as<uint32_t>(), n, dt.as<uint32_t>(), dout.as<uint32_t>()));
-    HIP_TRY(hipMemcpy(out.data(), dout.p, out.size() * 4, hipMemcpyDeviceToHost));
-    const GF& g = gf();
-    auto mul4 = [&](uint32_t v, uint8_t c) {
-        uint32_t r = 0;
-        for (int b = 0; b < 4; ++b) r |= (uint32_t)g.mul((uint8_t)(v >> (8 * b)), c) << (8 * b);
-        return r;
-    };
-    *bad_xtime = 0;
-    *bad_mul = 0;
-    for (uint32_t i = 0; i < n; ++i) {
-        if (out[i] != mul4(x[i], 2)) ++*bad_xtime;
-        for (uint32_t c = 0; c < 256; ++c)
-            if (out[n + (size_t)c * n + i] != mul4(x[i], (uint8_t)c)) ++*bad_mul;
-    }
-    return RQ_OK;
-}
-
-int rq_debug_run_wave_program(uint32_t K, uint32_t T, const uint32_t* words, uint32_t n_words,
-                              const uint32_t* wave_off, uint32_t n_levels, uint32_t n_blocks, uint32_t iters,
-                              float* ms) {
+int rq_debug_colprog_assemble(uint32_t K, const uint32_t* esi, uint32_t n_out, size_t* code_bytes) {
     Params p;
     int rc = params_for_K(K, &p);
     if (rc) return fail(rc, "k is too big");
-    DevCtx* ctx;
-    if ((rc = get_ctx(&ctx))) return rc;
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    DevPlan* dp;
-    if ((rc = get_dev_plan(ctx, p, &dp))) return rc;
-    Geometry g;
-    if ((rc = geometry(*dp, T, p.K, false, &g))) return rc;
-    DevWave* dwv;
-    if ((rc = get_dev_wave(dp, g.sd, &dwv))) return rc;
-    EncArgs a = base_args(*dp, *dwv, p, T, g.sd);
-    DevBuf w, wo, src;
-    std::vector<uint32_t> wv(words, words + n_words);
-    wv.resize(wv.size() + 256, 0);
-    std::vector<uint32_t> ov(wave_off, wave_off + enc_waves());
-    if ((rc = upload(w, wv)) || (rc = upload(wo, ov)) || (rc = src.ensure((size_t)n_blocks * K * T))) return rc;
-    HIP_TRY(hipMemset(src.p, 0, (size_t)n_blocks * K * T));
-    a.wstream = w.as<uint32_t>();
-    a.wave_off = wo.as<uint32_t>();
-    a.n_levels = n_levels;
-    a.src = src.as<uint8_t>();
-    a.src_stride = (uint64_t)K * T;
-    hipEvent_t e0, e1;
-    HIP_TRY(hipEventCreate(&e0));
-    HIP_TRY(hipEventCreate(&e1));
-    launch_encode(a, g.n_strips, n_blocks, g.group, nullptr);
-    HIP_TRY(hipEventRecord(e0, nullptr));
-    for (uint32_t i = 0; i < iters; ++i) launch_encode(a, g.n_strips, n_blocks, g.group, nullptr);
-    HIP_TRY(hipEventRecord(e1, nullptr));
-    HIP_TRY(hipEventSynchronize(e1));
-    float t = 0;
-    HIP_TRY(hipEventElapsedTime(&t, e0, e1));
-    *ms = t / (float)iters;
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
+    ColIR ir;
+    std::string err;
+    const bool ok = esi ? build_colprog(p, esi, n_out, &ir, &err) : build_colprog_C(p, &ir, &err);
+    if (!ok) return fail(RQ_ERR_PLAN, err);
+    MProg mp;
+    if (!allocate_colprog(ir, alloc_options(), &mp, &err)) return fail(RQ_ERR_PLAN, err);
+    std::vector<char> co;
+    if (!comgr_assemble(emit_colprog_asm(mp, "rq_colprog"), &co, &err)) return fail(RQ_ERR_PLAN, err);
+    if (code_bytes) *code_bytes = co.size();
     return RQ_OK;
 }
 
 int rq_encode_batch(const rq_encode_desc* d) {
     if (!d || d->T == 0) return fail(RQ_ERR_SYMBOL_SIZE_ZERO, "symbol size cannot be zero");
     if (d->T % 4 || d->K == 0 || (!d->src && d->n_blocks)) return fail(RQ_ERR_BAD_ARG, "bad encode descriptor (T % 4, K, src)");
-    if (d->n_blocks == 0) return RQ_OK;
-    if (d->n_esi && (!d->esi || !d->out)) return fail(RQ_ERR_BAD_ARG, "n_esi without esi/out");
-    for (uint32_t i = 0; i < d->n_esi; ++i)
-        if (d->esi[i] < d->K) return fail(RQ_ERR_BAD_ARG, "batch ESIs must be repair ids (>= K)");
+    if (d->n_blocks == 0 || d->n_esi == 0) return RQ_OK;
+    if (!d->esi || !d->out) return fail(RQ_ERR_BAD_ARG, "n_esi without esi/out");
+    if (d->src_stride < (uint64_t)d->K * d->T || d->out_stride < (uint64_t)d->n_esi * d->T)
+        return fail(RQ_ERR_BAD_ARG, "stride smaller than a block");
     Params p;
     int rc = params_for_K(d->K, &p);
     if (rc) return fail(rc, "k is too big");
     DevCtx* ctx;
     if ((rc = get_ctx(&ctx))) return rc;
     std::lock_guard<std::mutex> lk(ctx->mu);
-    if (!d->c_out) {
-        if (!d->n_esi) return RQ_OK;
-        ColKernel* k;
-        if ((rc = get_col_kernel(ctx, p, d->esi, d->n_esi, false, &k))) return rc;
-        return launch_col(ctx, k, d->T, d->n_blocks, d->src, d->src_stride, d->out, d->out_stride, d->stream);
-    }
-    const uint32_t* d_esi = nullptr;
-    if (d->n_esi) {
-        if ((rc = ctx->ws_esi.ensure(d->n_esi * 4))) return rc;
-        HIP_TRY(hipMemcpyAsync(ctx->ws_esi.p, d->esi, d->n_esi * 4, hipMemcpyHostToDevice, (hipStream_t)d->stream));
-        d_esi = ctx->ws_esi.as<uint32_t>();
-    }
-    return encode_locked(ctx, p, d->T, d->n_blocks, d->src, d->src_stride, d->n_esi, d_esi, d->out, d->out_stride,
-                         d->c_out, d->c_stride, d->stream);
+    return encode_locked(ctx, p, d->T, d->n_blocks, d->src, d->src_stride, d->esi, d->n_esi, d->out, d->out_stride,
+                         d->stream);
 }
 
 int rq_decode_batch(const rq_decode_desc* d) {
@@ -795,6 +562,8 @@ int rq_decode_batch(const rq_decode_desc* d) {
 }
 
 // ---------------- per-object encoder (CreateEncoder / GenSymbol) ----------------
+// CreateEncoder computes the intermediate symbols C on the GPU (the column program with all L
+// outputs); GenSymbol gathers LT rows of C on the GPU (k_gather).
 rq_enc* rq_encoder_create(const uint8_t* data, size_t len, uint32_t T, int* err) {
     int dummy;
     if (!err) err = &dummy;
@@ -815,14 +584,19 @@ rq_enc* rq_encoder_create(const uint8_t* data, size_t len, uint32_t T, int* err)
     DevCtx* ctx;
     if ((rc = get_ctx(&ctx))) { *err = rc; return nullptr; }
     std::lock_guard<std::mutex> lk(ctx->mu);
+    if ((rc = ensure_tables(ctx))) { *err = rc; return nullptr; }
     if ((rc = e->d_src.ensure(e->src.size())) || (rc = e->d_C.ensure((size_t)p.L * e->Tp))) { *err = rc; return nullptr; }
     if (hipMemcpy(e->d_src.p, e->src.data(), e->src.size(), hipMemcpyHostToDevice) != hipSuccess) {
         *err = fail(RQ_ERR_DEVICE, "hipMemcpy H2D failed");
         return nullptr;
     }
-    rc = encode_locked(ctx, p, e->Tp, 1, e->d_src.p, e->src.size(), 0, nullptr, nullptr, 0, e->d_C.p, 0, nullptr);
-    if (!rc && hipDeviceSynchronize() != hipSuccess) rc = fail(RQ_ERR_DEVICE, "encode failed");
-    if (rc) { *err = rc; return nullptr; }
+    ColKernel* k;
+    if ((rc = get_col_kernel(ctx, p, nullptr, 0, true, &k)) ||
+        (rc = launch_col(ctx, k, e->Tp, 1, e->d_src.p, e->src.size(), e->d_C.p, (uint64_t)p.L * e->Tp, nullptr))) {
+        *err = rc;
+        return nullptr;
+    }
+    if (hipDeviceSynchronize() != hipSuccess) { *err = fail(RQ_ERR_DEVICE, "encode failed"); return nullptr; }
     *err = RQ_OK;
     return e.release();
 }

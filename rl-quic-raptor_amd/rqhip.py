@@ -38,8 +38,8 @@ EXPORTED = (
     "rq_strerror", "rq_last_error", "rq_params", "rq_encoder_create", "rq_encoder_k",
     "rq_encoder_symbol_size", "rq_encoder_symbol", "rq_encoder_symbols", "rq_encoder_free",
     "rq_decoder_create", "rq_decoder_k", "rq_decoder_add", "rq_decoder_decode", "rq_decoder_free",
-    "rq_encode_batch", "rq_decode_batch", "rq_device_count", "rq_set_device", "rq_plan_stats",
-    "rq_plan_export", "rq_wave_export", "rq_debug_run_wave_program", "rq_debug_gf_selftest",
+    "rq_encode_batch", "rq_decode_batch", "rq_device_count", "rq_set_device",
+    "rq_debug_colprog_eval", "rq_debug_colprog_emulate", "rq_debug_colprog_assemble",
 )
 
 
@@ -100,13 +100,13 @@ def lib():
             "rq_decode_batch": ([ctypes.POINTER(DecodeDesc)], ctypes.c_int),
             "rq_device_count": ([], ctypes.c_int),
             "rq_set_device": ([ctypes.c_int], ctypes.c_int),
-            "rq_plan_stats": ([ctypes.c_uint32, u32p], ctypes.c_int),
-            "rq_plan_export": ([ctypes.c_uint32, u32p, u32p, u32p, u32p, u16p, u16p], ctypes.c_int),
-            "rq_wave_export": ([ctypes.c_uint32, ctypes.c_uint32, u32p, u32p, u32p], ctypes.c_int),
-            "rq_debug_run_wave_program": ([ctypes.c_uint32, ctypes.c_uint32, u32p, ctypes.c_uint32, u32p,
-                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
-                                           ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
-            "rq_debug_gf_selftest": ([u32p, u32p], ctypes.c_int),
+            "rq_debug_colprog_eval": ([ctypes.c_uint32, ctypes.c_uint32, u32p, ctypes.c_uint32, vp, vp, u32p],
+                                      ctypes.c_int),
+            "rq_debug_colprog_emulate": ([ctypes.c_uint32, ctypes.c_uint32, u32p, ctypes.c_uint32, vp, vp, u32p, u32p,
+                                          ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)],
+                                         ctypes.c_int),
+            "rq_debug_colprog_assemble": ([ctypes.c_uint32, u32p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_size_t)],
+                                          ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -128,7 +128,7 @@ def _buf(data):
     return b, (ctypes.c_uint8 * max(len(b), 1)).from_buffer_copy(b if b else b"\0")
 
 
-# ------------------------------------------------------------------ parameters / plans
+# ------------------------------------------------------------------ parameters / column programs
 PARAM_NAMES = ("K", "Kp", "J", "S", "H", "W", "L", "P", "P1", "U", "B")
 
 
@@ -138,52 +138,68 @@ def params(size, T):
     return dict(zip(PARAM_NAMES, list(out)))
 
 
-PLAN_STAT_NAMES = ("n_stmts", "n_levels", "n_src_xor", "n_src_mul", "n_global", "u", "inactivated",
-                   "n_pivots", "n_slots", "passB_inplace", "passB_rebuild")
+COLPROG_STAT_NAMES = ("instructions", "valu", "src_loads", "out_stores", "spill_stores", "spill_loads", "accw",
+                      "accr", "waits", "nops", "sync_reloads", "scratch_slots", "ir_nodes", "xtimes")
 
 
-def plan_stats(K):
-    out = (ctypes.c_uint32 * 11)()
-    _check(lib().rq_plan_stats(K, out))
-    return dict(zip(PLAN_STAT_NAMES, list(out)))
-
-
-def plan_export(K):
-    """The compiled per-K' program (numpy arrays) for host-side verification in tests."""
+def colprog_stats(K, esis=None, opts=None):
+    """Host-only statistics of the column program for (K, output ESIs) (None: all L symbols)."""
     import numpy as np
-    sizes = (ctypes.c_uint32 * 5)()
-    _check(lib().rq_plan_export(K, sizes, None, None, None, None, None))
-    n_lv, n_so, n_w, Kp, L = list(sizes)
-    lv = np.zeros(n_lv, np.uint32)
-    so = np.zeros(n_so, np.uint32)
-    w = np.zeros(n_w, np.uint32)
-    ls = np.zeros(Kp, np.uint16)
-    cs = np.zeros(L, np.uint16)
+    st = np.zeros(16, np.uint32)
     P32 = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
-    P16 = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16))
-    _check(lib().rq_plan_export(K, sizes, P32(lv), P32(so), P32(w), P16(ls), P16(cs)))
-    return dict(level_start=lv, stmt_off=so, words=w, load_slot=ls, col_slot=cs, Kp=Kp, L=L)
+    e = np.asarray(esis if esis is not None else [0], np.uint32)
+    o = np.asarray(opts if opts is not None else [0] * 5, np.uint32)
+    _check(lib().rq_debug_colprog_emulate(K, 4, P32(e) if esis is not None else None, len(e), None, None, P32(o),
+                                          P32(st), None, 0, None))
+    return dict(zip(COLPROG_STAT_NAMES, (int(x) for x in st[:14])))
 
 
-def wave_export(K, sd):
-    """Per-wave instruction streams of the K' plan (numpy) for host-side emulation in tests.
-    sd > 0 emits slot fields as LDS dword offsets (slot * sd), exactly as the kernel receives them."""
+def colprog_emulate(K, T, esis, src, opts=None):
+    """Run the allocated machine program on the host for one block (test infrastructure)."""
     import numpy as np
-    sizes = (ctypes.c_uint32 * 4)()
-    _check(lib().rq_wave_export(K, sd, sizes, None, None))
-    n_words, n_waves, n_levels, n_slots = list(sizes)
-    w = np.zeros(n_words, np.uint32)
-    off = np.zeros(n_waves, np.uint32)
+    src = np.ascontiguousarray(src, np.uint8)
+    e = np.asarray(esis, np.uint32)
+    out = np.zeros((len(e), T), np.uint8)
+    o = np.asarray(opts if opts is not None else [0] * 5, np.uint32)
+    st = np.zeros(16, np.uint32)
     P32 = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
-    _check(lib().rq_wave_export(K, sd, sizes, P32(w), P32(off)))
-    return dict(words=w, wave_off=off, n_waves=n_waves, n_levels=n_levels, n_slots=n_slots, sd=sd)
+    _check(lib().rq_debug_colprog_emulate(K, T, P32(e), len(e), src.ctypes.data, out.ctypes.data, P32(o), P32(st),
+                                          None, 0, None))
+    return out, dict(zip(COLPROG_STAT_NAMES, (int(x) for x in st[:14])))
 
 
-def gf_selftest():
-    """Device GF(256) primitives vs host arithmetic: (bad xtime words, bad table-multiply words)."""
-    a, b = ctypes.c_uint32(0), ctypes.c_uint32(0)
-    _check(lib().rq_debug_gf_selftest(ctypes.byref(a), ctypes.byref(b)))
-    return a.value, b.value
+def colprog_eval(K, T, esis, src):
+    """Evaluate the column program's IR on the host for one block (test infrastructure)."""
+    import numpy as np
+    src = np.ascontiguousarray(src, np.uint8)
+    e = np.asarray(esis, np.uint32)
+    out = np.zeros((len(e), T), np.uint8)
+    st = np.zeros(12, np.uint32)
+    P32 = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+    _check(lib().rq_debug_colprog_eval(K, T, P32(e), len(e), src.ctypes.data, out.ctypes.data, P32(st)))
+    return out
+
+
+def colprog_asm(K, esis):
+    """gfx950 assembly text of the column program for (K, output ESIs)."""
+    import numpy as np
+    e = np.asarray(esis, np.uint32)
+    P32 = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+    n = ctypes.c_size_t(0)
+    _check(lib().rq_debug_colprog_emulate(K, 4, P32(e), len(e), None, None, None, None, None, 0, ctypes.byref(n)))
+    buf = ctypes.create_string_buffer(n.value)
+    _check(lib().rq_debug_colprog_emulate(K, 4, P32(e), len(e), None, None, None, None, buf, n.value, ctypes.byref(n)))
+    return buf.raw[:n.value].decode()
+
+
+def colprog_assemble(K, esis):
+    """Assemble the column program in process (amd_comgr); returns the code object size."""
+    import numpy as np
+    e = np.asarray(esis, np.uint32)
+    n = ctypes.c_size_t(0)
+    _check(lib().rq_debug_colprog_assemble(K, e.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), len(e),
+                                           ctypes.byref(n)))
+    return n.value
 
 
 def device_count():

@@ -1,0 +1,84 @@
+"""The column program (the encode hot path's code generator) checked on the CPU, stage by stage:
+
+* its IR (rq_colprog.cpp) evaluated on the host equals the oracle's repair / source symbols and
+  intermediate symbols (C is the unique solution, so any elimination order
+  must reproduce the reference bytes);
+* the register-allocated machine program (rq_colasm.cpp: VGPR/AGPR/scratch tiers, prefetched
+  loads, exact vmcnt waits) emulated on the host gives the same bytes, with every wait and
+  scratch ordering checked by the emulator;
+* the generated gfx950 assembly assembles in process (amd_comgr).
+
+The GPU runs exactly this machine program (tests/test_gpu_parity.py)."""
+import numpy as np
+import pytest
+
+CASES = [(64, 48, 16), (5, 20, 6), (1, 8, 4), (26, 8, 40), (257, 16, 20), (1000, 12, 10), (1024, 16, 76),
+         (2048, 8, 30)]
+
+
+def _esis(K, nrep):
+    # repairs, first/last source rows, one far repair ESI
+    return list(range(K, K + nrep)) + [0, K - 1, K + 5000]
+
+
+@pytest.mark.parametrize("K,T,nrep", CASES)
+def test_ir_matches_oracle(rq, oracle, K, T, nrep):
+    rng = np.random.default_rng(K * 3 + T)
+    data = rng.integers(0, 256, K * T, dtype=np.uint8)
+    esis = _esis(K, nrep)
+    out = rq.colprog_eval(K, T, esis, data)
+    enc = oracle.OracleEncoder(data.tobytes(), T)
+    for i, e in enumerate(esis):
+        assert np.array_equal(out[i], enc.gen_symbol(e)), (K, e)
+
+
+@pytest.mark.parametrize("K,T,nrep", CASES)
+def test_machine_program_matches_oracle(rq, oracle, K, T, nrep):
+    rng = np.random.default_rng(K * 5 + T)
+    data = rng.integers(0, 256, K * T, dtype=np.uint8)
+    esis = _esis(K, nrep)
+    out, st = rq.colprog_emulate(K, T, esis, data)
+    enc = oracle.OracleEncoder(data.tobytes(), T)
+    for i, e in enumerate(esis):
+        assert np.array_equal(out[i], enc.gen_symbol(e)), (K, e)
+    assert st["sync_reloads"] <= st["spill_loads"]
+
+
+@pytest.mark.parametrize("opts", [[64, 32, 40, 20, 8], [32, 0, 400, 400, 60], [200, 8, 16, 8, 4]])
+def test_machine_program_under_register_pressure(rq, oracle, opts):
+    """Tight register files, short/long look-aheads and a small vmcnt budget force every spill /
+    reload / wait path of the allocator; the bytes must not change."""
+    K, T = 257, 12
+    rng = np.random.default_rng(sum(opts))
+    data = rng.integers(0, 256, K * T, dtype=np.uint8)
+    esis = list(range(K, K + 12)) + [3]
+    out, st = rq.colprog_emulate(K, T, esis, data, opts)
+    enc = oracle.OracleEncoder(data.tobytes(), T)
+    for i, e in enumerate(esis):
+        assert np.array_equal(out[i], enc.gen_symbol(e)), e
+    assert st["spill_stores"] > 0
+
+
+@pytest.mark.parametrize("K,T", [(64, 48), (1024, 8)])
+def test_intermediate_symbols_mode(rq, oracle, K, T):
+    """Per-object encoder program: outputs are C[0..L-1] (RQ/encoder.go:15-33, Encoder.relaxed)."""
+    import ctypes
+    rng = np.random.default_rng(K)
+    data = rng.integers(0, 256, K * T, dtype=np.uint8)
+    p = rq.params(K * T, T)
+    out = np.zeros((p["L"], T), np.uint8)
+    st = np.zeros(12, np.uint32)
+    rc = rq.lib().rq_debug_colprog_eval(K, T, None, 0, data.ctypes.data, out.ctypes.data,
+                                        st.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
+    assert rc == 0
+    assert np.array_equal(out, oracle.encode_C(data, T))
+
+
+def test_program_size_and_assembly(rq):
+    st = rq.colprog_stats(1024, list(range(1024, 1100)))
+    # every XOR / xtime of the schedule is one VALU op of the machine program
+    assert st["valu"] > 5000 and st["src_loads"] == 1024 and st["out_stores"] == 76
+    asm = rq.colprog_asm(64, list(range(64, 80)))
+    assert ".amdhsa_kernel rq_colprog" in asm and "v_bitop3_b32" in asm
+    assert "s_store" not in asm and "s_dcache" not in asm  # vector stores only
+    assert rq.colprog_assemble(64, list(range(64, 80))) > 1000

@@ -196,8 +196,3 @@ def test_batch_decode_not_enough_and_fast_path(gpu, rq):
     assert st[0] == 1 and st[2] == rq.RQ_ERR_NOT_ENOUGH
     assert st[1] in (0, 1)
     assert torch.equal(data[0], src[0])
-
-
-def test_gf_primitives_on_device(gpu, rq):
-    """Packed GF(256) device primitives (v_perm xtime, table multiply) vs host arithmetic."""
-    assert rq.gf_selftest() == (0, 0)
