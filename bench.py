@@ -172,7 +172,7 @@ def main():
             "config": {"workload": "encode+decode K=%d T=%d N=%d erase=%d/%d symbols" % (K, T, N, n_erase, N),
                        "blocks_per_gpu": B, "bytes_per_gpu": B * K * T, "parallelism": "block-sharded x%d" % world,
                        "decode_ok_fraction": ok_frac},
-            "roofline": {"bound": "hbm", "kernel": "rq::k_encode<16, false> (encode batch)", "achieved": round(achieved, 2),
+            "roofline": {"bound": "hbm", "kernel": "rq_colprog_K%d_n%d (encode column program)" % (K, R), "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic, "traffic_source": traffic_src, "encode_ms_per_launch": round(enc_ms, 4),
                          "algorithmic_bytes_per_launch": B * K * T},

@@ -174,11 +174,13 @@ int get_col_kernel(DevCtx* ctx, const Params& p, const uint32_t* esi, uint32_t n
         if (!ok) { ctx->colk.erase(key); return fail(RQ_ERR_PLAN, err); }
         MProg mp;
         if (!allocate_colprog(ir, alloc_options(), &mp, &err)) { ctx->colk.erase(key); return fail(RQ_ERR_PLAN, err); }
-        const std::string src = emit_colprog_asm(mp, "rq_colprog");
+        // distinct symbol per program so kernel traces separate encode, decode and C programs
+        const std::string kname = "rq_colprog_K" + std::to_string(p.K) + (all_C ? "_C" : "_n" + std::to_string(n_esi));
+        const std::string src = emit_colprog_asm(mp, kname);
         std::vector<char> co;
         if (!comgr_assemble(src, &co, &err)) { ctx->colk.erase(key); return fail(RQ_ERR_PLAN, err); }
         if (hipModuleLoadData(&k->mod, co.data()) != hipSuccess ||
-            hipModuleGetFunction(&k->fn, k->mod, "rq_colprog") != hipSuccess) {
+            hipModuleGetFunction(&k->fn, k->mod, kname.c_str()) != hipSuccess) {
             ctx->colk.erase(key);
             return fail(RQ_ERR_DEVICE, "hipModuleLoadData/GetFunction failed for the column program");
         }
