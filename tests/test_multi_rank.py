@@ -1,0 +1,64 @@
+"""N>1 path on CPU: two gloo ranks shard a block batch exactly, time-reduce by max, and agree on the
+aggregate the bench reports (bench.py's multi-GPU logic; SURVEY.md sec. 8e: no data-path collective)."""
+import os
+import sys
+from pathlib import Path
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT / "rl-quic-raptor_amd"))
+import rqshard  # noqa: E402
+
+
+@pytest.mark.parametrize("n,world", [(8192, 8), (8192, 3), (5, 2), (0, 4), (1, 2)])
+def test_shard_partition(n, world):
+    seen = []
+    for r in range(world):
+        s, c = rqshard.shard(n, world, r)
+        seen.extend(range(s, s + c))
+    assert seen == list(range(n))
+    sizes = [rqshard.shard(n, world, r)[1] for r in range(world)]
+    assert max(sizes) - min(sizes) <= 1
+
+
+def test_shard_errors():
+    with pytest.raises(ValueError):
+        rqshard.shard(10, 0, 0)
+    with pytest.raises(ValueError):
+        rqshard.shard(10, 2, 2)
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n_total = 8192
+    s, c = rqshard.shard(n_total, world, rank)
+    seeds = [rqshard.block_seed(b) for b in range(s, s + c)]
+    t = 1.0 + rank  # per-rank wall time
+    dist.barrier()
+    tmax = rqshard.max_over_ranks(t, dist)
+    nsum = rqshard.sum_over_ranks(c, dist)
+    q.put((rank, s, c, seeds[0], tmax, nsum))
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [(r[1], r[2]) for r in res] == [(0, 4096), (4096, 4096)]
+    assert res[1][3] == 1337 + 4096
+    assert all(r[4] == 2.0 for r in res)      # max over ranks
+    assert all(r[5] == 8192 for r in res)     # every block processed exactly once
