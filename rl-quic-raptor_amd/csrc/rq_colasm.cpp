@@ -117,7 +117,11 @@ struct Allocator {
     // a VGPR for an operand / result
     int take_vgpr() {
         if (!freeV.empty()) { const int r = freeV.back(); freeV.pop_back(); return r; }
-        const int r = victim(0, (int)o.n_vgpr);
+        int r = victim(0, (int)o.n_vgpr);
+        while (r < 0 && !pend_loads.empty()) {  // every VGPR awaits a load: retire the oldest
+            wait_seq(pend_loads.front().first);
+            r = victim(0, (int)o.n_vgpr);
+        }
         if (r < 0) { fail("colasm: no evictable VGPR"); return 0; }
         const uint32_t n = nu((uint32_t)owner[r]);
         int a = -1;

@@ -367,15 +367,33 @@ bool build(const Params& p, const std::vector<OutDesc>& outs, ColIR* ir, std::st
         const uint32_t isi = row - S;
         return isi < K ? B.add(IR_LOAD, NOVAL, NOVAL, NOVAL, isi) : NOVAL;
     };
-    // ---- forward pass (peeling order)
+    // ---- forward pass, demand-driven: y_k = D(row_k) ^ XOR of its deps is emitted just before the
+    // column scan first needs it (deps first, iterative DFS), so few y values wait in registers.
     ir->phase_start[0] = 0;
     std::vector<uint32_t> y(npiv, NOVAL);
-    for (uint32_t k = 0; k < npiv; ++k) {
-        std::vector<uint32_t> t;
-        t.push_back(D(e.piv_row[k]));
-        for (uint32_t j : e.deps[k]) t.push_back(y[j]);
-        y[k] = B.xsum(t);
-    }
+    std::vector<uint8_t> ystate(npiv, 0);  // 0 todo, 1 deps pushed, 2 done
+    std::vector<uint32_t> stk;
+    auto getY = [&](uint32_t k0) -> uint32_t {
+        if (ystate[k0] == 2) return y[k0];
+        stk.push_back(k0);
+        while (!stk.empty()) {
+            const uint32_t k = stk.back();
+            if (ystate[k] == 2) { stk.pop_back(); continue; }
+            if (ystate[k] == 0) {
+                ystate[k] = 1;
+                for (auto it = e.deps[k].rbegin(); it != e.deps[k].rend(); ++it)
+                    if (ystate[*it] != 2) stk.push_back(*it);
+                continue;
+            }
+            std::vector<uint32_t> t;
+            t.push_back(D(e.piv_row[k]));
+            for (uint32_t j : e.deps[k]) t.push_back(y[j]);
+            y[k] = B.xsum(t);
+            ystate[k] = 2;
+            stk.pop_back();
+        }
+        return y[k0];
+    };
     // ---- per output: y-part (pivoted columns) and W-hat (U part) -> V1 (n2 bits), V2 (H bits)
     const uint32_t no = (uint32_t)outs.size();
     std::vector<std::vector<uint32_t>> col_outs(e.L);  // column -> outputs using it (odd multiplicity)
@@ -421,7 +439,7 @@ bool build(const Params& p, const std::vector<OutDesc>& outs, ColIR* ir, std::st
     for (uint32_t i = 0; i < n2; ++i) b2acc[i].push(B, D(e.rem[i]));
     uint32_t t = NOVAL;
     for (uint32_t j = 0; j < KS; ++j) {
-        const uint32_t yj = (e.cstate[j] == 1) ? y[(uint32_t)e.col_order[j]] : NOVAL;
+        const uint32_t yj = (e.cstate[j] == 1) ? getY((uint32_t)e.col_order[j]) : NOVAL;
         t = B.xt(t, yj);
         if (j + 1 < KS && t != NOVAL) {
             part[e.ma[j]].push(B, t);
@@ -434,7 +452,7 @@ bool build(const Params& p, const std::vector<OutDesc>& outs, ColIR* ir, std::st
     }
     for (uint32_t c = KS; c < e.L; ++c) {  // pivoted columns past the HDPC range (none in practice)
         if (e.cstate[c] != 1) continue;
-        const uint32_t yc = y[(uint32_t)e.col_order[c]];
+        const uint32_t yc = getY((uint32_t)e.col_order[c]);
         for (uint32_t i : col_rem[c]) b2acc[i].push(B, yc);
         for (uint32_t o : col_outs[c]) oacc[o].push(B, yc);
     }

@@ -36,11 +36,14 @@ struct SolveArgs {
     const uint32_t* rep_uidx;
     const uint8_t* mrep;
     uint32_t mrep_stride;
-    uint64_t* xbits;            // per solved block X as bit planes (rq_kernels.hip k_solve)
+    uint8_t* xcoef;             // per solved block: X[k][m] at xcoef[(m * xc_stride) + k]
     uint16_t* xpiv;             // per solved block max_e received-repair indices (within the block)
-    int32_t* status;            // per block: 1 ok, 0 rank-deficient
+    int32_t* status;            // per block: 1 ok, 0 rank-deficient, ST_FALLBACK (general solver)
     uint32_t max_e;
+    uint32_t xc_stride;         // bytes per m row of xcoef (64 * ceil(max_e / 64))
 };
+constexpr int32_t ST_PENDING = -100;   // queued for the solver
+constexpr int32_t ST_FALLBACK = -101;  // beyond the one-wave solver: general solver decides
 
 struct ApplyArgs {
     const uint32_t* blk_map;
@@ -51,19 +54,22 @@ struct ApplyArgs {
     const uint8_t* recv;        // received repair rows (T bytes each), rep_off order
     const uint8_t* r0;          // n_union rows of T bytes per block
     uint32_t n_union;
-    const uint64_t* xbits;
+    const uint8_t* xcoef;
     const uint16_t* xpiv;
     const int32_t* status;
     uint8_t* data;
     uint64_t data_stride;
     uint32_t T;
     uint32_t max_e;
+    uint32_t xc_stride;
 };
 
 // Launchers (rq_kernels.hip).  Return hipError_t as int.
 int launch_zero_rows(const ZeroArgs& a, void* stream);
-int launch_solve(const SolveArgs& a, uint32_t n_blocks, uint32_t lds_bytes, void* stream);
-int launch_apply(const ApplyArgs& a, uint32_t n_strips, uint32_t n_blocks, uint32_t lds_bytes, void* stream);
+// Fast one-wave solve (e <= 64, first 64 received repairs), then the general solver for the
+// blocks it deferred (lds_bytes sized for the largest e + nr of the batch).
+int launch_solve(const SolveArgs& a, uint32_t n_blocks, uint32_t lds_bytes, bool need_general, void* stream);
+int launch_apply(const ApplyArgs& a, uint32_t n_strips, uint32_t n_blocks, void* stream);
 int launch_gather(const DevParams& p, const uint8_t* C, uint32_t T, const uint32_t* esi, uint32_t n, uint8_t* out,
                   void* stream);
 int upload_tables();  // rand / degree tables to __constant__ memory (once per device)

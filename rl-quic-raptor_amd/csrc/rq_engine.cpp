@@ -285,6 +285,7 @@ int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, v
     std::vector<uint32_t> blk_map, eoff(n_blocks + 1, 0), roff(n_blocks + 1, 0);
     size_t max_lds_solve = 0;
     uint32_t max_e = 0;
+    bool need_general = false;  // some block may exceed the one-wave solver (e or nr > 64)
     for (uint32_t b = 0; b < n_blocks; ++b) {
         eoff[b + 1] = eoff[b] + n_erased[b];
         roff[b + 1] = roff[b] + n_repair[b];
@@ -300,7 +301,8 @@ int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, v
         if (e == 0) { status[b] = 1; continue; }
         const size_t need = (size_t)nr * (e + nr);
         if (e > MAX_E || nr > 255 || need > 140 * 1024) { status[b] = RQ_ERR_UNSUPPORTED; continue; }
-        status[b] = -100;  // pending
+        status[b] = ST_PENDING;
+        need_general |= (e > 64 || nr > 64);
         blk_map.push_back(b);
         max_lds_solve = std::max(max_lds_solve, need);
         max_e = std::max(max_e, e);
@@ -343,9 +345,9 @@ int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, v
         for (uint32_t i = eoff[b]; i < eoff[b + 1]; ++i) idx.push_back(erased[i]);
     if ((rc = upload(ctx->ws_idx, idx, stream))) return rc;
     const uint32_t* di = ctx->ws_idx.as<uint32_t>();
-    const uint32_t nkc = (max_e + 63) / 64;
+    const uint32_t xc_stride = 64 * ((max_e + 63) / 64);
     if ((rc = ctx->ws_r0.ensure((size_t)n_blocks * uni.size() * T))) return rc;
-    if ((rc = ctx->ws_xb.ensure((size_t)nw * nkc * max_e * 8 * 8))) return rc;
+    if ((rc = ctx->ws_xb.ensure((size_t)nw * max_e * xc_stride))) return rc;
     if ((rc = ctx->ws_xp.ensure((size_t)nw * max_e * 2))) return rc;
 
     // 1) erased rows := 0, then r0 = the column program on every block (syndromes s = r ^ r0)
@@ -364,11 +366,13 @@ int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, v
     s.rep_uidx = di + o_ru;
     s.mrep = k->mrep.as<uint8_t>();
     s.mrep_stride = k->mrep_stride;
-    s.xbits = ctx->ws_xb.as<uint64_t>();
+    s.xcoef = ctx->ws_xb.as<uint8_t>();
     s.xpiv = ctx->ws_xp.as<uint16_t>();
     s.status = reinterpret_cast<int32_t*>(ctx->ws_idx.as<uint32_t>() + o_st);
     s.max_e = max_e;
-    if (launch_solve(s, nw, (uint32_t)((max_lds_solve + 15) & ~size_t(15)), stream)) return fail(RQ_ERR_DEVICE, "k_solve launch failed");
+    s.xc_stride = xc_stride;
+    if (launch_solve(s, nw, (uint32_t)((max_lds_solve + 15) & ~size_t(15)), need_general, stream))
+        return fail(RQ_ERR_DEVICE, "k_solve launch failed");
     // 3) apply: x_E = X * s
     ApplyArgs ap;
     ap.blk_map = di + o_map;
@@ -379,14 +383,15 @@ int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, v
     ap.recv = static_cast<const uint8_t*>(repair);
     ap.r0 = ctx->ws_r0.as<uint8_t>();
     ap.n_union = (uint32_t)uni.size();
-    ap.xbits = s.xbits;
+    ap.xcoef = s.xcoef;
     ap.xpiv = s.xpiv;
     ap.status = s.status;
     ap.data = static_cast<uint8_t*>(data);
     ap.data_stride = data_stride;
     ap.T = T;
     ap.max_e = max_e;
-    if (launch_apply(ap, (T / 4 + 63) / 64, nw, 0, stream)) return fail(RQ_ERR_DEVICE, "k_apply launch failed");
+    ap.xc_stride = xc_stride;
+    if (launch_apply(ap, (T / 4 + 63) / 64, nw, stream)) return fail(RQ_ERR_DEVICE, "k_apply launch failed");
     std::vector<int32_t> st(n_blocks);
     HIP_TRY(hipMemcpyAsync(st.data(), ctx->ws_idx.as<uint32_t>() + o_st, n_blocks * 4, hipMemcpyDeviceToHost,
                            (hipStream_t)stream));

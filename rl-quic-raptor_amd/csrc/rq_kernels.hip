@@ -93,25 +93,14 @@ int launch_zero_rows(const ZeroArgs& a, void* stream) {
 // M[j][k] = mrep[uidx_j][e_k] (received repair j, erased source e_k); Gauss-Jordan on [M | I]
 // (replaces GaussianElimination, RQ/discmath/gauss.go:7-45, on the e erased columns only):
 // rank e <=> the reference's system is full rank.
-// Output: X (e x e) and the e received repairs it combines: x_k = sum_m X[k][m] s_{piv[m]}.
+// Output: X (e x e) and the e received repairs it combines: x_k = sum_m X[k][m] s_{piv[m]}, stored
+// as xcoef[m * xc_stride + k] (one uniform 64-byte row per m for k_apply's scalar loads).
 __device__ __forceinline__ uint8_t gmul_t(const uint8_t* lg, const uint8_t* ex, uint8_t a, uint8_t b) {
     return (a && b) ? ex[lg[a] + lg[b]] : (uint8_t)0;
 }
 
-__global__ void __launch_bounds__(256) k_solve(SolveArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
-    __shared__ uint8_t ex[512], lg[256];
-    __shared__ uint8_t fac[256];
-    __shared__ uint16_t rowid[256];
-    __shared__ int piv;
-    const uint32_t b = a.blk_map[blockIdx.x];
-    const uint32_t tid = threadIdx.x, nthr = blockDim.x;
-    const uint32_t e = a.erased_off[b + 1] - a.erased_off[b];
-    const uint32_t nr = a.rep_off[b + 1] - a.rep_off[b];
-    const uint32_t* E = a.erased + a.erased_off[b];
-    const uint32_t* U = a.rep_uidx + a.rep_off[b];
-    const uint32_t ws = e + nr;
-    if (tid == 0) {
+__device__ __forceinline__ void gf_tables(uint8_t* ex, uint8_t* lg) {
+    if (threadIdx.x == 0) {
         uint32_t x = 1;
         for (int i = 0; i < 255; ++i) {
             ex[i] = (uint8_t)x; ex[i + 255] = (uint8_t)x; lg[x] = (uint8_t)i;
@@ -119,6 +108,125 @@ __global__ void __launch_bounds__(256) k_solve(SolveArgs a) {
         }
         ex[510] = ex[0]; ex[511] = ex[1]; lg[0] = 0;
     }
+}
+
+// One wave per block.  Lane j owns received repair j (j < 64) as a 128-byte LDS row: e coefficient
+// bytes, then the identity part (byte e + j).  Each step picks the lowest unused lane with a nonzero
+// coefficient (ballot), scales its row by the inverse, stores the eight alpha^b multiples of the
+// scaled row, and every other lane XORs in the multiples its own coefficient's bits select.
+constexpr uint32_t S64_W = 33;  // dwords per LDS row (32 + 1 pad: rows hit distinct banks)
+
+__global__ void __launch_bounds__(64) k_solve64(SolveArgs a) {
+    __shared__ uint32_t rows[64 * S64_W];
+    __shared__ uint32_t mult[8][32];
+    __shared__ uint8_t ex[512], lg[256];
+    __shared__ uint8_t pivl[64];
+    const uint32_t b = a.blk_map[blockIdx.x];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t e = a.erased_off[b + 1] - a.erased_off[b];
+    const uint32_t nr = a.rep_off[b + 1] - a.rep_off[b];
+    if (e > 64) {
+        if (lane == 0) a.status[b] = ST_FALLBACK;
+        return;
+    }
+    const uint32_t nrow = min(nr, 64u);
+    const uint32_t* E = a.erased + a.erased_off[b];
+    const uint32_t* U = a.rep_uidx + a.rep_off[b];
+    gf_tables(ex, lg);
+    uint32_t* my = rows + lane * S64_W;
+    {
+        uint32_t w[32];
+#pragma unroll
+        for (int d = 0; d < 32; ++d) w[d] = 0;
+        if (lane < nrow) {
+            const uint8_t* mr = a.mrep + (size_t)U[lane] * a.mrep_stride;
+            for (uint32_t k = 0; k < e; ++k) {
+                const uint32_t v = mr[E[k]];
+#pragma unroll
+                for (int d = 0; d < 32; ++d)
+                    if ((k >> 2) == (uint32_t)d) w[d] |= v << ((k & 3) * 8);
+            }
+            const uint32_t id = e + lane;
+#pragma unroll
+            for (int d = 0; d < 32; ++d)
+                if ((id >> 2) == (uint32_t)d) w[d] |= 1u << ((id & 3) * 8);
+        }
+#pragma unroll
+        for (int d = 0; d < 32; ++d) my[d] = w[d];
+    }
+    __syncthreads();
+    bool used = lane >= nrow;
+    for (uint32_t k = 0; k < e; ++k) {
+        const uint32_t f = (my[k >> 2] >> ((k & 3) * 8)) & 0xFFu;
+        const uint64_t bal = __ballot(f != 0 && !used);
+        if (bal == 0) {
+            if (lane == 0) a.status[b] = (nr > nrow) ? ST_FALLBACK : 0;
+            return;
+        }
+        const uint32_t p = (uint32_t)__ffsll((unsigned long long)bal) - 1;
+        if (lane == p) used = true;
+        if (lane == 0) pivl[k] = (uint8_t)p;
+        const uint32_t fp = __shfl(f, p);
+        const uint32_t inv = ex[255 - lg[fp]];
+        if (lane < 32) {  // scaled pivot row and its alpha multiples
+            uint32_t x = rows[p * S64_W + lane], r = 0;
+#pragma unroll
+            for (int bt = 0; bt < 8; ++bt) {
+                if ((inv >> bt) & 1u) r ^= x;
+                x = xtime4(x);
+            }
+#pragma unroll
+            for (int bt = 0; bt < 8; ++bt) {
+                mult[bt][lane] = r;
+                r = xtime4(r);
+            }
+        }
+        __syncthreads();
+        if (lane == p) {
+#pragma unroll
+            for (int d = 0; d < 32; ++d) my[d] = mult[0][d];
+        } else if (f) {
+            uint32_t msk[8];
+#pragma unroll
+            for (int bt = 0; bt < 8; ++bt) msk[bt] = 0u - ((f >> bt) & 1u);
+#pragma unroll
+            for (int d = 0; d < 32; ++d) {
+                uint32_t r = my[d];
+#pragma unroll
+                for (int bt = 0; bt < 8; ++bt) r ^= mult[bt][d] & msk[bt];
+                my[d] = r;
+            }
+        }
+        __syncthreads();
+    }
+    // X[k][m] = identity byte (e + piv_m) of pivot row piv_k
+    uint8_t* xc = a.xcoef + (size_t)blockIdx.x * a.max_e * a.xc_stride;
+    uint16_t* XP = a.xpiv + (size_t)blockIdx.x * a.max_e;
+    const uint8_t* rb = reinterpret_cast<const uint8_t*>(rows);
+    for (uint32_t m = lane; m < e; m += 64) XP[m] = pivl[m];
+    for (uint32_t idx = lane; idx < e * e; idx += 64) {
+        const uint32_t m = idx / e, k = idx - m * e;
+        xc[m * a.xc_stride + k] = rb[pivl[k] * S64_W * 4 + e + pivl[m]];
+    }
+    if (lane == 0) a.status[b] = 1;
+}
+
+// General solver (any e, nr with nr*(e+nr) bytes in LDS) for the blocks k_solve64 deferred.
+__global__ void __launch_bounds__(256) k_solve(SolveArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
+    __shared__ uint8_t ex[512], lg[256];
+    __shared__ uint8_t fac[256];
+    __shared__ uint16_t rowid[256];
+    __shared__ int piv;
+    const uint32_t b = a.blk_map[blockIdx.x];
+    if (a.status[b] != ST_FALLBACK) return;
+    const uint32_t tid = threadIdx.x, nthr = blockDim.x;
+    const uint32_t e = a.erased_off[b + 1] - a.erased_off[b];
+    const uint32_t nr = a.rep_off[b + 1] - a.rep_off[b];
+    const uint32_t* E = a.erased + a.erased_off[b];
+    const uint32_t* U = a.rep_uidx + a.rep_off[b];
+    const uint32_t ws = e + nr;
+    gf_tables(ex, lg);
     for (uint32_t r = tid; r < nr; r += nthr) rowid[r] = (uint16_t)r;
     for (uint32_t idx = tid; idx < nr * ws; idx += nthr) {
         const uint32_t j = idx / ws, k = idx - j * ws;
@@ -156,23 +264,21 @@ __global__ void __launch_bounds__(256) k_solve(SolveArgs a) {
         }
         __syncthreads();
     }
-    // X as bit planes: xb[(kc * e + m) * 8 + bit] has bit k of X[64*kc + k][m]'s bit `bit`
-    const uint32_t nkc = (a.max_e + 63) / 64;
-    uint64_t* xb = a.xbits + (size_t)blockIdx.x * nkc * a.max_e * 8;
+    uint8_t* xc = a.xcoef + (size_t)blockIdx.x * a.max_e * a.xc_stride;
     uint16_t* XP = a.xpiv + (size_t)blockIdx.x * a.max_e;
     for (uint32_t m = tid; m < e; m += nthr) XP[m] = rowid[m];
     __syncthreads();
-    for (uint32_t idx = tid; idx < ((e + 63) / 64) * e * 8; idx += nthr) {
-        const uint32_t bt = idx & 7, m = (idx >> 3) % e, kc = (idx >> 3) / e;
-        uint64_t w = 0;
-        for (uint32_t k = 0; k < 64 && kc * 64 + k < e; ++k)
-            w |= (uint64_t)((sm[(kc * 64 + k) * ws + e + rowid[m]] >> bt) & 1u) << k;
-        xb[idx] = w;
+    for (uint32_t idx = tid; idx < e * e; idx += nthr) {
+        const uint32_t m = idx / e, k = idx - m * e;
+        xc[m * a.xc_stride + k] = sm[k * ws + e + rowid[m]];
     }
     if (tid == 0) a.status[b] = 1;
 }
 
-int launch_solve(const SolveArgs& a, uint32_t n_blocks, uint32_t lds_bytes, void* stream) {
+int launch_solve(const SolveArgs& a, uint32_t n_blocks, uint32_t lds_bytes, bool need_general, void* stream) {
+    hipLaunchKernelGGL(k_solve64, dim3(n_blocks), dim3(64), 0, (hipStream_t)stream, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || !need_general) return (int)e;
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)k_solve, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
@@ -184,11 +290,10 @@ int launch_solve(const SolveArgs& a, uint32_t n_blocks, uint32_t lds_bytes, void
 
 // ------------------------------ decode: x_E = X * s ------------------------------------------
 // grid = (strips of 64 dwords, solved blocks), one wave.  s_m = recv_{piv m} ^ r0_{piv m} (the
-// syndrome, formed on the fly).  GF(256) by bit decomposition: for each source m the eight
-// multiples alpha^b s_m are built by xtime and XORed into every output k whose coefficient has
-// bit b set (uniform masks) -- 8 bitwise ops per mul-add, no tables.
-constexpr uint32_t APPLY_KC = 64;  // outputs per pass (registers)
-
+// syndrome, formed on the fly).  GF(256) by bit decomposition: the eight multiples alpha^b s_m are
+// built by xtime, and output k takes those its coefficient X[k][m] selects.  X[k][m] is uniform
+// (scalar loads), so a selection is one s_bfe_i32 mask and one v_bitop3 per bit.
+template <int KC>
 __global__ void __launch_bounds__(64) k_apply(ApplyArgs a) {
     const uint32_t b = a.blk_map[blockIdx.y];
     if (a.status[b] != 1) return;
@@ -197,44 +302,63 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a) {
     const uint32_t Td = a.T >> 2, c = blockIdx.x * 64 + lane;
     const bool live = c < Td;
     const uint32_t* E = a.erased + a.erased_off[b];
-    const uint32_t nkc = (a.max_e + 63) / 64;
-    const uint64_t* xb = a.xbits + (size_t)blockIdx.y * nkc * a.max_e * 8;
+    const uint8_t* xc = a.xcoef + (size_t)blockIdx.y * a.max_e * a.xc_stride;
     const uint16_t* XP = a.xpiv + (size_t)blockIdx.y * a.max_e;
     const uint32_t r0b = a.rep_off[b];
+    const uint32_t* recv = reinterpret_cast<const uint32_t*>(a.recv);
+    const uint32_t* r0 = reinterpret_cast<const uint32_t*>(a.r0) + (size_t)b * a.n_union * Td;
     uint8_t* blk = a.data + (size_t)b * a.data_stride;
-    for (uint32_t kc = 0; kc * APPLY_KC < e; ++kc) {
-        const uint32_t k0 = kc * APPLY_KC, kn = min(APPLY_KC, e - k0);
-        uint32_t acc[APPLY_KC];
+    for (uint32_t k0 = 0; k0 < e; k0 += KC) {
+        uint32_t acc[KC];
 #pragma unroll
-        for (uint32_t k = 0; k < APPLY_KC; ++k) acc[k] = 0;
+        for (int k = 0; k < KC; ++k) acc[k] = 0;
+        const uint32_t cc = live ? c : 0;
         for (uint32_t m = 0; m < e; ++m) {
             const uint32_t j = r0b + XP[m];
-            uint32_t s = 0;
-            if (live) {
-                s = reinterpret_cast<const uint32_t*>(a.recv + (size_t)j * a.T)[c] ^
-                    reinterpret_cast<const uint32_t*>(a.r0 + ((size_t)b * a.n_union + a.rep_uidx[j]) * a.T)[c];
-            }
-            const uint64_t* w = xb + ((size_t)kc * e + m) * 8;
+            uint32_t s = recv[(size_t)j * Td + cc] ^ r0[(size_t)a.rep_uidx[j] * Td + cc];
+            const uint32_t* cw = reinterpret_cast<const uint32_t*>(xc + (size_t)m * a.xc_stride + k0);
+            uint32_t mul[8];
 #pragma unroll
-            for (uint32_t bt = 0; bt < 8; ++bt) {
-                const uint64_t wb = w[bt];
-                const uint32_t lo = (uint32_t)wb, hi = (uint32_t)(wb >> 32);
-#pragma unroll
-                for (uint32_t k = 0; k < APPLY_KC; ++k) {
-                    const uint32_t word = k < 32 ? lo : hi;
-                    const uint32_t msk = 0u - ((word >> (k & 31)) & 1u);
-                    acc[k] ^= s & msk;
-                }
+            for (int bt = 0; bt < 8; ++bt) {
+                mul[bt] = s;
                 s = xtime4(s);
             }
+#pragma unroll
+            for (int kq = 0; kq < KC / 16; ++kq) {
+                const uint4 w4 = reinterpret_cast<const uint4*>(cw)[kq];
+                const uint32_t wv[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+                for (int kw = 0; kw < 4; ++kw) {
+                    const int w = __builtin_amdgcn_readfirstlane((int)wv[kw]);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+                        for (int bt = 0; bt < 8; ++bt) {
+                            const int msk = __builtin_amdgcn_sbfe(w, q * 8 + bt, 1);
+                            // acc ^= mul & msk  (v_bitop3: src0 acc 0xF0, src1 mul 0xCC, src2 msk 0xAA)
+                            asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x78"
+                                         : "+v"(acc[kq * 16 + kw * 4 + q])
+                                         : "v"(mul[bt]), "s"(msk));
+                        }
+                    }
+                }
+            }
         }
-        if (live)
-            for (uint32_t k = 0; k < kn; ++k) reinterpret_cast<uint32_t*>(blk + (size_t)E[k0 + k] * a.T)[c] = acc[k];
+        if (live) {
+            const uint32_t kn = min((uint32_t)KC, e - k0);
+#pragma unroll
+            for (int k = 0; k < KC; ++k)
+                if ((uint32_t)k < kn) reinterpret_cast<uint32_t*>(blk + (size_t)E[k0 + k] * a.T)[c] = acc[k];
+        }
     }
 }
 
-int launch_apply(const ApplyArgs& a, uint32_t n_strips, uint32_t n_blocks, uint32_t /*lds_bytes*/, void* stream) {
-    hipLaunchKernelGGL(k_apply, dim3(n_strips, n_blocks), dim3(64), 0, (hipStream_t)stream, a);
+int launch_apply(const ApplyArgs& a, uint32_t n_strips, uint32_t n_blocks, void* stream) {
+    const dim3 g(n_strips, n_blocks);
+    if (a.max_e <= 16) hipLaunchKernelGGL(k_apply<16>, g, dim3(64), 0, (hipStream_t)stream, a);
+    else if (a.max_e <= 32) hipLaunchKernelGGL(k_apply<32>, g, dim3(64), 0, (hipStream_t)stream, a);
+    else if (a.max_e <= 48) hipLaunchKernelGGL(k_apply<48>, g, dim3(64), 0, (hipStream_t)stream, a);
+    else hipLaunchKernelGGL(k_apply<64>, g, dim3(64), 0, (hipStream_t)stream, a);
     return (int)hipGetLastError();
 }
 

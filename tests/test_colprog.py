@@ -46,7 +46,7 @@ def test_machine_program_matches_oracle(rq, oracle, K, T, nrep):
     assert st["sync_reloads"] <= st["spill_loads"]
 
 
-@pytest.mark.parametrize("opts", [[64, 32, 40, 20, 8], [32, 0, 400, 400, 60], [200, 8, 16, 8, 4]])
+@pytest.mark.parametrize("opts", [[64, 32, 40, 20, 8], [32, 4, 400, 400, 60], [200, 8, 16, 8, 4]])
 def test_machine_program_under_register_pressure(rq, oracle, opts):
     """Tight register files, short/long look-aheads and a small vmcnt budget force every spill /
     reload / wait path of the allocator; the bytes must not change."""
