@@ -246,10 +246,19 @@ int encode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, c
 // multiple of 16) when the received ESIs are not too sparse -- one compiled program then serves
 // every erasure pattern of that range -- otherwise the exact sorted set.
 std::vector<uint32_t> decode_union(uint32_t K, const std::vector<uint32_t>& rep) {
-    std::vector<uint32_t> u(rep);
-    std::sort(u.begin(), u.end());
-    u.erase(std::unique(u.begin(), u.end()), u.end());
-    if (u.empty()) return u;
+    std::vector<uint32_t> u;
+    if (rep.empty()) return u;
+    const uint32_t mx = *std::max_element(rep.begin(), rep.end());
+    if ((uint64_t)mx - K < (1u << 22)) {  // presence map: O(n), no sort of the per-block lists
+        std::vector<uint8_t> seen((size_t)(mx - K) + 1, 0);
+        for (uint32_t e : rep) seen[e - K] = 1;
+        for (size_t i = 0; i < seen.size(); ++i)
+            if (seen[i]) u.push_back(K + (uint32_t)i);
+    } else {
+        u = rep;
+        std::sort(u.begin(), u.end());
+        u.erase(std::unique(u.begin(), u.end()), u.end());
+    }
     const uint64_t span = ((uint64_t)u.back() - K + 16) & ~(uint64_t)15;
     if (span <= 4 * u.size() + 64) {
         std::vector<uint32_t> r((size_t)span);
@@ -314,9 +323,8 @@ int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, v
     ColKernel* k;
     if ((rc = get_col_kernel(ctx, p, uni.data(), (uint32_t)uni.size(), false, &k))) return rc;
     if ((rc = ensure_mrep(ctx, k, stream))) return rc;
-    // union index of every received repair
-    std::map<uint32_t, uint32_t> upos;
-    for (uint32_t i = 0; i < uni.size(); ++i) upos[uni[i]] = i;
+    // union index of every received repair: direct for a dense union, binary search otherwise
+    const bool dense_uni = uni.back() - uni.front() + 1 == uni.size();
     const size_t n_er = eoff[n_blocks], n_rep = roff[n_blocks];
     // index workspace: blk_map | eoff | roff | erased | rep_uidx | status | zero (blk, row) lists
     std::vector<uint32_t> idx;
@@ -331,8 +339,13 @@ int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, v
     idx.insert(idx.end(), erased, erased + n_er);
     const size_t o_ru = idx.size();
     for (size_t i = 0; i < n_rep; ++i) {
-        auto it = upos.find(repair_esi[i]);
-        idx.push_back(it == upos.end() ? 0u : it->second);
+        const uint32_t x = repair_esi[i];
+        if (dense_uni) {
+            idx.push_back(x >= uni.front() && x - uni.front() < uni.size() ? x - uni.front() : 0u);
+        } else {
+            const auto it = std::lower_bound(uni.begin(), uni.end(), x);
+            idx.push_back(it != uni.end() && *it == x ? (uint32_t)(it - uni.begin()) : 0u);
+        }
     }
     const size_t o_st = idx.size();
     idx.resize(idx.size() + n_blocks, 0);
