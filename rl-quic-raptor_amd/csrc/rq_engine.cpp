@@ -76,12 +76,30 @@ struct ColKernel {
     ~ColKernel() { if (mod) (void)hipModuleUnload(mod); }
 };
 
+// Pinned host staging (descriptor uploads and status downloads run as true async copies).
+struct HostBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t n) {
+        if (n <= cap) return RQ_OK;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        const size_t want = std::max<size_t>(n, 1 << 16);
+        if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) return fail(RQ_ERR_DEVICE, "hipHostMalloc failed");
+        cap = want;
+        return RQ_OK;
+    }
+    ~HostBuf() { if (p) (void)hipHostFree(p); }
+};
+
 struct DevCtx {
     int device = -1;
     std::mutex mu;
     bool tables = false;
     std::map<std::string, std::unique_ptr<ColKernel>> colk;  // keyed by (K', K, outputs)
     DevBuf ws_idx, ws_r0, ws_xb, ws_xp, ws_scratch;
+    HostBuf h_idx, h_status;
 };
 
 std::mutex g_ctx_mu;
@@ -356,7 +374,13 @@ int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, v
     const size_t o_zr = idx.size();
     for (uint32_t b : blk_map)
         for (uint32_t i = eoff[b]; i < eoff[b + 1]; ++i) idx.push_back(erased[i]);
-    if ((rc = upload(ctx->ws_idx, idx, stream))) return rc;
+    // descriptor upload through pinned staging: the copy is queued behind the caller's work on the
+    // stream (e.g. the encode that produced `repair`) without blocking this thread
+    if ((rc = ctx->ws_idx.ensure(idx.size() * 4)) || (rc = ctx->h_idx.ensure(idx.size() * 4)) ||
+        (rc = ctx->h_status.ensure((size_t)n_blocks * 4)))
+        return rc;
+    std::memcpy(ctx->h_idx.p, idx.data(), idx.size() * 4);
+    HIP_TRY(hipMemcpyAsync(ctx->ws_idx.p, ctx->h_idx.p, idx.size() * 4, hipMemcpyHostToDevice, (hipStream_t)stream));
     const uint32_t* di = ctx->ws_idx.as<uint32_t>();
     const uint32_t xc_stride = 64 * ((max_e + 63) / 64);
     if ((rc = ctx->ws_r0.ensure((size_t)n_blocks * uni.size() * T))) return rc;
@@ -405,8 +429,8 @@ int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, v
     ap.max_e = max_e;
     ap.xc_stride = xc_stride;
     if (launch_apply(ap, (T / 4 + 63) / 64, nw, stream)) return fail(RQ_ERR_DEVICE, "k_apply launch failed");
-    std::vector<int32_t> st(n_blocks);
-    HIP_TRY(hipMemcpyAsync(st.data(), ctx->ws_idx.as<uint32_t>() + o_st, n_blocks * 4, hipMemcpyDeviceToHost,
+    int32_t* st = static_cast<int32_t*>(ctx->h_status.p);
+    HIP_TRY(hipMemcpyAsync(st, ctx->ws_idx.as<uint32_t>() + o_st, n_blocks * 4, hipMemcpyDeviceToHost,
                            (hipStream_t)stream));
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
     for (uint32_t b : blk_map) status[b] = st[b];

@@ -114,11 +114,11 @@ __device__ __forceinline__ void gf_tables(uint8_t* ex, uint8_t* lg) {
 // bytes, then the identity part (byte e + j).  Each step picks the lowest unused lane with a nonzero
 // coefficient (ballot), scales its row by the inverse, stores the eight alpha^b multiples of the
 // scaled row, and every other lane XORs in the multiples its own coefficient's bits select.
-constexpr uint32_t S64_W = 33;  // dwords per LDS row (32 + 1 pad: rows hit distinct banks)
+constexpr uint32_t S64_W = 36;  // dwords per LDS row (128 B + 16 B pad; 16-B aligned for b128 access)
 
 __global__ void __launch_bounds__(64) k_solve64(SolveArgs a) {
-    __shared__ uint32_t rows[64 * S64_W];
-    __shared__ uint32_t mult[8][32];
+    __shared__ __attribute__((aligned(16))) uint32_t rows[64 * S64_W];
+    __shared__ __attribute__((aligned(16))) uint4 mult[8][8];  // alpha^b * scaled pivot row, 8 quads
     __shared__ uint8_t ex[512], lg[256];
     __shared__ uint8_t pivl[64];
     const uint32_t b = a.blk_map[blockIdx.x];
@@ -134,27 +134,17 @@ __global__ void __launch_bounds__(64) k_solve64(SolveArgs a) {
     const uint32_t* U = a.rep_uidx + a.rep_off[b];
     gf_tables(ex, lg);
     uint32_t* my = rows + lane * S64_W;
-    {
-        uint32_t w[32];
+    uint4* my4 = reinterpret_cast<uint4*>(my);
 #pragma unroll
-        for (int d = 0; d < 32; ++d) w[d] = 0;
-        if (lane < nrow) {
-            const uint8_t* mr = a.mrep + (size_t)U[lane] * a.mrep_stride;
-            for (uint32_t k = 0; k < e; ++k) {
-                const uint32_t v = mr[E[k]];
-#pragma unroll
-                for (int d = 0; d < 32; ++d)
-                    if ((k >> 2) == (uint32_t)d) w[d] |= v << ((k & 3) * 8);
-            }
-            const uint32_t id = e + lane;
-#pragma unroll
-            for (int d = 0; d < 32; ++d)
-                if ((id >> 2) == (uint32_t)d) w[d] |= 1u << ((id & 3) * 8);
-        }
-#pragma unroll
-        for (int d = 0; d < 32; ++d) my[d] = w[d];
+    for (int q = 0; q < 8; ++q) my4[q] = make_uint4(0, 0, 0, 0);
+    if (lane < nrow) {
+        uint8_t* myb = reinterpret_cast<uint8_t*>(my);
+        const uint8_t* mr = a.mrep + (size_t)U[lane] * a.mrep_stride;
+        for (uint32_t k = 0; k < e; ++k) myb[k] = mr[E[k]];
+        myb[e + lane] = 1;
     }
     __syncthreads();
+    const uint32_t q1 = (e + nrow + 15) >> 4;  // quads holding live columns
     bool used = lane >= nrow;
     for (uint32_t k = 0; k < e; ++k) {
         const uint32_t f = (my[k >> 2] >> ((k & 3) * 8)) & 0xFFu;
@@ -175,26 +165,33 @@ __global__ void __launch_bounds__(64) k_solve64(SolveArgs a) {
                 if ((inv >> bt) & 1u) r ^= x;
                 x = xtime4(x);
             }
+            uint32_t* mflat = reinterpret_cast<uint32_t*>(mult);
 #pragma unroll
             for (int bt = 0; bt < 8; ++bt) {
-                mult[bt][lane] = r;
+                mflat[bt * 32 + lane] = r;
                 r = xtime4(r);
             }
         }
         __syncthreads();
+        // columns < k are zero in the pivot row (all are earlier pivot columns): start at quad k/16
+        const uint32_t q0 = k >> 4;
         if (lane == p) {
-#pragma unroll
-            for (int d = 0; d < 32; ++d) my[d] = mult[0][d];
+            for (uint32_t q = q0; q < q1; ++q) my4[q] = mult[0][q];
         } else if (f) {
             uint32_t msk[8];
 #pragma unroll
             for (int bt = 0; bt < 8; ++bt) msk[bt] = 0u - ((f >> bt) & 1u);
+            for (uint32_t q = q0; q < q1; ++q) {
+                uint4 r = my4[q];
 #pragma unroll
-            for (int d = 0; d < 32; ++d) {
-                uint32_t r = my[d];
-#pragma unroll
-                for (int bt = 0; bt < 8; ++bt) r ^= mult[bt][d] & msk[bt];
-                my[d] = r;
+                for (int bt = 0; bt < 8; ++bt) {
+                    const uint4 m = mult[bt][q];
+                    r.x ^= m.x & msk[bt];
+                    r.y ^= m.y & msk[bt];
+                    r.z ^= m.z & msk[bt];
+                    r.w ^= m.w & msk[bt];
+                }
+                my4[q] = r;
             }
         }
         __syncthreads();
