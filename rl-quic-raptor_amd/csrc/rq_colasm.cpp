@@ -24,19 +24,24 @@ struct Allocator {
     std::vector<uint32_t> uptr;
     std::vector<int16_t> reg;                       // value -> register or -1
     std::vector<int32_t> slot;                      // value -> scratch slot with a valid copy or -1
+    std::vector<int32_t> lslot;                     // value -> LDS slot with a valid copy or -1
     std::vector<uint8_t> issued;                    // LOAD value already issued
     int32_t owner[512];
-    uint64_t inflight[512];
+    uint64_t inflight[512];                         // vector-memory load into the register (seq) or 0
+    uint64_t linflight[512];                        // LDS load into the register (lgkm seq) or 0
     uint8_t pinned[512];
     int last_accw[512];                             // instruction index of the last ACCW into an AGPR
     std::vector<int> freeV, freeA;
-    std::vector<int32_t> free_slots;
+    std::vector<int32_t> free_slots, free_lslots;
     std::vector<uint64_t> slot_st, slot_ld;         // last store / load seq per slot
     uint64_t seq = 0, retired = 0;
     std::deque<std::pair<uint64_t, int>> pend_loads;  // (seq, reg)
+    uint64_t lseq = 0, lretired = 0;                // LDS operations (lgkmcnt, in order, max 15)
+    std::deque<std::pair<uint64_t, int>> pend_lds;
     using HE = std::pair<uint32_t, uint32_t>;       // (next use, value)
     std::priority_queue<HE, std::vector<HE>, std::greater<HE>> reload_q;
     bool failed = false;
+    uint32_t cur = 0;                               // IR node being allocated
 
     Allocator(const ColIR& i, const AllocOpts& op, MProg* m, std::string* e) : ir(i), o(op), mp(m), err(e) {}
 
@@ -79,6 +84,32 @@ struct Allocator {
         return ++seq;
     }
 
+    void retire_l(uint64_t s) {
+        if (s <= lretired) return;
+        lretired = s;
+        while (!pend_lds.empty() && pend_lds.front().first <= lretired) {
+            const int r = pend_lds.front().second;
+            if (linflight[r] == pend_lds.front().first) linflight[r] = 0;
+            pend_lds.pop_front();
+        }
+    }
+    void wait_lseq(uint64_t s) {
+        if (s == 0 || s <= lretired) return;
+        const uint64_t n = std::min<uint64_t>(lseq - s, 15);
+        emit(MI_WAITL, -1, -1, -1, -1, (uint32_t)n);
+        mp->st.waitl++;
+        retire_l(lseq - n);
+    }
+    uint64_t issue_lgkm() {
+        if (lseq - lretired >= 15) {
+            emit(MI_WAITL, -1, -1, -1, -1, 14);
+            mp->st.waitl++;
+            retire_l(lseq - 14);
+        }
+        return ++lseq;
+    }
+    bool busy(int r) const { return inflight[r] || linflight[r]; }
+
     // ---- scratch ----
     int32_t new_slot() {
         int32_t s;
@@ -91,7 +122,17 @@ struct Allocator {
     // value in register r -> scratch copy (if none); r becomes free (not pushed to a free list)
     void spill_out(int r) {
         const int32_t v = owner[r];
-        if (slot[v] < 0) {
+        if (slot[v] < 0 && lslot[v] < 0 && !free_lslots.empty() &&  // LDS tier for nearer reuse
+            nu((uint32_t)v) < cur + o.lds_horizon) {
+            const int32_t s = free_lslots.back();
+            free_lslots.pop_back();
+            mp->n_lds_slots = std::max<uint32_t>(mp->n_lds_slots, (uint32_t)s + 1);
+            issue_lgkm();
+            emit(MI_LDST, -1, r, -1, -1, (uint32_t)s);
+            mp->st.ldst++;
+            lslot[v] = s;
+        }
+        if (slot[v] < 0 && lslot[v] < 0) {
             const int32_t s = new_slot();
             const uint64_t q = issue_vmem();
             emit(MI_SPST, -1, r, -1, -1, (uint32_t)s);
@@ -108,7 +149,7 @@ struct Allocator {
         uint32_t bn = 0;
         for (int r = lo; r < hi; ++r) {
             const int32_t v = owner[r];
-            if (v < 0 || pinned[r] || inflight[r]) continue;
+            if (v < 0 || pinned[r] || busy(r)) continue;
             const uint32_t n = nu((uint32_t)v);
             if (best < 0 || n > bn) { best = r; bn = n; }
         }
@@ -118,8 +159,9 @@ struct Allocator {
     int take_vgpr() {
         if (!freeV.empty()) { const int r = freeV.back(); freeV.pop_back(); return r; }
         int r = victim(0, (int)o.n_vgpr);
-        while (r < 0 && !pend_loads.empty()) {  // every VGPR awaits a load: retire the oldest
-            wait_seq(pend_loads.front().first);
+        while (r < 0 && (!pend_loads.empty() || !pend_lds.empty())) {  // every VGPR awaits a load
+            if (!pend_lds.empty()) wait_lseq(pend_lds.front().first);
+            else wait_seq(pend_loads.front().first);
             r = victim(0, (int)o.n_vgpr);
         }
         if (r < 0) { fail("colasm: no evictable VGPR"); return 0; }
@@ -159,8 +201,18 @@ struct Allocator {
     void kill(uint32_t v) {  // value dead: free register and scratch slot
         if (reg[v] >= 0) { release(reg[v]); reg[v] = -1; }
         if (slot[v] >= 0) { free_slots.push_back(slot[v]); slot[v] = -1; }
+        if (lslot[v] >= 0) { free_lslots.push_back(lslot[v]); lslot[v] = -1; }
     }
     void reload_into(uint32_t v, int r) {
+        if (lslot[v] >= 0) {
+            const uint64_t q = issue_lgkm();
+            emit(MI_LDLD, r, -1, -1, -1, (uint32_t)lslot[v]);
+            mp->st.ldld++;
+            linflight[r] = q;
+            pend_lds.push_back({q, r});
+            owner[r] = (int32_t)v; reg[v] = (int16_t)r;
+            return;
+        }
         const int32_t s = slot[v];
         wait_seq(slot_st[s]);
         const uint64_t q = issue_vmem();
@@ -184,13 +236,14 @@ struct Allocator {
     int to_vgpr(uint32_t v) {
         int r = reg[v];
         if (r < 0) {  // not prefetched: synchronous reload
-            if (slot[v] < 0) { fail("colasm: value lost"); return 0; }
+            if (slot[v] < 0 && lslot[v] < 0) { fail("colasm: value lost"); return 0; }
             const int t = take_vgpr();
             reload_into(v, t);
             mp->st.sync_reload++;
             r = t;
         }
         if (inflight[r]) wait_seq(inflight[r]);
+        if (linflight[r]) wait_lseq(linflight[r]);
         if (is_agpr(r)) {
             pinned[r] = 1;
             const int t = take_vgpr();
@@ -216,8 +269,10 @@ struct Allocator {
         uptr.assign(nv, 0);
         reg.assign(nv, -1);
         slot.assign(nv, -1);
+        lslot.assign(nv, -1);
+        for (int s = (int)o.n_lds - 1; s >= 0; --s) free_lslots.push_back(s);
         issued.assign(nv, 0);
-        for (int r = 0; r < 512; ++r) { owner[r] = -1; inflight[r] = 0; pinned[r] = 0; last_accw[r] = -100; }
+        for (int r = 0; r < 512; ++r) { owner[r] = -1; inflight[r] = 0; linflight[r] = 0; pinned[r] = 0; last_accw[r] = -100; }
         for (int r = (int)o.n_vgpr - 1; r >= 0; --r) freeV.push_back(r);
         for (int r = REG_A0 + (int)o.n_agpr - 1; r >= REG_A0; --r) freeA.push_back(r);
         std::vector<uint32_t> loads;
@@ -230,6 +285,7 @@ struct Allocator {
         mp->K = ir.p.K;
 
         for (uint32_t i = 0; i < nv && !failed; ++i) {
+            cur = i;
             // -- prefetch source rows
             while (lp < loads.size() && loads[lp] <= i + o.la_load) {
                 const uint32_t v = loads[lp];
@@ -245,7 +301,7 @@ struct Allocator {
             while (!reload_q.empty() && reload_q.top().first <= i + o.la_reload) {
                 const HE e = reload_q.top();
                 const uint32_t v = e.second;
-                if (reg[v] >= 0 || slot[v] < 0 || nu(v) != e.first) { reload_q.pop(); continue; }
+                if (reg[v] >= 0 || (slot[v] < 0 && lslot[v] < 0) || nu(v) != e.first) { reload_q.pop(); continue; }
                 if (seq - retired >= o.max_vmem && e.first > i + 8) break;
                 const int r = take_any(e.first);
                 if (r < 0) break;
@@ -265,12 +321,13 @@ struct Allocator {
                     const uint32_t v = n.a;
                     int r = reg[v];
                     if (r < 0) {
-                        if (slot[v] < 0) { fail("colasm: store of a lost value"); break; }
+                        if (slot[v] < 0 && lslot[v] < 0) { fail("colasm: store of a lost value"); break; }
                         r = take_vgpr();
                         reload_into(v, r);
                         mp->st.sync_reload++;
                     }
                     if (inflight[r]) wait_seq(inflight[r]);
+                    if (linflight[r]) wait_lseq(linflight[r]);
                     const uint64_t q = issue_vmem();
                     (void)q;
                     emit(MI_STOUT, -1, r, -1, -1, n.imm);
@@ -316,7 +373,11 @@ struct Allocator {
                         const uint32_t v = ops[q];
                         pinned[rr[q]] = 0;
                         if (nu(v) == INF && reg[v] >= 0) {
-                            if (reg[v] == dst) { reg[v] = -1; owner[dst] = -1; if (slot[v] >= 0) { free_slots.push_back(slot[v]); slot[v] = -1; } }
+                            if (reg[v] == dst) {
+                                reg[v] = -1; owner[dst] = -1;
+                                if (slot[v] >= 0) { free_slots.push_back(slot[v]); slot[v] = -1; }
+                                if (lslot[v] >= 0) { free_lslots.push_back(lslot[v]); lslot[v] = -1; }
+                            }
                             else kill(v);
                         }
                     }
@@ -335,6 +396,12 @@ struct Allocator {
 
 bool allocate_colprog(const ColIR& ir, const AllocOpts& o, MProg* mp, std::string* err) {
     *mp = MProg();
+    if (o.n_vgpr < 8 || o.n_vgpr > V_ALLOC || o.n_agpr > 256) {
+        if (err) *err = "colasm: register budget out of range";
+        return false;
+    }
+    mp->n_vgpr = o.n_vgpr;
+    mp->n_agpr = o.n_agpr;
     Allocator a(ir, o, mp, err);
     return a.run();
 }
@@ -357,6 +424,10 @@ bool divmagic(uint32_t d, uint32_t limit, uint32_t* magic, uint32_t* shift) {
 
 // ------------------------------------------------------------------------------------------
 std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
+    const Reserved rv(mp.n_vgpr);
+    const int V_T1 = rv.t1, V_T2 = rv.t2, V_SCROFF = rv.scroff, V_OUTOFF = rv.outoff, V_SRCOFF = rv.srcoff;
+    const uint32_t acc_off = (mp.n_vgpr + 5 + 3) & ~3u;                 // first AGPR in the unified file
+    const uint32_t n_regs = (acc_off + std::max<uint32_t>(mp.n_agpr, 1) + 7) & ~7u;
     std::string s;
     s.reserve(mp.ins.size() * 48 + 8192);
     char buf[256];
@@ -385,10 +456,10 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
         "v_sub_u32_e32 v3, v1, v3",
         "v_lshlrev_b32_e32 v3, 2, v3",
         "v_mul_lo_u32 v4, v2, s10",
-        "v_add_u32_e32 v255, v4, v3",
+        "v_add_u32_e32 V_SRCOFF, v4, v3",
         "v_mul_lo_u32 v4, v2, s11",
-        "v_add_u32_e32 v254, v4, v3",
-        "v_lshlrev_b32_e32 v253, 2, v0",
+        "v_add_u32_e32 V_OUTOFF, v4, v3",
+        "v_lshlrev_b32_e32 V_SCROFF, 2, v0",
         "s_mov_b32 s24, s4",
         "s_and_b32 s25, s5, 0xffff",
         "s_mov_b32 s26, -1",
@@ -408,7 +479,15 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
         "s_mov_b32 s37, 0xfefefefe",
         "s_mov_b32 s38, 0x1d1d1d1d",
     };
-    for (const char* p : pro) line(p);
+    for (const char* p : pro) {
+        std::string l(p);
+        const std::pair<const char*, int> names[] = {{"V_SRCOFF", V_SRCOFF}, {"V_OUTOFF", V_OUTOFF}, {"V_SCROFF", V_SCROFF}};
+        for (const auto& nm : names) {
+            const size_t at = l.find(nm.first);
+            if (at != std::string::npos) l.replace(at, std::strlen(nm.first), "v" + std::to_string(nm.second));
+        }
+        line(l.c_str());
+    }
     int sr = 0;
     auto srot = [&]() { sr = (sr + 1) & 7; return 40 + sr; };
     for (const MInst& m : mp.ins) {
@@ -462,23 +541,32 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
                 std::snprintf(buf, sizeof buf, "s_waitcnt vmcnt(%u)", m.imm); line(buf); break;
             case MI_NOP:
                 std::snprintf(buf, sizeof buf, "s_nop %u", m.imm); line(buf); break;
+            case MI_LDST:
+                std::snprintf(buf, sizeof buf, "ds_write_b32 v%d, %s offset:%u", V_SCROFF, R(m.a), m.imm * 256u); line(buf); break;
+            case MI_LDLD:
+                std::snprintf(buf, sizeof buf, "ds_read_b32 %s, v%d offset:%u", R(m.d), V_SCROFF, m.imm * 256u); line(buf); break;
+            case MI_WAITL:
+                std::snprintf(buf, sizeof buf, "s_waitcnt lgkmcnt(%u)", m.imm); line(buf); break;
         }
     }
     s += ".Lend:\n\ts_endpgm\n";
     s += ".Lfunc_end:\n\t.size " + kname + ", .Lfunc_end-" + kname + "\n";
     s += "\t.p2alignl 6, 3212836864\n\t.fill 256, 4, 3212836864\n";
     s += "\t.section .rodata,\"a\",@progbits\n\t.p2align 6, 0x0\n\t.amdhsa_kernel " + kname + "\n";
-    s += "\t\t.amdhsa_group_segment_fixed_size 0\n\t\t.amdhsa_private_segment_fixed_size 0\n";
+    const std::string lds = std::to_string(mp.n_lds_slots * 256u);
+    s += "\t\t.amdhsa_group_segment_fixed_size " + lds + "\n\t\t.amdhsa_private_segment_fixed_size 0\n";
     s += "\t\t.amdhsa_kernarg_size 64\n\t\t.amdhsa_user_sgpr_count 2\n";
     s += "\t\t.amdhsa_user_sgpr_kernarg_segment_ptr 1\n\t\t.amdhsa_system_sgpr_workgroup_id_x 1\n";
-    s += "\t\t.amdhsa_system_vgpr_workitem_id 0\n\t\t.amdhsa_next_free_vgpr 512\n";
-    s += "\t\t.amdhsa_next_free_sgpr 56\n\t\t.amdhsa_accum_offset 256\n\t\t.amdhsa_reserve_vcc 0\n";
+    s += "\t\t.amdhsa_system_vgpr_workitem_id 0\n\t\t.amdhsa_next_free_vgpr " + std::to_string(n_regs) + "\n";
+    s += "\t\t.amdhsa_next_free_sgpr 56\n\t\t.amdhsa_accum_offset " + std::to_string(acc_off) +
+         "\n\t\t.amdhsa_reserve_vcc 0\n";
     s += "\t\t.amdhsa_ieee_mode 0\n\t\t.amdhsa_dx10_clamp 0\n\t.end_amdhsa_kernel\n\t.text\n";
-    s += "\t.amdgpu_metadata\n---\namdhsa.kernels:\n  - .agpr_count: 256\n    .args:\n";
+    s += "\t.amdgpu_metadata\n---\namdhsa.kernels:\n  - .agpr_count: " + std::to_string(n_regs - acc_off) + "\n    .args:\n";
     s += "      - .offset: 0\n        .size: 64\n        .value_kind: by_value\n";
-    s += "    .group_segment_fixed_size: 0\n    .kernarg_segment_align: 8\n    .kernarg_segment_size: 64\n";
+    s += "    .group_segment_fixed_size: " + lds + "\n    .kernarg_segment_align: 8\n    .kernarg_segment_size: 64\n";
     s += "    .max_flat_workgroup_size: 64\n    .name: " + kname + "\n    .private_segment_fixed_size: 0\n";
-    s += "    .sgpr_count: 56\n    .symbol: " + kname + ".kd\n    .vgpr_count: 512\n    .wavefront_size: 64\n";
+    s += "    .sgpr_count: 56\n    .symbol: " + kname + ".kd\n    .vgpr_count: " + std::to_string(n_regs) +
+         "\n    .wavefront_size: 64\n";
     s += "amdhsa.target: amdgcn-amd-amdhsa--gfx950\namdhsa.version:\n  - 1\n  - 2\n...\n\t.end_amdgpu_metadata\n";
     return s;
 }
@@ -495,8 +583,9 @@ bool emulate_colprog(const MProg& mp, const uint8_t* src, uint32_t T, uint8_t* o
     const uint32_t Td = T / 4;
     std::vector<std::vector<uint32_t>> R(512, std::vector<uint32_t>(Td, 0));
     std::vector<std::vector<uint32_t>> scr(mp.n_slots, std::vector<uint32_t>(Td, 0));
-    std::vector<uint64_t> pend(512, 0), slot_st(mp.n_slots, 0);
-    uint64_t seq = 0, retired = 0;
+    std::vector<uint64_t> pend(512, 0), slot_st(mp.n_slots, 0), lpend(512, 0);
+    std::vector<std::vector<uint32_t>> lds(std::max<uint32_t>(mp.n_lds_slots, 1), std::vector<uint32_t>(Td, 0));
+    uint64_t seq = 0, retired = 0, lseq = 0, lretired = 0;
     char buf[160];
     auto bad = [&](size_t i, const char* what) {
         std::snprintf(buf, sizeof buf, "emulate: instruction %zu: %s", i, what);
@@ -505,7 +594,9 @@ bool emulate_colprog(const MProg& mp, const uint8_t* src, uint32_t T, uint8_t* o
     };
     for (size_t i = 0; i < mp.ins.size(); ++i) {
         const MInst& m = mp.ins[i];
-        auto ready = [&](int r) { return r < 0 || pend[r] == 0 || pend[r] <= retired; };
+        auto ready = [&](int r) {
+            return r < 0 || ((pend[r] == 0 || pend[r] <= retired) && (lpend[r] == 0 || lpend[r] <= lretired));
+        };
         if (!ready(m.a) || !ready(m.b) || !ready(m.c)) return bad(i, "operand read before its load completed");
         if (m.d >= 0 && !ready(m.d)) return bad(i, "register overwritten while a load into it is pending");
         auto vmem = [&]() {
@@ -565,12 +656,27 @@ bool emulate_colprog(const MProg& mp, const uint8_t* src, uint32_t T, uint8_t* o
                 break;
             case MI_NOP:
                 break;
+            case MI_LDST:
+                if (m.imm >= mp.n_lds_slots) return bad(i, "LDS slot out of range");
+                lds[m.imm] = R[m.a];
+                if (++lseq - lretired > 15) return bad(i, "more than 15 LDS operations outstanding");
+                break;
+            case MI_LDLD:
+                if (m.imm >= mp.n_lds_slots) return bad(i, "LDS slot out of range");
+                R[m.d] = lds[m.imm];
+                if (++lseq - lretired > 15) return bad(i, "more than 15 LDS operations outstanding");
+                lpend[m.d] = lseq;
+                break;
+            case MI_WAITL:
+                if (lseq > m.imm) lretired = std::max(lretired, lseq - m.imm);
+                break;
         }
         if ((m.op == MI_XOR2 || m.op == MI_XOR3 || m.op == MI_XT || m.op == MI_XTX || m.op == MI_ZERO) &&
             (m.d >= REG_A0 || m.a >= REG_A0 || m.b >= REG_A0 || m.c >= REG_A0))
             return bad(i, "VALU operand in an AGPR");
-        if ((m.op <= MI_ZERO) && (m.d >= V_ALLOC || (m.a >= V_ALLOC && m.a < REG_A0) || (m.b >= V_ALLOC && m.b < REG_A0) ||
-                                  (m.c >= V_ALLOC && m.c < REG_A0)))
+        const int nva = (int)mp.n_vgpr;
+        if ((m.op <= MI_ZERO) && (m.d >= nva || (m.a >= nva && m.a < REG_A0) || (m.b >= nva && m.b < REG_A0) ||
+                                  (m.c >= nva && m.c < REG_A0)))
             return bad(i, "VALU operand in a reserved VGPR");
     }
     return true;

@@ -2,8 +2,9 @@
 // column program (rq_colprog.hpp).
 //
 // Storage tiers of a value (one dword per lane): arch VGPR (operand of a VALU op), AGPR (one
-// v_accvgpr_read/write away; also a direct target/source of buffer loads/stores), and a per-wave
-// global scratch slot (256 B per value, L2/MALL-resident in practice).  Allocation is Belady's
+// v_accvgpr_read/write away; also a direct target/source of buffer loads/stores), a per-wave LDS
+// slot (256 B; ds_write/ds_read, off the vector-memory path), and a per-wave global scratch slot
+// (256 B per value, L2/MALL-resident in practice).  Allocation is Belady's
 // furthest-next-use rule over the straight-line program; source-row loads and scratch reloads
 // are issued ahead of their use (look-ahead windows) and waited for with exact vmcnt counts.
 #pragma once
@@ -25,11 +26,18 @@ enum MOp : uint8_t {
     MI_ACCR,    // VGPR d <- AGPR a
     MI_WAIT,    // s_waitcnt vmcnt(imm)
     MI_NOP,     // s_nop imm
+    MI_LDST,    // LDS slot imm <- a (ds_write_b32)
+    MI_LDLD,    // d <- LDS slot imm (ds_read_b32)
+    MI_WAITL,   // s_waitcnt lgkmcnt(imm)
 };
 
 constexpr int REG_A0 = 256;       // register ids: 0..255 VGPR, 256..511 AGPR
-constexpr int V_SRCOFF = 255, V_OUTOFF = 254, V_SCROFF = 253, V_T1 = 252, V_T2 = 251;
-constexpr int V_ALLOC = 251;      // v0..v250 are allocatable
+constexpr int V_ALLOC = 251;      // at most v0..v250 allocatable; 5 reserved VGPRs sit just above
+// Reserved VGPRs of a program with n allocatable VGPRs: v(n)..v(n+4).
+struct Reserved {
+    int t2, t1, scroff, outoff, srcoff;
+    explicit Reserved(uint32_t n) : t2((int)n), t1((int)n + 1), scroff((int)n + 2), outoff((int)n + 3), srcoff((int)n + 4) {}
+};
 
 struct MInst {
     uint8_t op = MI_NOP;
@@ -43,16 +51,22 @@ struct AllocOpts {
     uint32_t la_load = 320;      // look-ahead (IR nodes) for source-row loads
     uint32_t la_reload = 160;    // look-ahead (IR nodes) for scratch reloads
     uint32_t max_vmem = 56;      // outstanding vector-memory operations per wave
+    uint32_t n_lds = 156;        // LDS spill slots per wave (256 B each; 1 wave/SIMD -> 40 KB)
+    uint32_t lds_horizon = 2000; // spill to LDS only values needed again within this many IR nodes
 };
 
 struct MProg {
     std::vector<MInst> ins;
     uint32_t n_slots = 0;        // scratch slots per wave (256 B each)
+    uint32_t n_lds_slots = 0;    // LDS slots per wave used (256 B each)
+    uint32_t n_vgpr = V_ALLOC;   // allocatable VGPRs / AGPRs the program was allocated for
+    uint32_t n_agpr = 256;
     uint32_t n_out = 0;
     uint32_t K = 0;
     struct Stats {
         uint32_t valu = 0, ldsrc = 0, stout = 0, spst = 0, spld = 0, accw = 0, accr = 0, wait = 0, nop = 0;
         uint32_t sync_reload = 0;  // reloads that were not prefetched
+        uint32_t ldst = 0, ldld = 0, waitl = 0;  // LDS spill stores / reloads / lgkm waits
     } st;
 };
 

@@ -153,13 +153,16 @@ int ensure_tables(DevCtx* ctx) {
     return RQ_OK;
 }
 
-// Allocation options; RQHIP_ALLOC="v,a,la_load,la_reload,max_vmem" overrides them for experiments.
+// Allocation options; RQHIP_ALLOC="v,a,la_load,la_reload,max_vmem,lds+1" overrides them for
+// experiments (0 = keep the default; the sixth field is the LDS slot count plus one).
 const AllocOpts& alloc_options() {
     static const AllocOpts o = [] {
         AllocOpts r;
         if (const char* e = std::getenv("RQHIP_ALLOC")) {
-            unsigned v[5] = {0, 0, 0, 0, 0};
-            std::sscanf(e, "%u,%u,%u,%u,%u", &v[0], &v[1], &v[2], &v[3], &v[4]);
+            unsigned v[6] = {0, 0, 0, 0, 0, 0};
+            std::sscanf(e, "%u,%u,%u,%u,%u,%u", &v[0], &v[1], &v[2], &v[3], &v[4], &v[5]);
+            if (v[5]) r.n_lds = std::min<uint32_t>(v[5] - 1, 156);
+            if (const char* h = std::getenv("RQHIP_LDS_HORIZON")) r.lds_horizon = (uint32_t)std::atoi(h);
             if (v[0]) r.n_vgpr = std::min<uint32_t>(v[0], V_ALLOC);
             if (v[1]) r.n_agpr = std::min<uint32_t>(v[1], 256);
             if (v[2]) r.la_load = v[2];
@@ -522,7 +525,7 @@ int rq_debug_colprog_eval(uint32_t K, uint32_t T, const uint32_t* esi, uint32_t 
 }
 
 int rq_debug_colprog_emulate(uint32_t K, uint32_t T, const uint32_t* esi, uint32_t n_out, const uint8_t* src,
-                             uint8_t* out, const uint32_t opts[5], uint32_t stats[16], char* asm_buf, size_t asm_cap,
+                             uint8_t* out, const uint32_t opts[6], uint32_t stats[18], char* asm_buf, size_t asm_cap,
                              size_t* asm_len) {
     Params p;
     int rc = params_for_K(K, &p);
@@ -539,15 +542,16 @@ int rq_debug_colprog_emulate(uint32_t K, uint32_t T, const uint32_t* esi, uint32
         if (opts[2]) o.la_load = opts[2];
         if (opts[3]) o.la_reload = opts[3];
         if (opts[4]) o.max_vmem = std::min<uint32_t>(opts[4], 60);
+        if (opts[5]) o.n_lds = std::min<uint32_t>(opts[5] - 1, 156);
     }
     MProg mp;
     if (!allocate_colprog(ir, o, &mp, &err)) return fail(RQ_ERR_PLAN, err);
     if (src && out && !emulate_colprog(mp, src, T, out, &err)) return fail(RQ_ERR_PLAN, err);
     if (stats) {
         const auto& s = mp.st;
-        const uint32_t v[16] = {(uint32_t)mp.ins.size(), s.valu, s.ldsrc, s.stout, s.spst, s.spld, s.accw, s.accr,
+        const uint32_t v[18] = {(uint32_t)mp.ins.size(), s.valu, s.ldsrc, s.stout, s.spst, s.spld, s.accw, s.accr,
                                 s.wait, s.nop, s.sync_reload, mp.n_slots, (uint32_t)ir.nodes.size(), ir.st.xt + ir.st.xtx,
-                                0, 0};
+                                s.ldst, s.ldld, s.waitl, mp.n_lds_slots};
         std::memcpy(stats, v, sizeof v);
     }
     if (asm_len) {

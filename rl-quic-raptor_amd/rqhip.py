@@ -139,19 +139,20 @@ def params(size, T):
 
 
 COLPROG_STAT_NAMES = ("instructions", "valu", "src_loads", "out_stores", "spill_stores", "spill_loads", "accw",
-                      "accr", "waits", "nops", "sync_reloads", "scratch_slots", "ir_nodes", "xtimes")
+                      "accr", "waits", "nops", "sync_reloads", "scratch_slots", "ir_nodes", "xtimes", "lds_stores",
+                      "lds_loads", "lgkm_waits", "lds_slots")
 
 
 def colprog_stats(K, esis=None, opts=None):
     """Host-only statistics of the column program for (K, output ESIs) (None: all L symbols)."""
     import numpy as np
-    st = np.zeros(16, np.uint32)
+    st = np.zeros(18, np.uint32)
     P32 = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
     e = np.asarray(esis if esis is not None else [0], np.uint32)
-    o = np.asarray(opts if opts is not None else [0] * 5, np.uint32)
+    o = np.asarray(opts if opts is not None else [0] * 6, np.uint32)
     _check(lib().rq_debug_colprog_emulate(K, 4, P32(e) if esis is not None else None, len(e), None, None, P32(o),
                                           P32(st), None, 0, None))
-    return dict(zip(COLPROG_STAT_NAMES, (int(x) for x in st[:14])))
+    return dict(zip(COLPROG_STAT_NAMES, (int(x) for x in st[:18])))
 
 
 def colprog_emulate(K, T, esis, src, opts=None):
@@ -160,12 +161,12 @@ def colprog_emulate(K, T, esis, src, opts=None):
     src = np.ascontiguousarray(src, np.uint8)
     e = np.asarray(esis, np.uint32)
     out = np.zeros((len(e), T), np.uint8)
-    o = np.asarray(opts if opts is not None else [0] * 5, np.uint32)
-    st = np.zeros(16, np.uint32)
+    o = np.asarray(opts if opts is not None else [0] * 6, np.uint32)
+    st = np.zeros(18, np.uint32)
     P32 = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
     _check(lib().rq_debug_colprog_emulate(K, T, P32(e), len(e), src.ctypes.data, out.ctypes.data, P32(o), P32(st),
                                           None, 0, None))
-    return out, dict(zip(COLPROG_STAT_NAMES, (int(x) for x in st[:14])))
+    return out, dict(zip(COLPROG_STAT_NAMES, (int(x) for x in st[:18])))
 
 
 def colprog_eval(K, T, esis, src):

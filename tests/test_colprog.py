@@ -46,10 +46,13 @@ def test_machine_program_matches_oracle(rq, oracle, K, T, nrep):
     assert st["sync_reloads"] <= st["spill_loads"]
 
 
-@pytest.mark.parametrize("opts", [[64, 32, 40, 20, 8], [32, 4, 400, 400, 60], [200, 8, 16, 8, 4]])
+# opts = {n_vgpr, n_agpr, la_load, la_reload, max_vmem, n_lds + 1}
+@pytest.mark.parametrize("opts", [[64, 32, 40, 20, 8, 1], [32, 4, 400, 400, 60, 1], [200, 8, 16, 8, 4, 1],
+                                  [32, 4, 400, 400, 60, 9], [24, 1, 40, 20, 8, 17], [16, 2, 100, 50, 12, 3]])
 def test_machine_program_under_register_pressure(rq, oracle, opts):
-    """Tight register files, short/long look-aheads and a small vmcnt budget force every spill /
-    reload / wait path of the allocator; the bytes must not change."""
+    """Tight register files, short/long look-aheads, a small vmcnt budget and a small LDS tier force
+    every spill / reload / wait path of the allocator (global scratch, LDS slots, lgkmcnt); the bytes
+    must not change."""
     K, T = 257, 12
     rng = np.random.default_rng(sum(opts))
     data = rng.integers(0, 256, K * T, dtype=np.uint8)
@@ -59,6 +62,22 @@ def test_machine_program_under_register_pressure(rq, oracle, opts):
     for i, e in enumerate(esis):
         assert np.array_equal(out[i], enc.gen_symbol(e)), e
     assert st["spill_stores"] > 0
+    if opts[5] > 1:
+        assert 0 < st["lds_slots"] <= opts[5] - 1 and st["lds_loads"] > 0
+
+
+@pytest.mark.parametrize("opts", [[123, 128, 0, 0, 0, 81], [246, 1, 0, 0, 0, 81], [79, 84, 0, 0, 0, 54]])
+def test_two_and_three_wave_budgets(rq, oracle, opts):
+    """Register budgets of 256 / 168 per lane (2 / 3 waves per SIMD) at K=1024: emulated bytes equal the
+    oracle's and the program assembles."""
+    K, T = 1024, 8
+    rng = np.random.default_rng(7)
+    data = rng.integers(0, 256, K * T, dtype=np.uint8)
+    esis = list(range(K, K + 20))
+    out, st = rq.colprog_emulate(K, T, esis, data, opts)
+    enc = oracle.OracleEncoder(data.tobytes(), T)
+    for i, e in enumerate(esis):
+        assert np.array_equal(out[i], enc.gen_symbol(e)), e
 
 
 @pytest.mark.parametrize("K,T", [(64, 48), (1024, 8)])
