@@ -426,7 +426,7 @@ bool divmagic(uint32_t d, uint32_t limit, uint32_t* magic, uint32_t* shift) {
 std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
     const Reserved rv(mp.n_vgpr);
     const int V_T1 = rv.t1, V_T2 = rv.t2, V_SCROFF = rv.scroff, V_OUTOFF = rv.outoff, V_SRCOFF = rv.srcoff;
-    const uint32_t acc_off = (mp.n_vgpr + 5 + 3) & ~3u;                 // first AGPR in the unified file
+    const uint32_t acc_off = (mp.n_vgpr + N_RESERVED + 3) & ~3u;        // first AGPR in the unified file
     const uint32_t n_regs = (acc_off + std::max<uint32_t>(mp.n_agpr, 1) + 7) & ~7u;
     std::string s;
     s.reserve(mp.ins.size() * 48 + 8192);
@@ -460,6 +460,7 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
         "v_mul_lo_u32 v4, v2, s11",
         "v_add_u32_e32 V_OUTOFF, v4, v3",
         "v_lshlrev_b32_e32 V_SCROFF, 2, v0",
+        "v_add_u32_e32 V_LDS2, 0x10000, V_SCROFF",
         "s_mov_b32 s24, s4",
         "s_and_b32 s25, s5, 0xffff",
         "s_mov_b32 s26, -1",
@@ -481,11 +482,11 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
     };
     for (const char* p : pro) {
         std::string l(p);
-        const std::pair<const char*, int> names[] = {{"V_SRCOFF", V_SRCOFF}, {"V_OUTOFF", V_OUTOFF}, {"V_SCROFF", V_SCROFF}};
-        for (const auto& nm : names) {
-            const size_t at = l.find(nm.first);
-            if (at != std::string::npos) l.replace(at, std::strlen(nm.first), "v" + std::to_string(nm.second));
-        }
+        const std::pair<const char*, int> names[] = {
+            {"V_SRCOFF", V_SRCOFF}, {"V_OUTOFF", V_OUTOFF}, {"V_SCROFF", V_SCROFF}, {"V_LDS2", rv.lds2}};
+        for (const auto& nm : names)
+            for (size_t at = l.find(nm.first); at != std::string::npos; at = l.find(nm.first))
+                l.replace(at, std::strlen(nm.first), "v" + std::to_string(nm.second));
         line(l.c_str());
     }
     int sr = 0;
@@ -542,9 +543,15 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
             case MI_NOP:
                 std::snprintf(buf, sizeof buf, "s_nop %u", m.imm); line(buf); break;
             case MI_LDST:
-                std::snprintf(buf, sizeof buf, "ds_write_b32 v%d, %s offset:%u", V_SCROFF, R(m.a), m.imm * 256u); line(buf); break;
+                std::snprintf(buf, sizeof buf, "ds_write_b32 v%d, %s offset:%u", m.imm < 256 ? V_SCROFF : rv.lds2, R(m.a),
+                              (m.imm & 255u) * 256u);
+                line(buf);
+                break;
             case MI_LDLD:
-                std::snprintf(buf, sizeof buf, "ds_read_b32 %s, v%d offset:%u", R(m.d), V_SCROFF, m.imm * 256u); line(buf); break;
+                std::snprintf(buf, sizeof buf, "ds_read_b32 %s, v%d offset:%u", R(m.d), m.imm < 256 ? V_SCROFF : rv.lds2,
+                              (m.imm & 255u) * 256u);
+                line(buf);
+                break;
             case MI_WAITL:
                 std::snprintf(buf, sizeof buf, "s_waitcnt lgkmcnt(%u)", m.imm); line(buf); break;
         }

@@ -32,11 +32,14 @@ enum MOp : uint8_t {
 };
 
 constexpr int REG_A0 = 256;       // register ids: 0..255 VGPR, 256..511 AGPR
-constexpr int V_ALLOC = 251;      // at most v0..v250 allocatable; 5 reserved VGPRs sit just above
-// Reserved VGPRs of a program with n allocatable VGPRs: v(n)..v(n+4).
+constexpr int V_ALLOC = 250;      // at most v0..v249 allocatable; 6 reserved VGPRs sit just above
+// Reserved VGPRs of a program with n allocatable VGPRs: v(n)..v(n+5).  lds2 = scroff + 64 KiB
+// addresses LDS slots 256.. (the ds offset field is 16 bits).
+constexpr int N_RESERVED = 6;
 struct Reserved {
-    int t2, t1, scroff, outoff, srcoff;
-    explicit Reserved(uint32_t n) : t2((int)n), t1((int)n + 1), scroff((int)n + 2), outoff((int)n + 3), srcoff((int)n + 4) {}
+    int t2, t1, scroff, outoff, srcoff, lds2;
+    explicit Reserved(uint32_t n)
+        : t2((int)n), t1((int)n + 1), scroff((int)n + 2), outoff((int)n + 3), srcoff((int)n + 4), lds2((int)n + 5) {}
 };
 
 struct MInst {
@@ -51,7 +54,7 @@ struct AllocOpts {
     uint32_t la_load = 320;      // look-ahead (IR nodes) for source-row loads
     uint32_t la_reload = 160;    // look-ahead (IR nodes) for scratch reloads
     uint32_t max_vmem = 56;      // outstanding vector-memory operations per wave
-    uint32_t n_lds = 156;        // LDS spill slots per wave (256 B each; 1 wave/SIMD -> 40 KB)
+    uint32_t n_lds = 156;        // LDS spill slots per wave (256 B each; 4 waves/CU -> 40 KB; <= 640)
     uint32_t lds_horizon = 2000; // spill to LDS only values needed again within this many IR nodes
 };
 

@@ -161,7 +161,7 @@ const AllocOpts& alloc_options() {
         if (const char* e = std::getenv("RQHIP_ALLOC")) {
             unsigned v[6] = {0, 0, 0, 0, 0, 0};
             std::sscanf(e, "%u,%u,%u,%u,%u,%u", &v[0], &v[1], &v[2], &v[3], &v[4], &v[5]);
-            if (v[5]) r.n_lds = std::min<uint32_t>(v[5] - 1, 156);
+            if (v[5]) r.n_lds = std::min<uint32_t>(v[5] - 1, 640);
             if (const char* h = std::getenv("RQHIP_LDS_HORIZON")) r.lds_horizon = (uint32_t)std::atoi(h);
             if (v[0]) r.n_vgpr = std::min<uint32_t>(v[0], V_ALLOC);
             if (v[1]) r.n_agpr = std::min<uint32_t>(v[1], 256);
@@ -542,7 +542,7 @@ int rq_debug_colprog_emulate(uint32_t K, uint32_t T, const uint32_t* esi, uint32
         if (opts[2]) o.la_load = opts[2];
         if (opts[3]) o.la_reload = opts[3];
         if (opts[4]) o.max_vmem = std::min<uint32_t>(opts[4], 60);
-        if (opts[5]) o.n_lds = std::min<uint32_t>(opts[5] - 1, 156);
+        if (opts[5]) o.n_lds = std::min<uint32_t>(opts[5] - 1, 640);
     }
     MProg mp;
     if (!allocate_colprog(ir, o, &mp, &err)) return fail(RQ_ERR_PLAN, err);

@@ -121,6 +121,7 @@ __global__ void __launch_bounds__(64) k_solve64(SolveArgs a) {
     __shared__ __attribute__((aligned(16))) uint4 mult[8][8];  // alpha^b * scaled pivot row, 8 quads
     __shared__ uint8_t ex[512], lg[256];
     __shared__ uint8_t pivl[64];
+    __shared__ uint32_t Es[64];
     const uint32_t b = a.blk_map[blockIdx.x];
     const uint32_t lane = threadIdx.x;
     const uint32_t e = a.erased_off[b + 1] - a.erased_off[b];
@@ -132,15 +133,25 @@ __global__ void __launch_bounds__(64) k_solve64(SolveArgs a) {
     const uint32_t nrow = min(nr, 64u);
     const uint32_t* E = a.erased + a.erased_off[b];
     const uint32_t* U = a.rep_uidx + a.rep_off[b];
+    if (lane < e) Es[lane] = E[lane];
     gf_tables(ex, lg);
     uint32_t* my = rows + lane * S64_W;
     uint4* my4 = reinterpret_cast<uint4*>(my);
 #pragma unroll
     for (int q = 0; q < 8; ++q) my4[q] = make_uint4(0, 0, 0, 0);
-    if (lane < nrow) {
+    __syncthreads();
+    if (lane < nrow) {  // row gather: eight independent L2 loads in flight per step
         uint8_t* myb = reinterpret_cast<uint8_t*>(my);
         const uint8_t* mr = a.mrep + (size_t)U[lane] * a.mrep_stride;
-        for (uint32_t k = 0; k < e; ++k) myb[k] = mr[E[k]];
+        uint32_t k = 0;
+        for (; k + 8 <= e; k += 8) {
+            uint8_t v[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = mr[Es[k + i]];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) myb[k + i] = v[i];
+        }
+        for (; k < e; ++k) myb[k] = mr[Es[k]];
         myb[e + lane] = 1;
     }
     __syncthreads();
@@ -305,14 +316,23 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a) {
     const uint32_t* recv = reinterpret_cast<const uint32_t*>(a.recv);
     const uint32_t* r0 = reinterpret_cast<const uint32_t*>(a.r0) + (size_t)b * a.n_union * Td;
     uint8_t* blk = a.data + (size_t)b * a.data_stride;
+    // dword offsets of the syndrome operands of every m (received row, r0 row), staged once
+    __shared__ uint32_t offr[256], off0[256];
+    for (uint32_t m = lane; m < e; m += 64) {
+        const uint32_t j = r0b + XP[m];
+        offr[m] = j * Td;
+        off0[m] = a.rep_uidx[j] * Td;
+    }
+    __syncthreads();
+    const uint32_t cc = live ? c : 0;
     for (uint32_t k0 = 0; k0 < e; k0 += KC) {
         uint32_t acc[KC];
 #pragma unroll
         for (int k = 0; k < KC; ++k) acc[k] = 0;
-        const uint32_t cc = live ? c : 0;
+        uint32_t s_next = recv[(size_t)offr[0] + cc] ^ r0[(size_t)off0[0] + cc];
         for (uint32_t m = 0; m < e; ++m) {
-            const uint32_t j = r0b + XP[m];
-            uint32_t s = recv[(size_t)j * Td + cc] ^ r0[(size_t)a.rep_uidx[j] * Td + cc];
+            uint32_t s = s_next;
+            if (m + 1 < e) s_next = recv[(size_t)offr[m + 1] + cc] ^ r0[(size_t)off0[m + 1] + cc];  // prefetch
             const uint32_t* cw = reinterpret_cast<const uint32_t*>(xc + (size_t)m * a.xc_stride + k0);
             uint32_t mul[8];
 #pragma unroll
