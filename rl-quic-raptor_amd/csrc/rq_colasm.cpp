@@ -6,6 +6,7 @@
 #include <cstring>
 #include <deque>
 #include <queue>
+#include <set>
 
 namespace rq {
 
@@ -33,6 +34,7 @@ struct Allocator {
     int last_accw[512];                             // instruction index of the last ACCW into an AGPR
     std::vector<int> freeV, freeA;
     std::vector<int32_t> free_slots, free_lslots;
+    std::set<std::pair<uint32_t, uint32_t>> lds_res;  // (next use, value) of values held in LDS
     std::vector<uint64_t> slot_st, slot_ld;         // last store / load seq per slot
     uint64_t seq = 0, retired = 0;
     std::deque<std::pair<uint64_t, int>> pend_loads;  // (seq, reg)
@@ -119,27 +121,50 @@ struct Allocator {
         wait_seq(slot_st[s]);  // WAW
         return s;
     }
-    // value in register r -> scratch copy (if none); r becomes free (not pushed to a free list)
+    void to_global(uint32_t v, int r) {  // store register r (holding v) into a new scratch slot
+        const int32_t s = new_slot();
+        const uint64_t q = issue_vmem();
+        emit(MI_SPST, -1, r, -1, -1, (uint32_t)s);
+        mp->st.spst++;
+        slot_st[s] = q;
+        slot[v] = s;
+    }
+    void lds_put(uint32_t v, int r, int32_t s) {
+        mp->n_lds_slots = std::max<uint32_t>(mp->n_lds_slots, (uint32_t)s + 1);
+        issue_lgkm();
+        emit(MI_LDST, -1, r, -1, -1, (uint32_t)s);
+        mp->st.ldst++;
+        lslot[v] = s;
+        lds_res.insert({nu(v), v});
+    }
+    // value in register r -> a copy in LDS or global scratch (if none); r becomes free (not pushed
+    // to a free list).  Registers + LDS act as one Belady cache in front of global scratch: a value
+    // enters LDS if a slot is free, or by pushing the LDS resident with the furthest next use out to
+    // global scratch when its own next use is nearer (through the reserved temp VGPR).
     void spill_out(int r) {
         const int32_t v = owner[r];
-        if (slot[v] < 0 && lslot[v] < 0 && !free_lslots.empty() &&  // LDS tier for nearer reuse
-            nu((uint32_t)v) < cur + o.lds_horizon) {
-            const int32_t s = free_lslots.back();
-            free_lslots.pop_back();
-            mp->n_lds_slots = std::max<uint32_t>(mp->n_lds_slots, (uint32_t)s + 1);
-            issue_lgkm();
-            emit(MI_LDST, -1, r, -1, -1, (uint32_t)s);
-            mp->st.ldst++;
-            lslot[v] = s;
+        if (slot[v] < 0 && lslot[v] < 0 && o.n_lds) {
+            const uint32_t n = nu((uint32_t)v);
+            if (!free_lslots.empty()) {
+                const int32_t s = free_lslots.back();
+                free_lslots.pop_back();
+                lds_put((uint32_t)v, r, s);
+            } else if (!lds_res.empty() && std::prev(lds_res.end())->first > n + o.lds_horizon) {
+                const uint32_t w = std::prev(lds_res.end())->second;
+                const int32_t s = lslot[w];
+                const int t = Reserved(o.n_vgpr).t1;
+                lds_res.erase(std::prev(lds_res.end()));
+                const uint64_t q = issue_lgkm();
+                emit(MI_LDLD, t, -1, -1, -1, (uint32_t)s);
+                mp->st.ldld++;
+                wait_lseq(q);
+                lslot[w] = -1;
+                to_global(w, t);
+                mp->st.migrate++;
+                lds_put((uint32_t)v, r, s);
+            }
         }
-        if (slot[v] < 0 && lslot[v] < 0) {
-            const int32_t s = new_slot();
-            const uint64_t q = issue_vmem();
-            emit(MI_SPST, -1, r, -1, -1, (uint32_t)s);
-            mp->st.spst++;
-            slot_st[s] = q;
-            slot[v] = s;
-        }
+        if (slot[v] < 0 && lslot[v] < 0) to_global((uint32_t)v, r);
         reg[v] = -1;
         owner[r] = -1;
         reload_q.push({nu((uint32_t)v), (uint32_t)v});
@@ -201,15 +226,21 @@ struct Allocator {
     void kill(uint32_t v) {  // value dead: free register and scratch slot
         if (reg[v] >= 0) { release(reg[v]); reg[v] = -1; }
         if (slot[v] >= 0) { free_slots.push_back(slot[v]); slot[v] = -1; }
-        if (lslot[v] >= 0) { free_lslots.push_back(lslot[v]); lslot[v] = -1; }
+        if (lslot[v] >= 0) free_lds(v);
+    }
+    void free_lds(uint32_t v) {
+        lds_res.erase({nu(v), v});
+        free_lslots.push_back(lslot[v]);
+        lslot[v] = -1;
     }
     void reload_into(uint32_t v, int r) {
-        if (lslot[v] >= 0) {
+        if (lslot[v] >= 0) {  // the LDS slot is released at once: LDS operations run in order
             const uint64_t q = issue_lgkm();
             emit(MI_LDLD, r, -1, -1, -1, (uint32_t)lslot[v]);
             mp->st.ldld++;
             linflight[r] = q;
             pend_lds.push_back({q, r});
+            free_lds(v);
             owner[r] = (int32_t)v; reg[v] = (int16_t)r;
             return;
         }
@@ -376,7 +407,7 @@ struct Allocator {
                             if (reg[v] == dst) {
                                 reg[v] = -1; owner[dst] = -1;
                                 if (slot[v] >= 0) { free_slots.push_back(slot[v]); slot[v] = -1; }
-                                if (lslot[v] >= 0) { free_lslots.push_back(lslot[v]); lslot[v] = -1; }
+                                if (lslot[v] >= 0) free_lds(v);
                             }
                             else kill(v);
                         }
@@ -396,7 +427,7 @@ struct Allocator {
 
 bool allocate_colprog(const ColIR& ir, const AllocOpts& o, MProg* mp, std::string* err) {
     *mp = MProg();
-    if (o.n_vgpr < 8 || o.n_vgpr > V_ALLOC || o.n_agpr > 256) {
+    if (o.n_vgpr < 8 || o.n_vgpr > V_ALLOC || o.n_agpr > 256 || o.n_lds > 512) {  // 2 LDS bases
         if (err) *err = "colasm: register budget out of range";
         return false;
     }

@@ -54,8 +54,8 @@ struct AllocOpts {
     uint32_t la_load = 320;      // look-ahead (IR nodes) for source-row loads
     uint32_t la_reload = 160;    // look-ahead (IR nodes) for scratch reloads
     uint32_t max_vmem = 56;      // outstanding vector-memory operations per wave
-    uint32_t n_lds = 156;        // LDS spill slots per wave (256 B each; 4 waves/CU -> 40 KB; <= 640)
-    uint32_t lds_horizon = 2000; // spill to LDS only values needed again within this many IR nodes
+    uint32_t n_lds = 156;        // LDS spill slots per wave (256 B each; 4 waves/CU -> 40 KB; <= 512)
+    uint32_t lds_horizon = 0;    // push an LDS resident out only if its next use is this much further
 };
 
 struct MProg {
@@ -70,6 +70,7 @@ struct MProg {
         uint32_t valu = 0, ldsrc = 0, stout = 0, spst = 0, spld = 0, accw = 0, accr = 0, wait = 0, nop = 0;
         uint32_t sync_reload = 0;  // reloads that were not prefetched
         uint32_t ldst = 0, ldld = 0, waitl = 0;  // LDS spill stores / reloads / lgkm waits
+        uint32_t migrate = 0;                    // LDS residents pushed out to global scratch
     } st;
 };
 

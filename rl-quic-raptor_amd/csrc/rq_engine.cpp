@@ -93,13 +93,24 @@ struct HostBuf {
     ~HostBuf() { if (p) (void)hipHostFree(p); }
 };
 
+// Per-stream workspaces: kernels of calls on different streams may run concurrently, so every
+// stream gets its own scratch / index / syndrome buffers (calls on one stream are ordered).
+struct Workspace {
+    DevBuf idx, r0, xb, xp, scratch;
+    HostBuf h_idx, h_status;
+};
+
 struct DevCtx {
     int device = -1;
     std::mutex mu;
     bool tables = false;
     std::map<std::string, std::unique_ptr<ColKernel>> colk;  // keyed by (K', K, outputs)
-    DevBuf ws_idx, ws_r0, ws_xb, ws_xp, ws_scratch;
-    HostBuf h_idx, h_status;
+    std::map<void*, std::unique_ptr<Workspace>> ws;
+    Workspace* wsp(void* stream) {
+        auto& w = ws[stream];
+        if (!w) w.reset(new Workspace());
+        return w.get();
+    }
 };
 
 std::mutex g_ctx_mu;
@@ -161,7 +172,7 @@ const AllocOpts& alloc_options() {
         if (const char* e = std::getenv("RQHIP_ALLOC")) {
             unsigned v[6] = {0, 0, 0, 0, 0, 0};
             std::sscanf(e, "%u,%u,%u,%u,%u,%u", &v[0], &v[1], &v[2], &v[3], &v[4], &v[5]);
-            if (v[5]) r.n_lds = std::min<uint32_t>(v[5] - 1, 640);
+            if (v[5]) r.n_lds = std::min<uint32_t>(v[5] - 1, 512);
             if (const char* h = std::getenv("RQHIP_LDS_HORIZON")) r.lds_horizon = (uint32_t)std::atoi(h);
             if (v[0]) r.n_vgpr = std::min<uint32_t>(v[0], V_ALLOC);
             if (v[1]) r.n_agpr = std::min<uint32_t>(v[1], 256);
@@ -231,14 +242,15 @@ int launch_col(DevCtx* ctx, ColKernel* k, uint32_t T, uint32_t n_blocks, const v
     const uint32_t max_waves = (uint32_t)(((uint64_t)per * Td + 63) / 64);
     const size_t spw = (size_t)std::max<uint32_t>(k->n_slots, 1) * 256;
     int rc;
-    if ((rc = ctx->ws_scratch.ensure(spw * max_waves))) return rc;
+    Workspace* w = ctx->wsp(stream);
+    if ((rc = w->scratch.ensure(spw * max_waves))) return rc;
     for (uint32_t b0 = 0; b0 < n_blocks; b0 += per) {
         const uint32_t nb = std::min(per, n_blocks - b0);
         ColKernArgs a;
         std::memset(&a, 0, sizeof a);
         a.src = (uint64_t)(uintptr_t)src + (uint64_t)b0 * src_stride;
         a.out = (uint64_t)(uintptr_t)out + (uint64_t)b0 * out_stride;
-        a.scratch = (uint64_t)(uintptr_t)ctx->ws_scratch.p;
+        a.scratch = (uint64_t)(uintptr_t)w->scratch.p;
         a.src_stride = (uint32_t)src_stride;
         a.out_stride = (uint32_t)out_stride;
         a.T = T;
@@ -379,23 +391,24 @@ int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, v
         for (uint32_t i = eoff[b]; i < eoff[b + 1]; ++i) idx.push_back(erased[i]);
     // descriptor upload through pinned staging: the copy is queued behind the caller's work on the
     // stream (e.g. the encode that produced `repair`) without blocking this thread
-    if ((rc = ctx->ws_idx.ensure(idx.size() * 4)) || (rc = ctx->h_idx.ensure(idx.size() * 4)) ||
-        (rc = ctx->h_status.ensure((size_t)n_blocks * 4)))
+    Workspace* w = ctx->wsp(stream);
+    if ((rc = w->idx.ensure(idx.size() * 4)) || (rc = w->h_idx.ensure(idx.size() * 4)) ||
+        (rc = w->h_status.ensure((size_t)n_blocks * 4)))
         return rc;
-    std::memcpy(ctx->h_idx.p, idx.data(), idx.size() * 4);
-    HIP_TRY(hipMemcpyAsync(ctx->ws_idx.p, ctx->h_idx.p, idx.size() * 4, hipMemcpyHostToDevice, (hipStream_t)stream));
-    const uint32_t* di = ctx->ws_idx.as<uint32_t>();
+    std::memcpy(w->h_idx.p, idx.data(), idx.size() * 4);
+    HIP_TRY(hipMemcpyAsync(w->idx.p, w->h_idx.p, idx.size() * 4, hipMemcpyHostToDevice, (hipStream_t)stream));
+    const uint32_t* di = w->idx.as<uint32_t>();
     const uint32_t xc_stride = 64 * ((max_e + 63) / 64);
-    if ((rc = ctx->ws_r0.ensure((size_t)n_blocks * uni.size() * T))) return rc;
-    if ((rc = ctx->ws_xb.ensure((size_t)nw * max_e * xc_stride))) return rc;
-    if ((rc = ctx->ws_xp.ensure((size_t)nw * max_e * 2))) return rc;
+    if ((rc = w->r0.ensure((size_t)n_blocks * uni.size() * T))) return rc;
+    if ((rc = w->xb.ensure((size_t)nw * max_e * xc_stride))) return rc;
+    if ((rc = w->xp.ensure((size_t)nw * max_e * 2))) return rc;
 
     // 1) erased rows := 0, then r0 = the column program on every block (syndromes s = r ^ r0)
     ZeroArgs z;
     z.blk = di + o_zb; z.row = di + o_zr; z.data = static_cast<uint8_t*>(data); z.data_stride = data_stride;
     z.T = T; z.n = nz;
     if (launch_zero_rows(z, stream)) return fail(RQ_ERR_DEVICE, "k_zero_rows launch failed");
-    if ((rc = launch_col(ctx, k, T, n_blocks, data, data_stride, ctx->ws_r0.p, (uint64_t)uni.size() * T, stream)))
+    if ((rc = launch_col(ctx, k, T, n_blocks, data, data_stride, w->r0.p, (uint64_t)uni.size() * T, stream)))
         return rc;
     // 2) per-block solve
     SolveArgs s;
@@ -406,9 +419,9 @@ int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, v
     s.rep_uidx = di + o_ru;
     s.mrep = k->mrep.as<uint8_t>();
     s.mrep_stride = k->mrep_stride;
-    s.xcoef = ctx->ws_xb.as<uint8_t>();
-    s.xpiv = ctx->ws_xp.as<uint16_t>();
-    s.status = reinterpret_cast<int32_t*>(ctx->ws_idx.as<uint32_t>() + o_st);
+    s.xcoef = w->xb.as<uint8_t>();
+    s.xpiv = w->xp.as<uint16_t>();
+    s.status = reinterpret_cast<int32_t*>(w->idx.as<uint32_t>() + o_st);
     s.max_e = max_e;
     s.xc_stride = xc_stride;
     if (launch_solve(s, nw, (uint32_t)((max_lds_solve + 15) & ~size_t(15)), need_general, stream))
@@ -421,7 +434,7 @@ int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, v
     ap.rep_off = di + o_roff;
     ap.rep_uidx = di + o_ru;
     ap.recv = static_cast<const uint8_t*>(repair);
-    ap.r0 = ctx->ws_r0.as<uint8_t>();
+    ap.r0 = w->r0.as<uint8_t>();
     ap.n_union = (uint32_t)uni.size();
     ap.xcoef = s.xcoef;
     ap.xpiv = s.xpiv;
@@ -432,8 +445,8 @@ int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, v
     ap.max_e = max_e;
     ap.xc_stride = xc_stride;
     if (launch_apply(ap, (T / 4 + 63) / 64, nw, stream)) return fail(RQ_ERR_DEVICE, "k_apply launch failed");
-    int32_t* st = static_cast<int32_t*>(ctx->h_status.p);
-    HIP_TRY(hipMemcpyAsync(st, ctx->ws_idx.as<uint32_t>() + o_st, n_blocks * 4, hipMemcpyDeviceToHost,
+    int32_t* st = static_cast<int32_t*>(w->h_status.p);
+    HIP_TRY(hipMemcpyAsync(st, w->idx.as<uint32_t>() + o_st, n_blocks * 4, hipMemcpyDeviceToHost,
                            (hipStream_t)stream));
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
     for (uint32_t b : blk_map) status[b] = st[b];
@@ -542,7 +555,7 @@ int rq_debug_colprog_emulate(uint32_t K, uint32_t T, const uint32_t* esi, uint32
         if (opts[2]) o.la_load = opts[2];
         if (opts[3]) o.la_reload = opts[3];
         if (opts[4]) o.max_vmem = std::min<uint32_t>(opts[4], 60);
-        if (opts[5]) o.n_lds = std::min<uint32_t>(opts[5] - 1, 640);
+        if (opts[5]) o.n_lds = std::min<uint32_t>(opts[5] - 1, 512);
     }
     MProg mp;
     if (!allocate_colprog(ir, o, &mp, &err)) return fail(RQ_ERR_PLAN, err);
