@@ -55,7 +55,7 @@ struct AllocOpts {
     uint32_t la_reload = 160;    // look-ahead (IR nodes) for scratch reloads
     uint32_t max_vmem = 56;      // outstanding vector-memory operations per wave
     uint32_t n_lds = 156;        // LDS spill slots per wave (256 B each; 4 waves/CU -> 40 KB; <= 512)
-    uint32_t lds_horizon = 0;    // push an LDS resident out only if its next use is this much further
+    uint32_t lds_horizon = 200;  // push an LDS resident out only if its next use is this much further
 };
 
 struct MProg {

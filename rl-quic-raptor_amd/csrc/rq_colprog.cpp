@@ -501,6 +501,33 @@ bool build(const Params& p, const std::vector<OutDesc>& outs, ColIR* ir, std::st
         if (v == NOVAL) v = B.add(IR_ZERO);
         B.add(IR_STORE, v, NOVAL, NOVAL, o);
     }
+    // dead-code elimination: keep only what the stores need (e.g. outputs that are all source rows)
+    {
+        std::vector<uint8_t> live(ir->nodes.size(), 0);
+        for (size_t i = ir->nodes.size(); i-- > 0;) {
+            const IrNode& n = ir->nodes[i];
+            if (n.k == IR_STORE) live[i] = 1;
+            if (!live[i]) continue;
+            for (uint32_t x : {n.a, n.b, n.c})
+                if (x != NOVAL) live[x] = 1;
+        }
+        std::vector<uint32_t> remap(ir->nodes.size(), NOVAL);
+        std::vector<IrNode> kept;
+        kept.reserve(ir->nodes.size());
+        uint32_t ph = 0, new_ph[4] = {0, 0, 0, 0};
+        for (size_t i = 0; i < ir->nodes.size(); ++i) {
+            while (ph < 4 && ir->phase_start[ph] == i) new_ph[ph++] = (uint32_t)kept.size();
+            if (!live[i]) continue;
+            IrNode n = ir->nodes[i];
+            for (uint32_t* x : {&n.a, &n.b, &n.c})
+                if (*x != NOVAL) *x = remap[*x];
+            remap[i] = (uint32_t)kept.size();
+            kept.push_back(n);
+        }
+        while (ph < 4) new_ph[ph++] = (uint32_t)kept.size();
+        ir->nodes.swap(kept);
+        std::memcpy(ir->phase_start, new_ph, sizeof new_ph);
+    }
     auto& st = ir->st;
     for (const IrNode& n : ir->nodes) {
         switch (n.k) {

@@ -1,11 +1,12 @@
-# Round-1 measurement session: parity, bench line, rocprofv3 kernel trace + HBM counters.
+# HBM traffic of the encode column program (rocprofv3 PMC, one counter group per pass, as
+# MI355X_MICROARCH.md prescribes): FETCH_SIZE and WRITE_SIZE of the bench workload's encode launch
+# and of a same-pattern copy launch of known byte count (calibration).  Then summarise into
+# profiles/<tag>_traffic.json (tools/prof_summary.py traffic).
 set -o pipefail
 export TMPDIR=/tmp
-mkdir -p gpurun_out
-timeout -k 10 400 python -m pytest tests -m gpu -q --tb=short -x > gpurun_out/pytest_gpu.log 2>&1 && \
-timeout -k 10 400 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err && \
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_trace -o trace -- python3 bench.py --steps 5 --warmup 2 --cpu-sample 0 > gpurun_out/prof_trace.log 2>&1 && \
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_encode --output-format csv -d gpurun_out/prof_fetch -o fetch -- python3 tools/ablate.py > gpurun_out/prof_fetch.log 2>&1 && \
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_encode --output-format csv -d gpurun_out/prof_write -o write -- python3 tools/ablate.py > gpurun_out/prof_write.log 2>&1 && \
-RQHIP_DBG=6 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_encode --output-format csv -d gpurun_out/prof_fetch_cal -o cal -- python3 tools/ablate.py > gpurun_out/prof_fetch_cal.log 2>&1
+TAG=${1:-r01}
+mkdir -p gpurun_out/pmc_traffic
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex rq_colprog --output-format csv -d gpurun_out/pmc_traffic/fetch -o fetch -- python3 tools/pmc_workload.py > gpurun_out/pmc_traffic/fetch.log 2>&1 && \
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex rq_colprog --output-format csv -d gpurun_out/pmc_traffic/write -o write -- python3 tools/pmc_workload.py > gpurun_out/pmc_traffic/write.log 2>&1 && \
+python3 tools/prof_summary.py traffic gpurun_out/pmc_traffic $TAG > gpurun_out/pmc_traffic/summary.json
 echo EXIT $?

@@ -1,15 +1,29 @@
-"""Summarise rocprofv3 CSV output for profiles/: per (kernel, grid) launch shape the count and mean
-duration from *_kernel_trace.csv, and per-dispatch HBM bytes from *_counter_collection.csv
-(FETCH_SIZE / WRITE_SIZE are in KiB)."""
-import csv, json, sys
+"""Summarise rocprofv3 CSV output for profiles/.
+
+  prof_summary.py trace TRACE_CSV [COUNTER_CSV ...]   per (kernel, grid) count and mean duration,
+                                                      plus per-dispatch counter means
+  prof_summary.py traffic DIR TAG                     FETCH_SIZE / WRITE_SIZE passes of
+                                                      tools/gpu_profile.sh (copied to profiles/TAG_traffic.json)
+
+FETCH_SIZE / WRITE_SIZE are in KiB.  Calibration (MI355X_MICROARCH.md, HBM section): the counters are
+exact only for some access widths, so each is divided by its ratio on a same-pattern copy launch of
+known byte count (rq_colprog_K10_n10 = load + store of every source row, tools/pmc_workload.py).
+"""
+import csv
+import glob
+import json
+import os
+import sys
 from collections import defaultdict
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
 
 
 def trace_summary(path):
     g = defaultdict(list)
     for r in csv.DictReader(open(path)):
-        g[(r["Kernel_Name"], int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"]) if "Grid_Size_X" in r else r.get("Grid_Size"))].append(
-            int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        g[(r["Kernel_Name"], r.get("Grid_Size"))].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     out = []
     for (k, grid), d in sorted(g.items(), key=lambda kv: -sum(kv[1])):
         out.append({"kernel": k, "grid_threads": grid, "calls": len(d), "mean_us": round(sum(d) / len(d) / 1e3, 2),
@@ -17,16 +31,40 @@ def trace_summary(path):
     return out
 
 
-def counter_summary(path):
+def counter_means(path):
     g = defaultdict(list)
     for r in csv.DictReader(open(path)):
-        g[(r["Kernel_Name"], r["Grid_Size"], r["Counter_Name"])].append(float(r["Counter_Value"]))
-    return [{"kernel": k, "grid_threads": int(grid), "counter": c, "dispatches": len(v),
-             "mean_bytes": round(sum(v) / len(v) * 1024)} for (k, grid, c), v in g.items()]
+        g[(r["Kernel_Name"], r["Counter_Name"])].append(float(r["Counter_Value"]) * 1024.0)
+    return {k: sum(v) / len(v) for k, v in g.items()}
+
+
+def traffic(d, tag):
+    fetch = counter_means(glob.glob(os.path.join(d, "fetch", "*counter_collection.csv"))[0])
+    write = counter_means(glob.glob(os.path.join(d, "write", "*counter_collection.csv"))[0])
+    cal_bytes = 65536 * 10 * 1200
+    cal, enc = "rq_colprog_K10_n10", "rq_colprog_K1024_n76"
+    f_cal, w_cal = fetch[(cal, "FETCH_SIZE")] / cal_bytes, write[(cal, "WRITE_SIZE")] / cal_bytes
+    f_enc, w_enc = fetch[(enc, "FETCH_SIZE")] / f_cal, write[(enc, "WRITE_SIZE")] / w_cal
+    out = {
+        "kernel": enc,
+        "workload": {"K": 1024, "T": 1200, "N": 1100, "blocks": 1024},
+        "fetch_bytes": round(f_enc), "write_bytes": round(w_enc), "traffic_bytes": round(f_enc + w_enc),
+        "algorithmic_bytes": {"read": 1024 * 1024 * 1200, "write": 1024 * 76 * 1200},
+        "calibration": {"kernel": cal, "bytes_read_and_written": cal_bytes, "fetch_ratio": round(f_cal, 4),
+                        "write_ratio": round(w_cal, 4)},
+        "raw_kib": {"fetch": fetch[(enc, "FETCH_SIZE")] / 1024, "write": write[(enc, "WRITE_SIZE")] / 1024},
+        "source": "tools/gpu_profile.sh: rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
+                  "tools/pmc_workload.py; counters divided by their ratio on the calibration copy",
+    }
+    out["tag"] = tag
+    return out
 
 
 if __name__ == "__main__":
-    res = {"trace": trace_summary(sys.argv[1]), "counters": []}
-    for p in sys.argv[2:]:
-        res["counters"] += counter_summary(p)
-    print(json.dumps(res, indent=1))
+    if sys.argv[1] == "traffic":
+        print(json.dumps(traffic(sys.argv[2], sys.argv[3]), indent=1))
+    else:
+        res = {"trace": trace_summary(sys.argv[2]), "counters": []}
+        for p in sys.argv[3:]:
+            res["counters"] += [{"kernel": k, "counter": c, "mean_bytes": round(v)} for (k, c), v in counter_means(p).items()]
+        print(json.dumps(res, indent=1))
