@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--erase", type=float, default=0.05)
     ap.add_argument("--cpu-sample", type=int, default=20, help="blocks in the CPU baseline sample (0 = skip)")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", help="process-group backend for the timing collectives "
+                    "(nccl = RCCL; gloo lets several ranks share one GPU for a functional rehearsal)")
     return ap.parse_args()
 
 
@@ -108,11 +110,13 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as tdist
-        tdist.init_process_group("nccl")
+        tdist.init_process_group(args.dist_backend)
         dist = tdist
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    rqhip.lib().rq_set_device(local)
+    gpu = local % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    rqhip.lib().rq_set_device(gpu)
+    coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
     K, T, N, B = args.K, args.T, args.N, args.blocks
     R = N - K
     n_erase = int(round(args.erase * N))
@@ -161,10 +165,10 @@ def main():
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
-    dt = rqshard.max_over_ranks(time.perf_counter() - t0, dist, dev)
+    dt = rqshard.max_over_ranks(time.perf_counter() - t0, dist, coll_dev)
     enc_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1, _ in ev]))
     dec_ms = float(np.mean([e1.elapsed_time(e2) for _, e1, e2 in ev]))
-    total_blocks = rqshard.sum_over_ranks(B, dist, dev)
+    total_blocks = rqshard.sum_over_ranks(B, dist, coll_dev)
     value = total_blocks * K * T * args.steps / dt / 1e9
     if rank == 0:
         kname = "rq_colprog_K%d_n%d" % (K, R)

@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <queue>
@@ -454,7 +455,27 @@ bool divmagic(uint32_t d, uint32_t limit, uint32_t* magic, uint32_t* shift) {
 }
 
 // ------------------------------------------------------------------------------------------
+// Cache-policy suffixes of the memory instructions (gfx950 sc0/sc1/nt bits).  Source rows and
+// output rows stream once; scratch lines are re-read soon.  RQHIP_POLICY="src;out;scr_st;scr_ld"
+// overrides them for experiments.
+struct Policy {
+    std::string src = " nt", out = " nt", scr_st = "", scr_ld = " sc1";
+    Policy() {
+        if (const char* e = std::getenv("RQHIP_POLICY")) {
+            std::string v(e), f[4];
+            int i = 0;
+            for (char c : v) {
+                if (c == ';') { if (++i == 4) break; continue; }
+                f[i] += c;
+            }
+            std::string* dst[4] = {&src, &out, &scr_st, &scr_ld};
+            for (int k = 0; k < 4; ++k) *dst[k] = f[k].empty() ? "" : " " + f[k];
+        }
+    }
+};
+
 std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
+    static const Policy pol;
     const Reserved rv(mp.n_vgpr);
     const int V_T1 = rv.t1, V_T2 = rv.t2, V_SCROFF = rv.scroff, V_OUTOFF = rv.outoff, V_SRCOFF = rv.srcoff;
     const uint32_t acc_off = (mp.n_vgpr + N_RESERVED + 3) & ~3u;        // first AGPR in the unified file
@@ -544,25 +565,25 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
             case MI_LDSRC: {
                 const int q = srot();
                 std::snprintf(buf, sizeof buf, "s_mul_i32 s%d, s12, %u", q, m.imm); line(buf);
-                std::snprintf(buf, sizeof buf, "buffer_load_dword %s, v%d, s[24:27], s%d offen", R(m.d), V_SRCOFF, q); line(buf);
+                std::snprintf(buf, sizeof buf, "buffer_load_dword %s, v%d, s[24:27], s%d offen%s", R(m.d), V_SRCOFF, q, pol.src.c_str()); line(buf);
                 break;
             }
             case MI_STOUT: {
                 const int q = srot();
                 std::snprintf(buf, sizeof buf, "s_mul_i32 s%d, s12, %u", q, m.imm); line(buf);
-                std::snprintf(buf, sizeof buf, "buffer_store_dword %s, v%d, s[28:31], s%d offen", R(m.a), V_OUTOFF, q); line(buf);
+                std::snprintf(buf, sizeof buf, "buffer_store_dword %s, v%d, s[28:31], s%d offen%s", R(m.a), V_OUTOFF, q, pol.out.c_str()); line(buf);
                 break;
             }
             case MI_SPST: {
                 const int q = srot();
                 std::snprintf(buf, sizeof buf, "s_mov_b32 s%d, %u", q, m.imm * 256u); line(buf);
-                std::snprintf(buf, sizeof buf, "buffer_store_dword %s, v%d, s[32:35], s%d offen", R(m.a), V_SCROFF, q); line(buf);
+                std::snprintf(buf, sizeof buf, "buffer_store_dword %s, v%d, s[32:35], s%d offen%s", R(m.a), V_SCROFF, q, pol.scr_st.c_str()); line(buf);
                 break;
             }
             case MI_SPLD: {
                 const int q = srot();
                 std::snprintf(buf, sizeof buf, "s_mov_b32 s%d, %u", q, m.imm * 256u); line(buf);
-                std::snprintf(buf, sizeof buf, "buffer_load_dword %s, v%d, s[32:35], s%d offen sc1", R(m.d), V_SCROFF, q); line(buf);
+                std::snprintf(buf, sizeof buf, "buffer_load_dword %s, v%d, s[32:35], s%d offen%s", R(m.d), V_SCROFF, q, pol.scr_ld.c_str()); line(buf);
                 break;
             }
             case MI_ACCW:

@@ -301,14 +301,20 @@ int launch_solve(const SolveArgs& a, uint32_t n_blocks, uint32_t lds_bytes, bool
 // syndrome, formed on the fly).  GF(256) by bit decomposition: the eight multiples alpha^b s_m are
 // built by xtime, and output k takes those its coefficient X[k][m] selects.  X[k][m] is uniform
 // (scalar loads), so a selection is one s_bfe_i32 mask and one v_bitop3 per bit.
+// Each lane owns APPLY_CPL dword columns (64 apart, so every load/store instruction stays one
+// contiguous 256-B segment): the scalar mask of a coefficient bit (one s_bfe_i32 -- the scalar
+// unit issues one instruction per cycle per CU and was the bound at one column per lane) is shared
+// by APPLY_CPL v_bitop3 ops.  Outputs are produced in passes of KC.
+constexpr int APPLY_CPL = 4;
+
 template <int KC>
 __global__ void __launch_bounds__(64) k_apply(ApplyArgs a) {
+    constexpr int CPL = APPLY_CPL;
     const uint32_t b = a.blk_map[blockIdx.y];
     if (a.status[b] != 1) return;
     const uint32_t lane = threadIdx.x;
     const uint32_t e = a.erased_off[b + 1] - a.erased_off[b];
-    const uint32_t Td = a.T >> 2, c = blockIdx.x * 64 + lane;
-    const bool live = c < Td;
+    const uint32_t Td = a.T >> 2;
     const uint32_t* E = a.erased + a.erased_off[b];
     const uint8_t* xc = a.xcoef + (size_t)blockIdx.y * a.max_e * a.xc_stride;
     const uint16_t* XP = a.xpiv + (size_t)blockIdx.y * a.max_e;
@@ -316,6 +322,14 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a) {
     const uint32_t* recv = reinterpret_cast<const uint32_t*>(a.recv);
     const uint32_t* r0 = reinterpret_cast<const uint32_t*>(a.r0) + (size_t)b * a.n_union * Td;
     uint8_t* blk = a.data + (size_t)b * a.data_stride;
+    uint32_t col[CPL];
+    bool live[CPL];
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+        const uint32_t c = blockIdx.x * 64 * CPL + j * 64 + lane;
+        live[j] = c < Td;
+        col[j] = live[j] ? c : 0;
+    }
     // dword offsets of the syndrome operands of every m (received row, r0 row), staged once
     __shared__ uint32_t offr[256], off0[256];
     for (uint32_t m = lane; m < e; m += 64) {
@@ -324,58 +338,78 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a) {
         off0[m] = a.rep_uidx[j] * Td;
     }
     __syncthreads();
-    const uint32_t cc = live ? c : 0;
     for (uint32_t k0 = 0; k0 < e; k0 += KC) {
-        uint32_t acc[KC];
+        uint32_t acc[KC][CPL];
 #pragma unroll
-        for (int k = 0; k < KC; ++k) acc[k] = 0;
-        uint32_t s_next = recv[(size_t)offr[0] + cc] ^ r0[(size_t)off0[0] + cc];
+        for (int k = 0; k < KC; ++k)
+#pragma unroll
+            for (int j = 0; j < CPL; ++j) acc[k][j] = 0;
+        uint32_t s_next[CPL];
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) s_next[j] = recv[(size_t)offr[0] + col[j]] ^ r0[(size_t)off0[0] + col[j]];
         for (uint32_t m = 0; m < e; ++m) {
-            uint32_t s = s_next;
-            if (m + 1 < e) s_next = recv[(size_t)offr[m + 1] + cc] ^ r0[(size_t)off0[m + 1] + cc];  // prefetch
-            const uint32_t* cw = reinterpret_cast<const uint32_t*>(xc + (size_t)m * a.xc_stride + k0);
-            uint32_t mul[8];
+            uint32_t mul[8][CPL];
 #pragma unroll
-            for (int bt = 0; bt < 8; ++bt) {
-                mul[bt] = s;
-                s = xtime4(s);
+            for (int j = 0; j < CPL; ++j) {
+                uint32_t s = s_next[j];
+#pragma unroll
+                for (int bt = 0; bt < 8; ++bt) {
+                    mul[bt][j] = s;
+                    s = xtime4(s);
+                }
             }
+            if (m + 1 < e) {  // prefetch the next syndrome while this one is applied
 #pragma unroll
-            for (int kq = 0; kq < KC / 16; ++kq) {
-                const uint4 w4 = reinterpret_cast<const uint4*>(cw)[kq];
-                const uint32_t wv[4] = {w4.x, w4.y, w4.z, w4.w};
+                for (int j = 0; j < CPL; ++j)
+                    s_next[j] = recv[(size_t)offr[m + 1] + col[j]] ^ r0[(size_t)off0[m + 1] + col[j]];
+            }
+            const uint32_t* cw = reinterpret_cast<const uint32_t*>(xc + (size_t)m * a.xc_stride + k0);
 #pragma unroll
-                for (int kw = 0; kw < 4; ++kw) {
-                    const int w = __builtin_amdgcn_readfirstlane((int)wv[kw]);
+            for (int kw = 0; kw < KC / 4; ++kw) {
+                const int w = __builtin_amdgcn_readfirstlane((int)cw[kw]);
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
+                for (int q = 0; q < 4; ++q) {
 #pragma unroll
-                        for (int bt = 0; bt < 8; ++bt) {
-                            const int msk = __builtin_amdgcn_sbfe(w, q * 8 + bt, 1);
+                    for (int bt = 0; bt < 8; ++bt) {
+                        const int msk = __builtin_amdgcn_sbfe(w, q * 8 + bt, 1);
+#pragma unroll
+                        for (int j = 0; j < CPL; ++j)
                             // acc ^= mul & msk  (v_bitop3: src0 acc 0xF0, src1 mul 0xCC, src2 msk 0xAA)
                             asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x78"
-                                         : "+v"(acc[kq * 16 + kw * 4 + q])
-                                         : "v"(mul[bt]), "s"(msk));
-                        }
+                                         : "+v"(acc[kw * 4 + q][j])
+                                         : "v"(mul[bt][j]), "s"(msk));
                     }
                 }
             }
         }
-        if (live) {
-            const uint32_t kn = min((uint32_t)KC, e - k0);
+        const uint32_t kn = min((uint32_t)KC, e - k0);
 #pragma unroll
-            for (int k = 0; k < KC; ++k)
-                if ((uint32_t)k < kn) reinterpret_cast<uint32_t*>(blk + (size_t)E[k0 + k] * a.T)[c] = acc[k];
+        for (int k = 0; k < KC; ++k) {
+            if ((uint32_t)k < kn) {
+                uint32_t* row = reinterpret_cast<uint32_t*>(blk + (size_t)E[k0 + k] * a.T);
+#pragma unroll
+                for (int j = 0; j < CPL; ++j)
+                    if (live[j]) row[col[j]] = acc[k][j];
+            }
         }
     }
 }
 
-int launch_apply(const ApplyArgs& a, uint32_t n_strips, uint32_t n_blocks, void* stream) {
-    const dim3 g(n_strips, n_blocks);
-    if (a.max_e <= 16) hipLaunchKernelGGL(k_apply<16>, g, dim3(64), 0, (hipStream_t)stream, a);
-    else if (a.max_e <= 32) hipLaunchKernelGGL(k_apply<32>, g, dim3(64), 0, (hipStream_t)stream, a);
-    else if (a.max_e <= 48) hipLaunchKernelGGL(k_apply<48>, g, dim3(64), 0, (hipStream_t)stream, a);
-    else hipLaunchKernelGGL(k_apply<64>, g, dim3(64), 0, (hipStream_t)stream, a);
+int launch_apply(const ApplyArgs& a, uint32_t /*n_strips*/, uint32_t n_blocks, void* stream) {
+    const uint32_t strips = (a.T / 4 + 64 * APPLY_CPL - 1) / (64 * APPLY_CPL);
+    const dim3 g(strips, n_blocks);
+    // passes of at most 32 outputs, balanced: e.g. e = 52 -> two passes of KC = 28
+    const uint32_t np = (a.max_e + 31) / 32, kc = (((a.max_e + np - 1) / np) + 3) & ~3u;
+    switch (kc) {
+        case 4: hipLaunchKernelGGL(k_apply<4>, g, dim3(64), 0, (hipStream_t)stream, a); break;
+        case 8: hipLaunchKernelGGL(k_apply<8>, g, dim3(64), 0, (hipStream_t)stream, a); break;
+        case 12: hipLaunchKernelGGL(k_apply<12>, g, dim3(64), 0, (hipStream_t)stream, a); break;
+        case 16: hipLaunchKernelGGL(k_apply<16>, g, dim3(64), 0, (hipStream_t)stream, a); break;
+        case 20: hipLaunchKernelGGL(k_apply<20>, g, dim3(64), 0, (hipStream_t)stream, a); break;
+        case 24: hipLaunchKernelGGL(k_apply<24>, g, dim3(64), 0, (hipStream_t)stream, a); break;
+        case 28: hipLaunchKernelGGL(k_apply<28>, g, dim3(64), 0, (hipStream_t)stream, a); break;
+        default: hipLaunchKernelGGL(k_apply<32>, g, dim3(64), 0, (hipStream_t)stream, a); break;
+    }
     return (int)hipGetLastError();
 }
 
