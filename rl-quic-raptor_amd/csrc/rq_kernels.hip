@@ -301,15 +301,13 @@ int launch_solve(const SolveArgs& a, uint32_t n_blocks, uint32_t lds_bytes, bool
 // syndrome, formed on the fly).  GF(256) by bit decomposition: the eight multiples alpha^b s_m are
 // built by xtime, and output k takes those its coefficient X[k][m] selects.  X[k][m] is uniform
 // (scalar loads), so a selection is one s_bfe_i32 mask and one v_bitop3 per bit.
-// Each lane owns APPLY_CPL dword columns (64 apart, so every load/store instruction stays one
-// contiguous 256-B segment): the scalar mask of a coefficient bit (one s_bfe_i32 -- the scalar
-// unit issues one instruction per cycle per CU and was the bound at one column per lane) is shared
-// by APPLY_CPL v_bitop3 ops.  Outputs are produced in passes of KC.
-constexpr int APPLY_CPL = 4;
-
-template <int KC>
+// Each lane owns CPL dword columns (64 apart, so every load/store instruction stays one contiguous
+// 256-B segment): the scalar mask of a coefficient bit (one s_bfe_i32 -- the scalar unit issues one
+// instruction per cycle per CU and bounds the one-column form) is shared by CPL v_bitop3 ops.  CPL
+// is chosen per T to minimise padded columns (T = 1200: 300 dwords = one wave of 5 x 64, 94 % live).
+// Outputs are produced in balanced passes of KC <= 32.
+template <int KC, int CPL>
 __global__ void __launch_bounds__(64) k_apply(ApplyArgs a) {
-    constexpr int CPL = APPLY_CPL;
     const uint32_t b = a.blk_map[blockIdx.y];
     if (a.status[b] != 1) return;
     const uint32_t lane = threadIdx.x;
@@ -395,20 +393,36 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a) {
     }
 }
 
+template <int CPL>
+static void launch_apply_cpl(const ApplyArgs& a, uint32_t kc, dim3 g, hipStream_t st) {
+    switch (kc) {
+        case 4: hipLaunchKernelGGL((k_apply<4, CPL>), g, dim3(64), 0, st, a); break;
+        case 8: hipLaunchKernelGGL((k_apply<8, CPL>), g, dim3(64), 0, st, a); break;
+        case 12: hipLaunchKernelGGL((k_apply<12, CPL>), g, dim3(64), 0, st, a); break;
+        case 16: hipLaunchKernelGGL((k_apply<16, CPL>), g, dim3(64), 0, st, a); break;
+        case 20: hipLaunchKernelGGL((k_apply<20, CPL>), g, dim3(64), 0, st, a); break;
+        case 24: hipLaunchKernelGGL((k_apply<24, CPL>), g, dim3(64), 0, st, a); break;
+        case 28: hipLaunchKernelGGL((k_apply<28, CPL>), g, dim3(64), 0, st, a); break;
+        default: hipLaunchKernelGGL((k_apply<32, CPL>), g, dim3(64), 0, st, a); break;
+    }
+}
+
 int launch_apply(const ApplyArgs& a, uint32_t /*n_strips*/, uint32_t n_blocks, void* stream) {
-    const uint32_t strips = (a.T / 4 + 64 * APPLY_CPL - 1) / (64 * APPLY_CPL);
-    const dim3 g(strips, n_blocks);
+    const uint32_t Td = a.T / 4;
+    uint32_t cpl = 1, best = 0xFFFFFFFFu;  // fewest padded columns, then the widest lanes
+    for (uint32_t c : {1u, 2u, 4u, 5u}) {
+        const uint32_t w = 64 * c, pad = (Td + w - 1) / w * w - Td;
+        if (pad <= best) { best = pad; cpl = c; }
+    }
+    const dim3 g((Td + 64 * cpl - 1) / (64 * cpl), n_blocks);
     // passes of at most 32 outputs, balanced: e.g. e = 52 -> two passes of KC = 28
     const uint32_t np = (a.max_e + 31) / 32, kc = (((a.max_e + np - 1) / np) + 3) & ~3u;
-    switch (kc) {
-        case 4: hipLaunchKernelGGL(k_apply<4>, g, dim3(64), 0, (hipStream_t)stream, a); break;
-        case 8: hipLaunchKernelGGL(k_apply<8>, g, dim3(64), 0, (hipStream_t)stream, a); break;
-        case 12: hipLaunchKernelGGL(k_apply<12>, g, dim3(64), 0, (hipStream_t)stream, a); break;
-        case 16: hipLaunchKernelGGL(k_apply<16>, g, dim3(64), 0, (hipStream_t)stream, a); break;
-        case 20: hipLaunchKernelGGL(k_apply<20>, g, dim3(64), 0, (hipStream_t)stream, a); break;
-        case 24: hipLaunchKernelGGL(k_apply<24>, g, dim3(64), 0, (hipStream_t)stream, a); break;
-        case 28: hipLaunchKernelGGL(k_apply<28>, g, dim3(64), 0, (hipStream_t)stream, a); break;
-        default: hipLaunchKernelGGL(k_apply<32>, g, dim3(64), 0, (hipStream_t)stream, a); break;
+    const hipStream_t st = (hipStream_t)stream;
+    switch (cpl) {
+        case 1: launch_apply_cpl<1>(a, kc, g, st); break;
+        case 2: launch_apply_cpl<2>(a, kc, g, st); break;
+        case 4: launch_apply_cpl<4>(a, kc, g, st); break;
+        default: launch_apply_cpl<5>(a, kc, g, st); break;
     }
     return (int)hipGetLastError();
 }
