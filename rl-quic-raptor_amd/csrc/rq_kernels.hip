@@ -41,6 +41,13 @@ __device__ __forceinline__ uint32_t xtime4(uint32_t x) {
     return ((x & 0x7F7F7F7Fu) << 1) ^ (mask & 0x1D1D1D1Du);
 }
 
+// a ^ (b & m) in one v_bitop3 (src0 a 0xF0, src1 b 0xCC, src2 m 0xAA -> 0x78)
+__device__ __forceinline__ uint32_t bitop_xand(uint32_t a, uint32_t b, uint32_t m) {
+    uint32_t d;
+    asm volatile("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x78" : "=v"(d) : "v"(a), "v"(b), "v"(m));
+    return d;
+}
+
 // ------------------------------ LT tuple on device (RQ/params.go:83-112) -------------------
 __device__ __forceinline__ uint32_t d_rand(uint32_t y, uint32_t i, uint32_t m) {
     return (c_V[0][(y + i) & 255u] ^ c_V[1][((y >> 8) + i) & 255u] ^ c_V[2][((y >> 16) + i) & 255u] ^
@@ -197,10 +204,10 @@ __global__ void __launch_bounds__(64) k_solve64(SolveArgs a) {
 #pragma unroll
                 for (int bt = 0; bt < 8; ++bt) {
                     const uint4 m = mult[bt][q];
-                    r.x ^= m.x & msk[bt];
-                    r.y ^= m.y & msk[bt];
-                    r.z ^= m.z & msk[bt];
-                    r.w ^= m.w & msk[bt];
+                    r.x = bitop_xand(r.x, m.x, msk[bt]);
+                    r.y = bitop_xand(r.y, m.y, msk[bt]);
+                    r.z = bitop_xand(r.z, m.z, msk[bt]);
+                    r.w = bitop_xand(r.w, m.w, msk[bt]);
                 }
                 my4[q] = r;
             }
@@ -305,17 +312,23 @@ int launch_solve(const SolveArgs& a, uint32_t n_blocks, uint32_t lds_bytes, bool
 // 256-B segment): the scalar mask of a coefficient bit (one s_bfe_i32 -- the scalar unit issues one
 // instruction per cycle per CU and bounds the one-column form) is shared by CPL v_bitop3 ops.  CPL
 // is chosen per T to minimise padded columns (T = 1200: 300 dwords = one wave of 5 x 64, 94 % live).
-// Outputs are produced in balanced passes of KC <= 32.
+// Outputs are split into balanced slices of KC <= 32, one wave per (strip, slice, block): enough
+// waves for two per SIMD (the VALU then issues every 2 cycles instead of 4).
 template <int KC, int CPL>
 __global__ void __launch_bounds__(64) k_apply(ApplyArgs a) {
-    const uint32_t b = a.blk_map[blockIdx.y];
+    // grid.x = solved block * strips + strip, grid.y = output slice
+    const uint32_t strips = ((a.T >> 2) + 64 * CPL - 1) / (64 * CPL);
+    const uint32_t bi = blockIdx.x / strips, strip = blockIdx.x - bi * strips;
+    const uint32_t b = a.blk_map[bi];
     if (a.status[b] != 1) return;
     const uint32_t lane = threadIdx.x;
     const uint32_t e = a.erased_off[b + 1] - a.erased_off[b];
+    const uint32_t k0 = blockIdx.y * KC;
+    if (k0 >= e) return;
     const uint32_t Td = a.T >> 2;
     const uint32_t* E = a.erased + a.erased_off[b];
-    const uint8_t* xc = a.xcoef + (size_t)blockIdx.y * a.max_e * a.xc_stride;
-    const uint16_t* XP = a.xpiv + (size_t)blockIdx.y * a.max_e;
+    const uint8_t* xc = a.xcoef + (size_t)bi * a.max_e * a.xc_stride;
+    const uint16_t* XP = a.xpiv + (size_t)bi * a.max_e;
     const uint32_t r0b = a.rep_off[b];
     const uint32_t* recv = reinterpret_cast<const uint32_t*>(a.recv);
     const uint32_t* r0 = reinterpret_cast<const uint32_t*>(a.r0) + (size_t)b * a.n_union * Td;
@@ -324,7 +337,7 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a) {
     bool live[CPL];
 #pragma unroll
     for (int j = 0; j < CPL; ++j) {
-        const uint32_t c = blockIdx.x * 64 * CPL + j * 64 + lane;
+        const uint32_t c = strip * 64 * CPL + j * 64 + lane;
         live[j] = c < Td;
         col[j] = live[j] ? c : 0;
     }
@@ -336,7 +349,7 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a) {
         off0[m] = a.rep_uidx[j] * Td;
     }
     __syncthreads();
-    for (uint32_t k0 = 0; k0 < e; k0 += KC) {
+    {
         uint32_t acc[KC][CPL];
 #pragma unroll
         for (int k = 0; k < KC; ++k)
@@ -414,9 +427,9 @@ int launch_apply(const ApplyArgs& a, uint32_t /*n_strips*/, uint32_t n_blocks, v
         const uint32_t w = 64 * c, pad = (Td + w - 1) / w * w - Td;
         if (pad <= best) { best = pad; cpl = c; }
     }
-    const dim3 g((Td + 64 * cpl - 1) / (64 * cpl), n_blocks);
-    // passes of at most 32 outputs, balanced: e.g. e = 52 -> two passes of KC = 28
+    // slices of at most 32 outputs, balanced: e.g. e = 52 -> two slices of KC = 28
     const uint32_t np = (a.max_e + 31) / 32, kc = (((a.max_e + np - 1) / np) + 3) & ~3u;
+    const dim3 g((Td + 64 * cpl - 1) / (64 * cpl) * n_blocks, np);
     const hipStream_t st = (hipStream_t)stream;
     switch (cpl) {
         case 1: launch_apply_cpl<1>(a, kc, g, st); break;
