@@ -35,16 +35,17 @@ int upload_tables() {
 }
 
 // ------------------------------ GF(256) on packed dwords ------------------------------------
+// alpha * x per byte: v_perm's sign-replicating selectors turn the four top bits into 0x00/0xFF
+// byte masks (selector bytes 0x0a,0x08,0x0b,0x09 read bits 7,15,23,31 of {x<<8 : x}), no multiply.
 __device__ __forceinline__ uint32_t xtime4(uint32_t x) {
-    const uint32_t hi = (x >> 7) & 0x01010101u;
-    const uint32_t mask = (hi << 8) - hi;  // 0x00 / 0xFF per byte (no multiply)
-    return ((x & 0x7F7F7F7Fu) << 1) ^ (mask & 0x1D1D1D1Du);
+    const uint32_t mask = __builtin_amdgcn_perm(x << 8, x, 0x090b080au);
+    return ((x << 1) & 0xFEFEFEFEu) ^ (mask & 0x1D1D1D1Du);
 }
 
 // a ^ (b & m) in one v_bitop3 (src0 a 0xF0, src1 b 0xCC, src2 m 0xAA -> 0x78)
 __device__ __forceinline__ uint32_t bitop_xand(uint32_t a, uint32_t b, uint32_t m) {
     uint32_t d;
-    asm volatile("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x78" : "=v"(d) : "v"(a), "v"(b), "v"(m));
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x78" : "=v"(d) : "v"(a), "v"(b), "v"(m));
     return d;
 }
 
@@ -204,10 +205,10 @@ __global__ void __launch_bounds__(64) k_solve64(SolveArgs a) {
 #pragma unroll
                 for (int bt = 0; bt < 8; ++bt) {
                     const uint4 m = mult[bt][q];
-                    r.x = bitop_xand(r.x, m.x, msk[bt]);
-                    r.y = bitop_xand(r.y, m.y, msk[bt]);
-                    r.z = bitop_xand(r.z, m.z, msk[bt]);
-                    r.w = bitop_xand(r.w, m.w, msk[bt]);
+                    r.x ^= m.x & msk[bt];
+                    r.y ^= m.y & msk[bt];
+                    r.z ^= m.z & msk[bt];
+                    r.w ^= m.w & msk[bt];
                 }
                 my4[q] = r;
             }
@@ -358,7 +359,22 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a) {
         uint32_t s_next[CPL];
 #pragma unroll
         for (int j = 0; j < CPL; ++j) s_next[j] = recv[(size_t)offr[0] + col[j]] ^ r0[(size_t)off0[0] + col[j]];
+        // coefficient bytes X[k0..k0+KC)[m] (uniform): loaded one m ahead
+        uint32_t w_next[KC / 4];
+        {
+            const uint32_t* cw = reinterpret_cast<const uint32_t*>(xc + k0);
+#pragma unroll
+            for (int kw = 0; kw < KC / 4; ++kw) w_next[kw] = __builtin_amdgcn_readfirstlane((int)cw[kw]);
+        }
         for (uint32_t m = 0; m < e; ++m) {
+            uint32_t wcur[KC / 4];
+#pragma unroll
+            for (int kw = 0; kw < KC / 4; ++kw) wcur[kw] = w_next[kw];
+            if (m + 1 < e) {
+                const uint32_t* cw = reinterpret_cast<const uint32_t*>(xc + (size_t)(m + 1) * a.xc_stride + k0);
+#pragma unroll
+                for (int kw = 0; kw < KC / 4; ++kw) w_next[kw] = __builtin_amdgcn_readfirstlane((int)cw[kw]);
+            }
             uint32_t mul[8][CPL];
 #pragma unroll
             for (int j = 0; j < CPL; ++j) {
@@ -374,10 +390,9 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a) {
                 for (int j = 0; j < CPL; ++j)
                     s_next[j] = recv[(size_t)offr[m + 1] + col[j]] ^ r0[(size_t)off0[m + 1] + col[j]];
             }
-            const uint32_t* cw = reinterpret_cast<const uint32_t*>(xc + (size_t)m * a.xc_stride + k0);
 #pragma unroll
             for (int kw = 0; kw < KC / 4; ++kw) {
-                const int w = __builtin_amdgcn_readfirstlane((int)cw[kw]);
+                const int w = (int)wcur[kw];
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
 #pragma unroll
@@ -386,9 +401,9 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a) {
 #pragma unroll
                         for (int j = 0; j < CPL; ++j)
                             // acc ^= mul & msk  (v_bitop3: src0 acc 0xF0, src1 mul 0xCC, src2 msk 0xAA)
-                            asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x78"
-                                         : "+v"(acc[kw * 4 + q][j])
-                                         : "v"(mul[bt][j]), "s"(msk));
+                            asm("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x78"
+                                : "+v"(acc[kw * 4 + q][j])
+                                : "v"(mul[bt][j]), "s"(msk));
                     }
                 }
             }
