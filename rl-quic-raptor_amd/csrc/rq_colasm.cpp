@@ -474,8 +474,16 @@ struct Policy {
     }
 };
 
+// Diagnostic builds (wrong bytes, timing only): RQHIP_DIAG bit 1 drops global scratch traffic,
+// 2 drops LDS spill traffic, 4 replaces source loads by register writes, 8 drops output stores.
+static uint32_t diag_mask() {
+    const char* e = std::getenv("RQHIP_DIAG");
+    return e ? (uint32_t)std::atoi(e) : 0u;
+}
+
 std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
     static const Policy pol;
+    static const uint32_t diag = diag_mask();
     const Reserved rv(mp.n_vgpr);
     const int V_T1 = rv.t1, V_T2 = rv.t2, V_SCROFF = rv.scroff, V_OUTOFF = rv.outoff, V_SRCOFF = rv.srcoff;
     const uint32_t acc_off = (mp.n_vgpr + N_RESERVED + 3) & ~3u;        // first AGPR in the unified file
@@ -563,24 +571,33 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
             case MI_ZERO:
                 std::snprintf(buf, sizeof buf, "v_mov_b32_e32 v%d, 0", m.d); line(buf); break;
             case MI_LDSRC: {
+                if (diag & 4) {
+                    std::snprintf(buf, sizeof buf, is_agpr(m.d) ? "v_accvgpr_write_b32 %s, v%d" : "v_mov_b32_e32 %s, v%d",
+                                  R(m.d), V_SRCOFF);
+                    line(buf);
+                    break;
+                }
                 const int q = srot();
                 std::snprintf(buf, sizeof buf, "s_mul_i32 s%d, s12, %u", q, m.imm); line(buf);
                 std::snprintf(buf, sizeof buf, "buffer_load_dword %s, v%d, s[24:27], s%d offen%s", R(m.d), V_SRCOFF, q, pol.src.c_str()); line(buf);
                 break;
             }
             case MI_STOUT: {
+                if (diag & 8) break;
                 const int q = srot();
                 std::snprintf(buf, sizeof buf, "s_mul_i32 s%d, s12, %u", q, m.imm); line(buf);
                 std::snprintf(buf, sizeof buf, "buffer_store_dword %s, v%d, s[28:31], s%d offen%s", R(m.a), V_OUTOFF, q, pol.out.c_str()); line(buf);
                 break;
             }
             case MI_SPST: {
+                if (diag & 1) break;
                 const int q = srot();
                 std::snprintf(buf, sizeof buf, "s_mov_b32 s%d, %u", q, m.imm * 256u); line(buf);
                 std::snprintf(buf, sizeof buf, "buffer_store_dword %s, v%d, s[32:35], s%d offen%s", R(m.a), V_SCROFF, q, pol.scr_st.c_str()); line(buf);
                 break;
             }
             case MI_SPLD: {
+                if (diag & 1) break;
                 const int q = srot();
                 std::snprintf(buf, sizeof buf, "s_mov_b32 s%d, %u", q, m.imm * 256u); line(buf);
                 std::snprintf(buf, sizeof buf, "buffer_load_dword %s, v%d, s[32:35], s%d offen%s", R(m.d), V_SCROFF, q, pol.scr_ld.c_str()); line(buf);
@@ -595,11 +612,13 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
             case MI_NOP:
                 std::snprintf(buf, sizeof buf, "s_nop %u", m.imm); line(buf); break;
             case MI_LDST:
+                if (diag & 2) break;
                 std::snprintf(buf, sizeof buf, "ds_write_b32 v%d, %s offset:%u", m.imm < 256 ? V_SCROFF : rv.lds2, R(m.a),
                               (m.imm & 255u) * 256u);
                 line(buf);
                 break;
             case MI_LDLD:
+                if (diag & 2) break;
                 std::snprintf(buf, sizeof buf, "ds_read_b32 %s, v%d offset:%u", R(m.d), m.imm < 256 ? V_SCROFF : rv.lds2,
                               (m.imm & 255u) * 256u);
                 line(buf);
