@@ -28,6 +28,7 @@ struct Allocator {
     std::vector<int32_t> slot;                      // value -> scratch slot with a valid copy or -1
     std::vector<int32_t> lslot;                     // value -> LDS slot with a valid copy or -1
     std::vector<uint8_t> issued;                    // LOAD value already issued
+    std::vector<uint64_t> dma_seq;                  // LOAD value staged in LDS by DMA: its vmem seq
     int32_t owner[512];
     uint64_t inflight[512];                         // vector-memory load into the register (seq) or 0
     uint64_t linflight[512];                        // LDS load into the register (lgkm seq) or 0
@@ -155,6 +156,7 @@ struct Allocator {
                 const int32_t s = lslot[w];
                 const int t = Reserved(o.n_vgpr).t1;
                 lds_res.erase(std::prev(lds_res.end()));
+                if (dma_seq[w]) { wait_seq(dma_seq[w]); dma_seq[w] = 0; }
                 const uint64_t q = issue_lgkm();
                 emit(MI_LDLD, t, -1, -1, -1, (uint32_t)s);
                 mp->st.ldld++;
@@ -236,6 +238,7 @@ struct Allocator {
     }
     void reload_into(uint32_t v, int r) {
         if (lslot[v] >= 0) {  // the LDS slot is released at once: LDS operations run in order
+            if (dma_seq[v]) { wait_seq(dma_seq[v]); dma_seq[v] = 0; }
             const uint64_t q = issue_lgkm();
             emit(MI_LDLD, r, -1, -1, -1, (uint32_t)lslot[v]);
             mp->st.ldld++;
@@ -254,6 +257,23 @@ struct Allocator {
         inflight[r] = q;
         pend_loads.push_back({q, r});
         owner[r] = (int32_t)v; reg[v] = (int16_t)r;
+    }
+    // source row v -> a free LDS slot by LDS-DMA (its data is valid once vmcnt covers the DMA)
+    bool issue_dma(uint32_t v) {
+        if (free_lslots.empty()) return false;
+        const int32_t s = free_lslots.back();
+        free_lslots.pop_back();
+        mp->n_lds_slots = std::max<uint32_t>(mp->n_lds_slots, (uint32_t)s + 1);
+        const uint64_t q = issue_vmem();
+        emit(MI_DMA, s, -1, -1, -1, ir.nodes[v].imm);
+        mp->st.dma++;
+        mp->st.ldsrc++;
+        dma_seq[v] = q;
+        lslot[v] = s;
+        lds_res.insert({nu(v), v});
+        reload_q.push({nu(v), v});
+        issued[v] = 1;
+        return true;
     }
     void issue_load(uint32_t v, int r) {
         const uint64_t q = issue_vmem();
@@ -304,13 +324,14 @@ struct Allocator {
         lslot.assign(nv, -1);
         for (int s = (int)o.n_lds - 1; s >= 0; --s) free_lslots.push_back(s);
         issued.assign(nv, 0);
+        dma_seq.assign(nv, 0);
         for (int r = 0; r < 512; ++r) { owner[r] = -1; inflight[r] = 0; linflight[r] = 0; pinned[r] = 0; last_accw[r] = -100; }
         for (int r = (int)o.n_vgpr - 1; r >= 0; --r) freeV.push_back(r);
         for (int r = REG_A0 + (int)o.n_agpr - 1; r >= REG_A0; --r) freeA.push_back(r);
         std::vector<uint32_t> loads;
         for (uint32_t i = 0; i < nv; ++i)
             if (ir.nodes[i].k == IR_LOAD) loads.push_back(i);
-        size_t lp = 0;
+        size_t lp = 0, dp = 0;
         mp->ins.clear();
         mp->n_slots = 0;
         mp->n_out = ir.n_out;
@@ -318,7 +339,15 @@ struct Allocator {
 
         for (uint32_t i = 0; i < nv && !failed; ++i) {
             cur = i;
-            // -- prefetch source rows
+            // -- stage source rows in LDS by DMA far ahead (no register held while in flight)
+            while (o.la_dma && dp < loads.size() && loads[dp] <= i + o.la_dma) {
+                const uint32_t v = loads[dp];
+                if (issued[v] || uses[v].empty()) { ++dp; continue; }
+                if (seq - retired >= o.max_vmem) break;
+                if (!issue_dma(v)) break;
+                ++dp;
+            }
+            // -- prefetch source rows into registers (rows not staged)
             while (lp < loads.size() && loads[lp] <= i + o.la_load) {
                 const uint32_t v = loads[lp];
                 if (issued[v]) { ++lp; continue; }
@@ -582,6 +611,16 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
                 std::snprintf(buf, sizeof buf, "buffer_load_dword %s, v%d, s[24:27], s%d offen%s", R(m.d), V_SRCOFF, q, pol.src.c_str()); line(buf);
                 break;
             }
+            case MI_DMA: {
+                if (diag & 4) break;
+                const int q = srot();
+                std::snprintf(buf, sizeof buf, "s_mul_i32 s%d, s12, %u", q, m.imm); line(buf);
+                std::snprintf(buf, sizeof buf, "s_mov_b32 m0, %u", (uint32_t)m.d * 256u); line(buf);
+                line("s_nop 0");
+                std::snprintf(buf, sizeof buf, "buffer_load_dword v%d, s[24:27], s%d offen%s lds", V_SRCOFF, q, pol.src.c_str());
+                line(buf);
+                break;
+            }
             case MI_STOUT: {
                 if (diag & 8) break;
                 const int q = srot();
@@ -663,6 +702,7 @@ bool emulate_colprog(const MProg& mp, const uint8_t* src, uint32_t T, uint8_t* o
     std::vector<std::vector<uint32_t>> scr(mp.n_slots, std::vector<uint32_t>(Td, 0));
     std::vector<uint64_t> pend(512, 0), slot_st(mp.n_slots, 0), lpend(512, 0);
     std::vector<std::vector<uint32_t>> lds(std::max<uint32_t>(mp.n_lds_slots, 1), std::vector<uint32_t>(Td, 0));
+    std::vector<uint64_t> lds_dma(std::max<uint32_t>(mp.n_lds_slots, 1), 0);  // pending DMA seq per slot
     uint64_t seq = 0, retired = 0, lseq = 0, lretired = 0;
     char buf[160];
     auto bad = [&](size_t i, const char* what) {
@@ -676,7 +716,7 @@ bool emulate_colprog(const MProg& mp, const uint8_t* src, uint32_t T, uint8_t* o
             return r < 0 || ((pend[r] == 0 || pend[r] <= retired) && (lpend[r] == 0 || lpend[r] <= lretired));
         };
         if (!ready(m.a) || !ready(m.b) || !ready(m.c)) return bad(i, "operand read before its load completed");
-        if (m.d >= 0 && !ready(m.d)) return bad(i, "register overwritten while a load into it is pending");
+        if (m.op != MI_DMA && m.d >= 0 && !ready(m.d)) return bad(i, "register overwritten while a load into it is pending");
         auto vmem = [&]() {
             ++seq;
             if (seq - retired > 63) return false;
@@ -736,17 +776,27 @@ bool emulate_colprog(const MProg& mp, const uint8_t* src, uint32_t T, uint8_t* o
                 break;
             case MI_LDST:
                 if (m.imm >= mp.n_lds_slots) return bad(i, "LDS slot out of range");
+                if (lds_dma[m.imm] > retired) return bad(i, "LDS write over a pending DMA");
                 lds[m.imm] = R[m.a];
                 if (++lseq - lretired > 15) return bad(i, "more than 15 LDS operations outstanding");
                 break;
             case MI_LDLD:
                 if (m.imm >= mp.n_lds_slots) return bad(i, "LDS slot out of range");
+                if (lds_dma[m.imm] > retired) return bad(i, "LDS read before its DMA completed");
                 R[m.d] = lds[m.imm];
                 if (++lseq - lretired > 15) return bad(i, "more than 15 LDS operations outstanding");
                 lpend[m.d] = lseq;
                 break;
             case MI_WAITL:
                 if (lseq > m.imm) lretired = std::max(lretired, lseq - m.imm);
+                break;
+            case MI_DMA:
+                if (m.imm >= mp.K) return bad(i, "source row >= K");
+                if (m.d < 0 || (uint32_t)m.d >= mp.n_lds_slots) return bad(i, "DMA slot out of range");
+                if (lds_dma[m.d] > retired) return bad(i, "DMA over a pending DMA");
+                std::memcpy(lds[m.d].data(), src + (size_t)m.imm * T, (size_t)Td * 4);
+                if (!vmem()) return bad(i, "more than 63 vector-memory operations outstanding");
+                lds_dma[m.d] = seq;
                 break;
         }
         if ((m.op == MI_XOR2 || m.op == MI_XOR3 || m.op == MI_XT || m.op == MI_XTX || m.op == MI_ZERO) &&

@@ -29,6 +29,7 @@ enum MOp : uint8_t {
     MI_LDST,    // LDS slot imm <- a (ds_write_b32)
     MI_LDLD,    // d <- LDS slot imm (ds_read_b32)
     MI_WAITL,   // s_waitcnt lgkmcnt(imm)
+    MI_DMA,     // LDS slot d <- source row imm (buffer_load ... lds: no register, counts in vmcnt)
 };
 
 constexpr int REG_A0 = 256;       // register ids: 0..255 VGPR, 256..511 AGPR
@@ -56,6 +57,7 @@ struct AllocOpts {
     uint32_t max_vmem = 56;      // outstanding vector-memory operations per wave
     uint32_t n_lds = 156;        // LDS spill slots per wave (256 B each; 4 waves/CU -> 40 KB; <= 512)
     uint32_t lds_horizon = 200;  // push an LDS resident out only if its next use is this much further
+    uint32_t la_dma = 0;         // look-ahead (IR nodes) for LDS-DMA source staging (0 = off)
 };
 
 struct MProg {
@@ -71,6 +73,7 @@ struct MProg {
         uint32_t sync_reload = 0;  // reloads that were not prefetched
         uint32_t ldst = 0, ldld = 0, waitl = 0;  // LDS spill stores / reloads / lgkm waits
         uint32_t migrate = 0;                    // LDS residents pushed out to global scratch
+        uint32_t dma = 0;                        // source rows staged through LDS by DMA
     } st;
 };
 

@@ -173,13 +173,14 @@ const AllocOpts& alloc_options() {
             unsigned v[6] = {0, 0, 0, 0, 0, 0};
             std::sscanf(e, "%u,%u,%u,%u,%u,%u", &v[0], &v[1], &v[2], &v[3], &v[4], &v[5]);
             if (v[5]) r.n_lds = std::min<uint32_t>(v[5] - 1, 512);
-            if (const char* h = std::getenv("RQHIP_LDS_HORIZON")) r.lds_horizon = (uint32_t)std::atoi(h);
             if (v[0]) r.n_vgpr = std::min<uint32_t>(v[0], V_ALLOC);
             if (v[1]) r.n_agpr = std::min<uint32_t>(v[1], 256);
             if (v[2]) r.la_load = v[2];
             if (v[3]) r.la_reload = v[3];
             if (v[4]) r.max_vmem = std::min<uint32_t>(v[4], 60);
         }
+        if (const char* h = std::getenv("RQHIP_LDS_HORIZON")) r.lds_horizon = (uint32_t)std::atoi(h);
+        if (const char* h = std::getenv("RQHIP_LA_DMA")) r.la_dma = (uint32_t)std::atoi(h);
         return r;
     }();
     return o;
