@@ -534,7 +534,16 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
         "s_load_dwordx8 s[4:11], s[0:1], 0x0",
         "s_load_dwordx8 s[12:19], s[0:1], 0x20",
         "s_waitcnt lgkmcnt(0)",
-        "s_lshl_b32 s20, s2, 6",
+        // XCD-aware wave order: workgroups are dealt to the 8 XCDs round-robin, so logical wave
+        // L = (w % 8) * q + w / 8 (for w < 8q; s17 = q, s18 = 8q, both 0 = identity) keeps the
+        // waves of one block, which share the 128-B lines at their 256-B segment edges, on one L2.
+        "s_and_b32 s39, s2, 7",
+        "s_mul_i32 s39, s39, s17",
+        "s_lshr_b32 s40, s2, 3",
+        "s_add_u32 s39, s39, s40",
+        "s_cmp_lt_u32 s2, s18",
+        "s_cselect_b32 s39, s39, s2",
+        "s_lshl_b32 s20, s39, 6",
         "v_add_u32_e32 v1, s20, v0",
         "v_cmp_gt_u32_e64 s[22:23], s13, v1",
         "s_and_b64 exec, exec, s[22:23]",

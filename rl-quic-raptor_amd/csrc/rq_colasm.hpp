@@ -90,7 +90,8 @@ struct ColKernArgs {
     uint32_t n_cols;      // n_blocks * T/4
     uint32_t magic, shift;  // b = mulhi(g, magic) >> shift == g / (T/4) for g < n_cols
     uint32_t scr_per_wave;  // bytes
-    uint32_t pad[3];
+    uint32_t xcd_q, xcd_n;  // XCD-aware wave order: q = waves / 8, n = 8q (0, 0 = identity order)
+    uint32_t pad;
 };
 static_assert(sizeof(ColKernArgs) == 64, "kernarg layout");
 

@@ -227,6 +227,15 @@ int get_col_kernel(DevCtx* ctx, const Params& p, const uint32_t* esi, uint32_t n
     return RQ_OK;
 }
 
+// XCD-aware wave order in column programs (RQHIP_XCD=0 disables it for experiments).
+bool xcd_order() {
+    static const bool on = [] {
+        const char* e = std::getenv("RQHIP_XCD");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 // Run a column program over n_blocks device-resident blocks.  Caller holds ctx->mu.
 int launch_col(DevCtx* ctx, ColKernel* k, uint32_t T, uint32_t n_blocks, const void* src, uint64_t src_stride,
                void* out, uint64_t out_stride, void* stream) {
@@ -261,6 +270,10 @@ int launch_col(DevCtx* ctx, ColKernel* k, uint32_t T, uint32_t n_blocks, const v
         size_t sz = sizeof a;
         void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
         const uint32_t waves = (a.n_cols + 63) / 64;
+        if (xcd_order()) {
+            a.xcd_q = waves / 8;
+            a.xcd_n = a.xcd_q * 8;
+        }
         HIP_TRY(hipModuleLaunchKernel(k->fn, waves, 1, 1, 64, 1, 1, 0, (hipStream_t)stream, nullptr, cfg));
     }
     return RQ_OK;
