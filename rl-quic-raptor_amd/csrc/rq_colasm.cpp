@@ -510,6 +510,11 @@ static uint32_t diag_mask() {
     return e ? (uint32_t)std::atoi(e) : 0u;
 }
 
+uint32_t colprog_regs(const MProg& mp) {
+    const uint32_t acc_off = (mp.n_vgpr + N_RESERVED + 3) & ~3u;
+    return (acc_off + std::max<uint32_t>(mp.n_agpr, 1) + 7) & ~7u;
+}
+
 std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
     static const Policy pol;
     static const uint32_t diag = diag_mask();
@@ -530,33 +535,15 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
     auto line = [&](const char* t) { s += '\t'; s += t; s += '\n'; };
     s += "\t.amdgcn_target \"amdgcn-amd-amdhsa--gfx950\"\n\t.amdhsa_code_object_version 6\n\t.text\n";
     s += "\t.globl " + kname + "\n\t.p2align 8\n\t.type " + kname + ",@function\n" + kname + ":\n";
-    const char* pro[] = {
+    // Persistent loop: the grid holds as many waves as can be resident (the host sets n_wg = s49);
+    // wave w processes items w, w + n_wg, ... < n_items (s48), so its scratch lines are reused by
+    // its own next item instead of a fresh wave's, and the scratch footprint stays at the
+    // resident set.  One item = 64 dword columns (the lane -> (block, column) map below).
+    const char* pro_once[] = {
         "s_load_dwordx8 s[4:11], s[0:1], 0x0",
         "s_load_dwordx8 s[12:19], s[0:1], 0x20",
+        "s_load_dwordx2 s[48:49], s[0:1], 0x40",
         "s_waitcnt lgkmcnt(0)",
-        // XCD-aware wave order: workgroups are dealt to the 8 XCDs round-robin, so logical wave
-        // L = (w % 8) * q + w / 8 (for w < 8q; s17 = q, s18 = 8q, both 0 = identity) keeps the
-        // waves of one block, which share the 128-B lines at their 256-B segment edges, on one L2.
-        "s_and_b32 s39, s2, 7",
-        "s_mul_i32 s39, s39, s17",
-        "s_lshr_b32 s40, s2, 3",
-        "s_add_u32 s39, s39, s40",
-        "s_cmp_lt_u32 s2, s18",
-        "s_cselect_b32 s39, s39, s2",
-        "s_lshl_b32 s20, s39, 6",
-        "v_add_u32_e32 v1, s20, v0",
-        "v_cmp_gt_u32_e64 s[22:23], s13, v1",
-        "s_and_b64 exec, exec, s[22:23]",
-        "v_mul_hi_u32 v2, v1, s14",
-        "v_lshrrev_b32_e32 v2, s15, v2",
-        "s_lshr_b32 s21, s12, 2",
-        "v_mul_lo_u32 v3, v2, s21",
-        "v_sub_u32_e32 v3, v1, v3",
-        "v_lshlrev_b32_e32 v3, 2, v3",
-        "v_mul_lo_u32 v4, v2, s10",
-        "v_add_u32_e32 V_SRCOFF, v4, v3",
-        "v_mul_lo_u32 v4, v2, s11",
-        "v_add_u32_e32 V_OUTOFF, v4, v3",
         "v_lshlrev_b32_e32 V_SCROFF, 2, v0",
         "v_add_u32_e32 V_LDS2, 0x10000, V_SCROFF",
         "s_mov_b32 s24, s4",
@@ -577,8 +564,38 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
         "s_mov_b32 s36, 0x090b080a",
         "s_mov_b32 s37, 0xfefefefe",
         "s_mov_b32 s38, 0x1d1d1d1d",
+        "s_mov_b32 s52, s2",
     };
-    for (const char* p : pro) {
+    const char* pro_iter[] = {
+        "s_cmp_ge_u32 s52, s48",
+        "s_cbranch_scc1 .Lend",
+        "s_mov_b64 exec, -1",
+        // XCD-aware item order: workgroups are dealt to the 8 XCDs round-robin, so logical item
+        // L = (w % 8) * q + w / 8 (for w < 8q; s17 = q, s18 = 8q, both 0 = identity) keeps the
+        // items of one block, which share the 128-B lines at their 256-B segment edges, on one L2.
+        "s_and_b32 s39, s52, 7",
+        "s_mul_i32 s39, s39, s17",
+        "s_lshr_b32 s40, s52, 3",
+        "s_add_u32 s39, s39, s40",
+        "s_cmp_lt_u32 s52, s18",
+        "s_cselect_b32 s39, s39, s52",
+        "s_lshl_b32 s20, s39, 6",
+        "v_lshrrev_b32_e32 v0, 2, V_SCROFF",
+        "v_add_u32_e32 v1, s20, v0",
+        "v_cmp_gt_u32_e64 s[22:23], s13, v1",
+        "s_and_b64 exec, exec, s[22:23]",
+        "v_mul_hi_u32 v2, v1, s14",
+        "v_lshrrev_b32_e32 v2, s15, v2",
+        "s_lshr_b32 s21, s12, 2",
+        "v_mul_lo_u32 v3, v2, s21",
+        "v_sub_u32_e32 v3, v1, v3",
+        "v_lshlrev_b32_e32 v3, 2, v3",
+        "v_mul_lo_u32 v4, v2, s10",
+        "v_add_u32_e32 V_SRCOFF, v4, v3",
+        "v_mul_lo_u32 v4, v2, s11",
+        "v_add_u32_e32 V_OUTOFF, v4, v3",
+    };
+    auto put = [&](const char* p) {
         std::string l(p);
         const std::pair<const char*, int> names[] = {
             {"V_SRCOFF", V_SRCOFF}, {"V_OUTOFF", V_OUTOFF}, {"V_SCROFF", V_SCROFF}, {"V_LDS2", rv.lds2}};
@@ -586,7 +603,10 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
             for (size_t at = l.find(nm.first); at != std::string::npos; at = l.find(nm.first))
                 l.replace(at, std::strlen(nm.first), "v" + std::to_string(nm.second));
         line(l.c_str());
-    }
+    };
+    for (const char* p : pro_once) put(p);
+    s += ".Lloop:\n";
+    for (const char* p : pro_iter) put(p);
     int sr = 0;
     auto srot = [&]() { sr = (sr + 1) & 7; return 40 + sr; };
     for (const MInst& m : mp.ins) {
@@ -675,21 +695,24 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
                 std::snprintf(buf, sizeof buf, "s_waitcnt lgkmcnt(%u)", m.imm); line(buf); break;
         }
     }
+    line("s_waitcnt vmcnt(0) lgkmcnt(0)");
+    line("s_add_u32 s52, s52, s49");
+    line("s_branch .Lloop");
     s += ".Lend:\n\ts_endpgm\n";
     s += ".Lfunc_end:\n\t.size " + kname + ", .Lfunc_end-" + kname + "\n";
     s += "\t.p2alignl 6, 3212836864\n\t.fill 256, 4, 3212836864\n";
     s += "\t.section .rodata,\"a\",@progbits\n\t.p2align 6, 0x0\n\t.amdhsa_kernel " + kname + "\n";
     const std::string lds = std::to_string(mp.n_lds_slots * 256u);
     s += "\t\t.amdhsa_group_segment_fixed_size " + lds + "\n\t\t.amdhsa_private_segment_fixed_size 0\n";
-    s += "\t\t.amdhsa_kernarg_size 64\n\t\t.amdhsa_user_sgpr_count 2\n";
+    s += "\t\t.amdhsa_kernarg_size 80\n\t\t.amdhsa_user_sgpr_count 2\n";
     s += "\t\t.amdhsa_user_sgpr_kernarg_segment_ptr 1\n\t\t.amdhsa_system_sgpr_workgroup_id_x 1\n";
     s += "\t\t.amdhsa_system_vgpr_workitem_id 0\n\t\t.amdhsa_next_free_vgpr " + std::to_string(n_regs) + "\n";
     s += "\t\t.amdhsa_next_free_sgpr 56\n\t\t.amdhsa_accum_offset " + std::to_string(acc_off) +
          "\n\t\t.amdhsa_reserve_vcc 0\n";
     s += "\t\t.amdhsa_ieee_mode 0\n\t\t.amdhsa_dx10_clamp 0\n\t.end_amdhsa_kernel\n\t.text\n";
     s += "\t.amdgpu_metadata\n---\namdhsa.kernels:\n  - .agpr_count: " + std::to_string(n_regs - acc_off) + "\n    .args:\n";
-    s += "      - .offset: 0\n        .size: 64\n        .value_kind: by_value\n";
-    s += "    .group_segment_fixed_size: " + lds + "\n    .kernarg_segment_align: 8\n    .kernarg_segment_size: 64\n";
+    s += "      - .offset: 0\n        .size: 80\n        .value_kind: by_value\n";
+    s += "    .group_segment_fixed_size: " + lds + "\n    .kernarg_segment_align: 8\n    .kernarg_segment_size: 80\n";
     s += "    .max_flat_workgroup_size: 64\n    .name: " + kname + "\n    .private_segment_fixed_size: 0\n";
     s += "    .sgpr_count: 56\n    .symbol: " + kname + ".kd\n    .vgpr_count: " + std::to_string(n_regs) +
          "\n    .wavefront_size: 64\n";

@@ -90,12 +90,17 @@ struct ColKernArgs {
     uint32_t n_cols;      // n_blocks * T/4
     uint32_t magic, shift;  // b = mulhi(g, magic) >> shift == g / (T/4) for g < n_cols
     uint32_t scr_per_wave;  // bytes
-    uint32_t xcd_q, xcd_n;  // XCD-aware wave order: q = waves / 8, n = 8q (0, 0 = identity order)
+    uint32_t xcd_q, xcd_n;  // XCD-aware item order: q = items / 8, n = 8q (0, 0 = identity order)
     uint32_t pad;
+    uint32_t n_items;     // 64-column items (waves' worth of work) in this launch
+    uint32_t n_wg;        // persistent grid size: wave w takes items w, w + n_wg, ...
+    uint32_t pad2[2];
 };
-static_assert(sizeof(ColKernArgs) == 64, "kernarg layout");
+static_assert(sizeof(ColKernArgs) == 80, "kernarg layout");
 
 std::string emit_colprog_asm(const MProg& mp, const std::string& kname);
+// Registers (VGPR + AGPR, allocation granule 8) per lane of the emitted kernel.
+uint32_t colprog_regs(const MProg& mp);
 
 // Executes the machine program on the host for one block (T/4 lanes), checking vmcnt waits and
 // scratch ordering as it goes.  Test infrastructure for the allocator, not a product path.

@@ -70,6 +70,7 @@ struct ColKernel {
     Params p{};
     std::vector<uint32_t> esi;     // outputs (empty: all L intermediate symbols)
     uint32_t n_out = 0, n_slots = 0, n_ins = 0;
+    uint32_t waves_per_cu = 4;     // residency of the code object (registers, LDS)
     MProg::Stats st{};
     DevBuf mrep;                   // decode: outputs on the identity payload
     uint32_t mrep_stride = 0;
@@ -102,6 +103,7 @@ struct Workspace {
 
 struct DevCtx {
     int device = -1;
+    uint32_t n_cu = 256;
     std::mutex mu;
     bool tables = false;
     std::map<std::string, std::unique_ptr<ColKernel>> colk;  // keyed by (K', K, outputs)
@@ -138,6 +140,9 @@ int get_ctx(DevCtx** out) {
     if (!c) {
         c.reset(new DevCtx());
         c->device = dev;
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
+            c->n_cu = (uint32_t)cus;
     }
     *out = c.get();
     return RQ_OK;
@@ -219,6 +224,12 @@ int get_col_kernel(DevCtx* ctx, const Params& p, const uint32_t* esi, uint32_t n
         }
         k->n_out = ir.n_out;
         k->n_slots = mp.n_slots;
+        {
+            const uint32_t regs = colprog_regs(mp), lds = mp.n_lds_slots * 256u;
+            uint32_t w = 4 * std::max<uint32_t>(1, 512 / regs);
+            if (lds) w = std::min<uint32_t>(w, 163840u / lds);
+            k->waves_per_cu = std::max<uint32_t>(1, std::min<uint32_t>(w, 32));
+        }
         k->st = mp.st;
         k->n_ins = (uint32_t)mp.ins.size();
         slot = std::move(k);
@@ -249,11 +260,14 @@ int launch_col(DevCtx* ctx, ColKernel* k, uint32_t T, uint32_t n_blocks, const v
     if ((uint64_t)per * src_stride > lim || (uint64_t)per * out_stride > lim)
         return fail(RQ_ERR_UNSUPPORTED, "block stride beyond the 4 GiB buffer-offset range");
     if ((uint64_t)per * Td > 0x7FFFFFFFull) return fail(RQ_ERR_UNSUPPORTED, "batch too large");
-    const uint32_t max_waves = (uint32_t)(((uint64_t)per * Td + 63) / 64);
+    const uint32_t max_items = (uint32_t)(((uint64_t)per * Td + 63) / 64);
+    // persistent grid: at most the resident wave count (scratch is per grid wave)
+    const uint32_t resident = ctx->n_cu * k->waves_per_cu;
+    const uint32_t max_wg = std::min(max_items, resident);
     const size_t spw = (size_t)std::max<uint32_t>(k->n_slots, 1) * 256;
     int rc;
     Workspace* w = ctx->wsp(stream);
-    if ((rc = w->scratch.ensure(spw * max_waves))) return rc;
+    if ((rc = w->scratch.ensure(spw * max_wg))) return rc;
     for (uint32_t b0 = 0; b0 < n_blocks; b0 += per) {
         const uint32_t nb = std::min(per, n_blocks - b0);
         ColKernArgs a;
@@ -269,9 +283,12 @@ int launch_col(DevCtx* ctx, ColKernel* k, uint32_t T, uint32_t n_blocks, const v
         if (!divmagic(Td, a.n_cols, &a.magic, &a.shift)) return fail(RQ_ERR_UNSUPPORTED, "no division magic");
         size_t sz = sizeof a;
         void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
-        const uint32_t waves = (a.n_cols + 63) / 64;
-        if (xcd_order()) {
-            a.xcd_q = waves / 8;
+        const uint32_t items = (a.n_cols + 63) / 64;
+        const uint32_t waves = std::min(items, resident);
+        a.n_items = items;
+        a.n_wg = waves;
+        if (xcd_order() && waves % 8 == 0) {  // the remap needs the stride to keep w % 8 fixed
+            a.xcd_q = items / 8;
             a.xcd_n = a.xcd_q * 8;
         }
         HIP_TRY(hipModuleLaunchKernel(k->fn, waves, 1, 1, 64, 1, 1, 0, (hipStream_t)stream, nullptr, cfg));
