@@ -567,8 +567,11 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
         "s_mov_b32 s52, s2",
     };
     const char* pro_iter[] = {
-        "s_cmp_ge_u32 s52, s48",
-        "s_cbranch_scc1 .Lend",
+        // (the program is longer than a 16-bit branch reaches: exit in place, loop back by s_setpc)
+        "s_cmp_lt_u32 s52, s48",
+        "s_cbranch_scc1 .Lbody",
+        "s_endpgm",
+        ".Lbody:",
         "s_mov_b64 exec, -1",
         // XCD-aware item order: workgroups are dealt to the 8 XCDs round-robin, so logical item
         // L = (w % 8) * q + w / 8 (for w < 8q; s17 = q, s18 = 8q, both 0 = identity) keeps the
@@ -697,7 +700,11 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
     }
     line("s_waitcnt vmcnt(0) lgkmcnt(0)");
     line("s_add_u32 s52, s52, s49");
-    line("s_branch .Lloop");
+    line("s_getpc_b64 s[54:55]");
+    s += ".Lpc:\n";
+    line("s_sub_u32 s54, s54, .Lpc-.Lloop");
+    line("s_subb_u32 s55, s55, 0");
+    line("s_setpc_b64 s[54:55]");
     s += ".Lend:\n\ts_endpgm\n";
     s += ".Lfunc_end:\n\t.size " + kname + ", .Lfunc_end-" + kname + "\n";
     s += "\t.p2alignl 6, 3212836864\n\t.fill 256, 4, 3212836864\n";

@@ -98,7 +98,7 @@ def test_intermediate_symbols_mode(rq, oracle, K, T):
 SCALAR_ALLOWED = {"s_add_u32", "s_addc_u32", "s_and_b32", "s_and_b64", "s_endpgm", "s_load_dwordx8",
                   "s_lshl_b32", "s_lshr_b32", "s_mov_b32", "s_mul_hi_u32", "s_mul_i32", "s_nop",
                   "s_waitcnt", "s_cmp_ge_u32", "s_cbranch_scc1", "s_mov_b64", "s_cmp_lt_u32",
-                  "s_cselect_b32", "s_branch", "s_load_dwordx2"}
+                  "s_cselect_b32", "s_load_dwordx2", "s_getpc_b64", "s_sub_u32", "s_subb_u32", "s_setpc_b64"}
 
 
 def test_program_size_and_assembly(rq):
@@ -112,3 +112,5 @@ def test_program_size_and_assembly(rq):
     scalar_ops = set(re.findall(r"^\s*(s_[a-z0-9_]+)", asm, re.M))
     assert scalar_ops <= SCALAR_ALLOWED, scalar_ops - SCALAR_ALLOWED
     assert rq.colprog_assemble(64, list(range(64, 80))) > 1000
+    # a full-size program (>128 KiB of code: the loop back-edge must not be a 16-bit branch)
+    assert rq.colprog_assemble(1024, list(range(1024, 1100))) > 131072
