@@ -2,8 +2,9 @@
 
 1. Calibration: the column program with outputs = the K=10 source rows themselves (ESIs 0..9) is a
    pure copy in the encode kernel's own access pattern (4-byte-per-lane buffer loads and stores of
-   256-B row segments): it reads and writes exactly blocks*10*T bytes, so FETCH_SIZE / WRITE_SIZE of
-   that launch calibrate the counters for this pattern (rq_colprog_K10_n10).
+   256-B row segments).  At T=1024 every segment is whole 128-B lines that no other wave touches, so
+   it reads and writes exactly blocks*10*T bytes and FETCH_SIZE / WRITE_SIZE of that launch calibrate
+   the counters for this access width (rq_colprog_K10_n10).
 2. The bench workload's encode launch: K=1024 T=1200 N=1100, 1024 blocks (rq_colprog_K1024_n76).
 """
 import sys
@@ -18,22 +19,22 @@ import rqhip  # noqa: E402
 
 def main():
     dev = torch.device("cuda:0")
-    T = 1200
-    Bc = 65536
-    src = torch.randint(0, 256, (Bc, 10 * T), dtype=torch.uint8, device=dev)
+    Tc, Bc = 1024, 65536
+    src = torch.randint(0, 256, (Bc, 10 * Tc), dtype=torch.uint8, device=dev)
     out = torch.empty_like(src)
     for _ in range(3):
-        rqhip.encode_batch(src, 10, T, list(range(10)), out)
+        rqhip.encode_batch(src, 10, Tc, list(range(10)), out)
     torch.cuda.synchronize()
     assert torch.equal(src, out)
     del src, out
+    T = 1200
     K, N, B = 1024, 1100, 1024
     src = torch.randint(0, 256, (B, K * T), dtype=torch.uint8, device=dev)
     rep = torch.empty((B, (N - K) * T), dtype=torch.uint8, device=dev)
     for _ in range(3):
         rqhip.encode_batch(src, K, T, list(range(K, N)), rep)
     torch.cuda.synchronize()
-    print("calibration bytes per launch", Bc * 10 * T, "encode source bytes per launch", B * K * T)
+    print("calibration bytes per launch", Bc * 10 * Tc, "encode source bytes per launch", B * K * T)
 
 
 if __name__ == "__main__":

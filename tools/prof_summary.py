@@ -41,7 +41,7 @@ def counter_means(path):
 def traffic(d, tag):
     fetch = counter_means(glob.glob(os.path.join(d, "fetch", "*counter_collection.csv"))[0])
     write = counter_means(glob.glob(os.path.join(d, "write", "*counter_collection.csv"))[0])
-    cal_bytes = 65536 * 10 * 1200
+    cal_bytes = 65536 * 10 * 1024
     cal, enc = "rq_colprog_K10_n10", "rq_colprog_K1024_n76"
     f_cal, w_cal = fetch[(cal, "FETCH_SIZE")] / cal_bytes, write[(cal, "WRITE_SIZE")] / cal_bytes
     f_enc, w_enc = fetch[(enc, "FETCH_SIZE")] / f_cal, write[(enc, "WRITE_SIZE")] / w_cal
