@@ -305,19 +305,45 @@ int launch_solve(const SolveArgs& a, uint32_t n_blocks, uint32_t lds_bytes, bool
 }
 
 // ------------------------------ decode: x_E = X * s ------------------------------------------
-// grid = (strips of 64 dwords, solved blocks), one wave.  s_m = recv_{piv m} ^ r0_{piv m} (the
-// syndrome, formed on the fly).  GF(256) by bit decomposition: the eight multiples alpha^b s_m are
-// built by xtime, and output k takes those its coefficient X[k][m] selects.  X[k][m] is uniform
-// (scalar loads), so a selection is one s_bfe_i32 mask and one v_bitop3 per bit.
-// Each lane owns CPL dword columns (64 apart, so every load/store instruction stays one contiguous
-// 256-B segment): the scalar mask of a coefficient bit (one s_bfe_i32 -- the scalar unit issues one
-// instruction per cycle per CU and bounds the one-column form) is shared by CPL v_bitop3 ops.  CPL
-// is chosen per T to minimise padded columns (T = 1200: 300 dwords = one wave of 5 x 64, 94 % live).
-// Outputs are split into balanced slices of KC <= 32, one wave per (strip, slice, block): enough
-// waves for two per SIMD (the VALU then issues every 2 cycles instead of 4).
+// GF(256) multiply by a uniform constant c with v_perm_b32 as an 8-entry byte lookup on four bytes
+// at once: x = x0 + 8*x1 + 64*x2 (3 + 3 + 2 bits), c*x = c*x0 ^ c*(8*x1) ^ c*(64*x2), so three
+// v_perm (selectors x & 7, (x >> 3) & 7, x >> 6 per byte) against per-coefficient tables and two
+// XORs per dword: 5 VALU per mul-add instead of 8 bit-selects (replaces asmSSSE3MulAdd's nibble
+// pshufb, RQ/discmath/optimizations.s:36-78, with CDNA4's byte permute).
+
+// Tables for every coefficient of every solved block: 5 dwords per (m, k), k fastest.
+__global__ void __launch_bounds__(256) k_xtab(ApplyArgs a) {
+    __shared__ uint8_t ex[512], lg[256];
+    const uint32_t bi = blockIdx.x, b = a.blk_map[bi];
+    if (a.status[b] != 1) return;
+    gf_tables(ex, lg);
+    __syncthreads();
+    const uint32_t e = a.erased_off[b + 1] - a.erased_off[b];
+    const uint8_t* xc = a.xcoef + (size_t)bi * a.max_e * a.xc_stride;
+    uint32_t* xt = a.xtab + (size_t)bi * a.max_e * a.xc_stride * 5;
+    for (uint32_t idx = threadIdx.x; idx < e * e; idx += blockDim.x) {
+        const uint32_t m = idx / e, k = idx - m * e;
+        const uint8_t c = xc[m * a.xc_stride + k];
+        uint32_t t[5];
+        for (int w = 0; w < 5; ++w) {
+            uint32_t v = 0;
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t x = w < 2 ? (uint32_t)(w * 4 + i) : w < 4 ? (uint32_t)((w - 2) * 4 + i) * 8 : (uint32_t)i * 64;
+                v |= (uint32_t)gmul_t(lg, ex, c, (uint8_t)x) << (8 * i);
+            }
+            t[w] = v;
+        }
+        uint32_t* d = xt + ((size_t)m * a.xc_stride + k) * 5;
+        for (int w = 0; w < 5; ++w) d[w] = t[w];
+    }
+}
+
+// grid.x = solved block * strips + strip, grid.y = output slice of KC.  Each lane owns CPL dword
+// columns (64 apart: every load/store instruction is one contiguous 256-B segment).  The slice's
+// tables for all m are staged in LDS: A = the four 8-entry halves (b128), B = the 2-bit table.
 template <int KC, int CPL>
 __global__ void __launch_bounds__(64) k_apply(ApplyArgs a) {
-    // grid.x = solved block * strips + strip, grid.y = output slice
+    extern __shared__ __attribute__((aligned(16))) uint32_t xsh[];
     const uint32_t strips = ((a.T >> 2) + 64 * CPL - 1) / (64 * CPL);
     const uint32_t bi = blockIdx.x / strips, strip = blockIdx.x - bi * strips;
     const uint32_t b = a.blk_map[bi];
@@ -328,12 +354,33 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a) {
     if (k0 >= e) return;
     const uint32_t Td = a.T >> 2;
     const uint32_t* E = a.erased + a.erased_off[b];
-    const uint8_t* xc = a.xcoef + (size_t)bi * a.max_e * a.xc_stride;
     const uint16_t* XP = a.xpiv + (size_t)bi * a.max_e;
     const uint32_t r0b = a.rep_off[b];
     const uint32_t* recv = reinterpret_cast<const uint32_t*>(a.recv);
     const uint32_t* r0 = reinterpret_cast<const uint32_t*>(a.r0) + (size_t)b * a.n_union * Td;
     uint8_t* blk = a.data + (size_t)b * a.data_stride;
+    uint4* tA = reinterpret_cast<uint4*>(xsh);                  // [m][KC]
+    uint32_t* tB = xsh + (size_t)e * KC * 4;                     // [m][KC]
+    uint32_t* offr = tB + (size_t)e * KC;
+    uint32_t* off0 = offr + e;
+    const uint32_t* xt = a.xtab + (size_t)bi * a.max_e * a.xc_stride * 5;
+    for (uint32_t idx = lane; idx < e * KC; idx += 64) {
+        const uint32_t m = idx / KC, k = idx - m * KC;
+        if (k0 + k < e) {
+            const uint32_t* src = xt + ((size_t)m * a.xc_stride + k0 + k) * 5;
+            tA[idx] = make_uint4(src[0], src[1], src[2], src[3]);
+            tB[idx] = src[4];
+        } else {
+            tA[idx] = make_uint4(0, 0, 0, 0);
+            tB[idx] = 0;
+        }
+    }
+    for (uint32_t m = lane; m < e; m += 64) {
+        const uint32_t j = r0b + XP[m];
+        offr[m] = j * Td;
+        off0[m] = a.rep_uidx[j] * Td;
+    }
+    __syncthreads();
     uint32_t col[CPL];
     bool live[CPL];
 #pragma unroll
@@ -342,115 +389,95 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a) {
         live[j] = c < Td;
         col[j] = live[j] ? c : 0;
     }
-    // dword offsets of the syndrome operands of every m (received row, r0 row), staged once
-    __shared__ uint32_t offr[256], off0[256];
-    for (uint32_t m = lane; m < e; m += 64) {
-        const uint32_t j = r0b + XP[m];
-        offr[m] = j * Td;
-        off0[m] = a.rep_uidx[j] * Td;
-    }
-    __syncthreads();
-    {
-        uint32_t acc[KC][CPL];
+    uint32_t acc[KC][CPL];
 #pragma unroll
-        for (int k = 0; k < KC; ++k)
+    for (int k = 0; k < KC; ++k)
 #pragma unroll
-            for (int j = 0; j < CPL; ++j) acc[k][j] = 0;
-        uint32_t s_next[CPL];
+        for (int j = 0; j < CPL; ++j) acc[k][j] = 0;
+    uint32_t s_next[CPL];
 #pragma unroll
-        for (int j = 0; j < CPL; ++j) s_next[j] = recv[(size_t)offr[0] + col[j]] ^ r0[(size_t)off0[0] + col[j]];
-        // coefficient bytes X[k0..k0+KC)[m] (uniform): loaded one m ahead
-        uint32_t w_next[KC / 4];
-        {
-            const uint32_t* cw = reinterpret_cast<const uint32_t*>(xc + k0);
+    for (int j = 0; j < CPL; ++j) s_next[j] = recv[(size_t)offr[0] + col[j]] ^ r0[(size_t)off0[0] + col[j]];
+    for (uint32_t m = 0; m < e; ++m) {
+        uint32_t s0[CPL], s1[CPL], s2[CPL];
 #pragma unroll
-            for (int kw = 0; kw < KC / 4; ++kw) w_next[kw] = __builtin_amdgcn_readfirstlane((int)cw[kw]);
+        for (int j = 0; j < CPL; ++j) {
+            const uint32_t x = s_next[j];
+            s0[j] = x & 0x07070707u;
+            s1[j] = (x >> 3) & 0x07070707u;
+            s2[j] = (x >> 6) & 0x03030303u;
         }
-        for (uint32_t m = 0; m < e; ++m) {
-            uint32_t wcur[KC / 4];
+        if (m + 1 < e) {  // prefetch the next syndrome while this one is applied
 #pragma unroll
-            for (int kw = 0; kw < KC / 4; ++kw) wcur[kw] = w_next[kw];
-            if (m + 1 < e) {
-                const uint32_t* cw = reinterpret_cast<const uint32_t*>(xc + (size_t)(m + 1) * a.xc_stride + k0);
-#pragma unroll
-                for (int kw = 0; kw < KC / 4; ++kw) w_next[kw] = __builtin_amdgcn_readfirstlane((int)cw[kw]);
-            }
-            uint32_t mul[8][CPL];
-#pragma unroll
-            for (int j = 0; j < CPL; ++j) {
-                uint32_t s = s_next[j];
-#pragma unroll
-                for (int bt = 0; bt < 8; ++bt) {
-                    mul[bt][j] = s;
-                    s = xtime4(s);
-                }
-            }
-            if (m + 1 < e) {  // prefetch the next syndrome while this one is applied
-#pragma unroll
-                for (int j = 0; j < CPL; ++j)
-                    s_next[j] = recv[(size_t)offr[m + 1] + col[j]] ^ r0[(size_t)off0[m + 1] + col[j]];
-            }
-#pragma unroll
-            for (int kw = 0; kw < KC / 4; ++kw) {
-                const int w = (int)wcur[kw];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-#pragma unroll
-                    for (int bt = 0; bt < 8; ++bt) {
-                        const int msk = __builtin_amdgcn_sbfe(w, q * 8 + bt, 1);
-#pragma unroll
-                        for (int j = 0; j < CPL; ++j)
-                            // acc ^= mul & msk  (v_bitop3: src0 acc 0xF0, src1 mul 0xCC, src2 msk 0xAA)
-                            asm("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x78"
-                                : "+v"(acc[kw * 4 + q][j])
-                                : "v"(mul[bt][j]), "s"(msk));
-                    }
-                }
-            }
+            for (int j = 0; j < CPL; ++j)
+                s_next[j] = recv[(size_t)offr[m + 1] + col[j]] ^ r0[(size_t)off0[m + 1] + col[j]];
         }
-        const uint32_t kn = min((uint32_t)KC, e - k0);
 #pragma unroll
         for (int k = 0; k < KC; ++k) {
-            if ((uint32_t)k < kn) {
-                uint32_t* row = reinterpret_cast<uint32_t*>(blk + (size_t)E[k0 + k] * a.T);
+            const uint4 A = tA[m * KC + k];
+            const uint32_t B = tB[m * KC + k];
 #pragma unroll
-                for (int j = 0; j < CPL; ++j)
-                    if (live[j]) row[col[j]] = acc[k][j];
+            for (int j = 0; j < CPL; ++j) {
+                const uint32_t p0 = __builtin_amdgcn_perm(A.y, A.x, s0[j]);
+                const uint32_t p1 = __builtin_amdgcn_perm(A.w, A.z, s1[j]);
+                const uint32_t p2 = __builtin_amdgcn_perm(B, B, s2[j]);
+                acc[k][j] ^= p0 ^ p1 ^ p2;
             }
+        }
+    }
+    const uint32_t kn = min((uint32_t)KC, e - k0);
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+        if ((uint32_t)k < kn) {
+            uint32_t* row = reinterpret_cast<uint32_t*>(blk + (size_t)E[k0 + k] * a.T);
+#pragma unroll
+            for (int j = 0; j < CPL; ++j)
+                if (live[j]) row[col[j]] = acc[k][j];
         }
     }
 }
 
 template <int CPL>
-static void launch_apply_cpl(const ApplyArgs& a, uint32_t kc, dim3 g, hipStream_t st) {
+static void launch_apply_cpl(const ApplyArgs& a, uint32_t kc, dim3 g, size_t lds, hipStream_t st) {
     switch (kc) {
-        case 4: hipLaunchKernelGGL((k_apply<4, CPL>), g, dim3(64), 0, st, a); break;
-        case 8: hipLaunchKernelGGL((k_apply<8, CPL>), g, dim3(64), 0, st, a); break;
-        case 12: hipLaunchKernelGGL((k_apply<12, CPL>), g, dim3(64), 0, st, a); break;
-        case 16: hipLaunchKernelGGL((k_apply<16, CPL>), g, dim3(64), 0, st, a); break;
-        case 20: hipLaunchKernelGGL((k_apply<20, CPL>), g, dim3(64), 0, st, a); break;
-        case 24: hipLaunchKernelGGL((k_apply<24, CPL>), g, dim3(64), 0, st, a); break;
-        case 28: hipLaunchKernelGGL((k_apply<28, CPL>), g, dim3(64), 0, st, a); break;
-        default: hipLaunchKernelGGL((k_apply<32, CPL>), g, dim3(64), 0, st, a); break;
+        case 4: hipLaunchKernelGGL((k_apply<4, CPL>), g, dim3(64), lds, st, a); break;
+        case 8: hipLaunchKernelGGL((k_apply<8, CPL>), g, dim3(64), lds, st, a); break;
+        case 12: hipLaunchKernelGGL((k_apply<12, CPL>), g, dim3(64), lds, st, a); break;
+        case 16: hipLaunchKernelGGL((k_apply<16, CPL>), g, dim3(64), lds, st, a); break;
+        case 20: hipLaunchKernelGGL((k_apply<20, CPL>), g, dim3(64), lds, st, a); break;
+        case 24: hipLaunchKernelGGL((k_apply<24, CPL>), g, dim3(64), lds, st, a); break;
+        case 28: hipLaunchKernelGGL((k_apply<28, CPL>), g, dim3(64), lds, st, a); break;
+        default: hipLaunchKernelGGL((k_apply<32, CPL>), g, dim3(64), lds, st, a); break;
     }
 }
 
 int launch_apply(const ApplyArgs& a, uint32_t /*n_strips*/, uint32_t n_blocks, void* stream) {
+    const hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_xtab, dim3(n_blocks), dim3(256), 0, st, a);
     const uint32_t Td = a.T / 4;
     uint32_t cpl = 1, best = 0xFFFFFFFFu;  // fewest padded columns, then the widest lanes
     for (uint32_t c : {1u, 2u, 4u, 5u}) {
         const uint32_t w = 64 * c, pad = (Td + w - 1) / w * w - Td;
         if (pad <= best) { best = pad; cpl = c; }
     }
-    // slices of at most 32 outputs, balanced: e.g. e = 52 -> two slices of KC = 28
-    const uint32_t np = (a.max_e + 31) / 32, kc = (((a.max_e + np - 1) / np) + 3) & ~3u;
+    // balanced slices of KC outputs, KC <= 32 and the slice's tables (20 B per coefficient) within
+    // ~20 KB of LDS when possible (two waves per SIMD): e = 52 -> 3 slices of 20
+    const uint32_t e = std::max<uint32_t>(a.max_e, 1);
+    uint32_t cap = std::max<uint32_t>(4, std::min<uint32_t>(32, (21504 / (20 * e)) & ~3u));
+    const uint32_t np = (e + cap - 1) / cap, kc = (((e + np - 1) / np) + 3) & ~3u;
+    const size_t lds = (size_t)e * kc * 20 + (size_t)e * 8;
+    static bool attr = false;
+    if (!attr) {  // slices of large e need more than the default 64 KB
+        for (const void* f : {(const void*)k_apply<32, 1>, (const void*)k_apply<32, 2>, (const void*)k_apply<32, 4>,
+                              (const void*)k_apply<32, 5>, (const void*)k_apply<28, 5>, (const void*)k_apply<28, 4>})
+            (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr = true;
+    }
     const dim3 g((Td + 64 * cpl - 1) / (64 * cpl) * n_blocks, np);
-    const hipStream_t st = (hipStream_t)stream;
     switch (cpl) {
-        case 1: launch_apply_cpl<1>(a, kc, g, st); break;
-        case 2: launch_apply_cpl<2>(a, kc, g, st); break;
-        case 4: launch_apply_cpl<4>(a, kc, g, st); break;
-        default: launch_apply_cpl<5>(a, kc, g, st); break;
+        case 1: launch_apply_cpl<1>(a, kc, g, lds, st); break;
+        case 2: launch_apply_cpl<2>(a, kc, g, lds, st); break;
+        case 4: launch_apply_cpl<4>(a, kc, g, lds, st); break;
+        default: launch_apply_cpl<5>(a, kc, g, lds, st); break;
     }
     return (int)hipGetLastError();
 }
