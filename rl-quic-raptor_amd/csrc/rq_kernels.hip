@@ -49,6 +49,13 @@ __device__ __forceinline__ uint32_t bitop_xand(uint32_t a, uint32_t b, uint32_t 
     return d;
 }
 
+// a ^ b ^ c in one v_bitop3 (hipcc does not form it from three XORs)
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t d;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+
 // ------------------------------ LT tuple on device (RQ/params.go:83-112) -------------------
 __device__ __forceinline__ uint32_t d_rand(uint32_t y, uint32_t i, uint32_t m) {
     return (c_V[0][(y + i) & 255u] ^ c_V[1][((y >> 8) + i) & 255u] ^ c_V[2][((y >> 16) + i) & 255u] ^
@@ -420,7 +427,7 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a) {
                 const uint32_t p0 = __builtin_amdgcn_perm(A.y, A.x, s0[j]);
                 const uint32_t p1 = __builtin_amdgcn_perm(A.w, A.z, s1[j]);
                 const uint32_t p2 = __builtin_amdgcn_perm(B, B, s2[j]);
-                acc[k][j] ^= p0 ^ p1 ^ p2;
+                acc[k][j] = xor3(acc[k][j], p0, p1) ^ p2;
             }
         }
     }
