@@ -345,19 +345,24 @@ __global__ void __launch_bounds__(256) k_xtab(ApplyArgs a) {
     }
 }
 
-// grid.x = solved block * strips + strip, grid.y = output slice of KC.  Each lane owns CPL dword
-// columns (64 apart: every load/store instruction is one contiguous 256-B segment).  The slice's
-// tables for all m are staged in LDS: A = the four 8-entry halves (b128), B = the 2-bit table.
+// One wave per (unit = solved block x strip, output slice of KC).  Workgroup w maps to slice
+// (w / 8) % np of unit (w / 8np) * 8 + w % 8: the slices of one unit share an XCD (workgroups are
+// dealt to the 8 XCDs round-robin) and are dispatched together, so their common syndrome rows are
+// read from HBM once and hit L2 after.  Each lane owns CPL dword columns (64 apart: every
+// load/store instruction is one contiguous 256-B segment).  The slice's tables for all m are
+// staged in LDS: A = the four 8-entry halves (b128), B = the 2-bit table.
 template <int KC, int CPL>
-__global__ void __launch_bounds__(64) k_apply(ApplyArgs a) {
+__global__ void __launch_bounds__(64) k_apply(ApplyArgs a, uint32_t n_units, uint32_t np) {
     extern __shared__ __attribute__((aligned(16))) uint32_t xsh[];
     const uint32_t strips = ((a.T >> 2) + 64 * CPL - 1) / (64 * CPL);
-    const uint32_t bi = blockIdx.x / strips, strip = blockIdx.x - bi * strips;
+    const uint32_t w = blockIdx.x, slice = (w / 8) % np, unit = (w / (8 * np)) * 8 + (w & 7);
+    if (unit >= n_units) return;
+    const uint32_t bi = unit / strips, strip = unit - bi * strips;
     const uint32_t b = a.blk_map[bi];
     if (a.status[b] != 1) return;
     const uint32_t lane = threadIdx.x;
     const uint32_t e = a.erased_off[b + 1] - a.erased_off[b];
-    const uint32_t k0 = blockIdx.y * KC;
+    const uint32_t k0 = slice * KC;
     if (k0 >= e) return;
     const uint32_t Td = a.T >> 2;
     const uint32_t* E = a.erased + a.erased_off[b];
@@ -401,22 +406,33 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a) {
     for (int k = 0; k < KC; ++k)
 #pragma unroll
         for (int j = 0; j < CPL; ++j) acc[k][j] = 0;
-    uint32_t s_next[CPL];
+    // syndromes are loaded two m ahead (received row and r0 row, XORed on arrival)
+    uint32_t ra[CPL], rb[CPL], na[CPL], nb[CPL];
 #pragma unroll
-    for (int j = 0; j < CPL; ++j) s_next[j] = recv[(size_t)offr[0] + col[j]] ^ r0[(size_t)off0[0] + col[j]];
+    for (int j = 0; j < CPL; ++j) {
+        ra[j] = recv[(size_t)offr[0] + col[j]];
+        rb[j] = r0[(size_t)off0[0] + col[j]];
+        const uint32_t m1 = e > 1 ? 1 : 0;
+        na[j] = recv[(size_t)offr[m1] + col[j]];
+        nb[j] = r0[(size_t)off0[m1] + col[j]];
+    }
     for (uint32_t m = 0; m < e; ++m) {
         uint32_t s0[CPL], s1[CPL], s2[CPL];
 #pragma unroll
         for (int j = 0; j < CPL; ++j) {
-            const uint32_t x = s_next[j];
+            const uint32_t x = ra[j] ^ rb[j];
             s0[j] = x & 0x07070707u;
             s1[j] = (x >> 3) & 0x07070707u;
             s2[j] = (x >> 6) & 0x03030303u;
+            ra[j] = na[j];
+            rb[j] = nb[j];
         }
-        if (m + 1 < e) {  // prefetch the next syndrome while this one is applied
+        if (m + 2 < e) {
 #pragma unroll
-            for (int j = 0; j < CPL; ++j)
-                s_next[j] = recv[(size_t)offr[m + 1] + col[j]] ^ r0[(size_t)off0[m + 1] + col[j]];
+            for (int j = 0; j < CPL; ++j) {
+                na[j] = recv[(size_t)offr[m + 2] + col[j]];
+                nb[j] = r0[(size_t)off0[m + 2] + col[j]];
+            }
         }
 #pragma unroll
         for (int k = 0; k < KC; ++k) {
@@ -444,16 +460,17 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a) {
 }
 
 template <int CPL>
-static void launch_apply_cpl(const ApplyArgs& a, uint32_t kc, dim3 g, size_t lds, hipStream_t st) {
+static void launch_apply_cpl(const ApplyArgs& a, uint32_t kc, dim3 g, size_t lds, hipStream_t st, uint32_t nu,
+                             uint32_t np) {
     switch (kc) {
-        case 4: hipLaunchKernelGGL((k_apply<4, CPL>), g, dim3(64), lds, st, a); break;
-        case 8: hipLaunchKernelGGL((k_apply<8, CPL>), g, dim3(64), lds, st, a); break;
-        case 12: hipLaunchKernelGGL((k_apply<12, CPL>), g, dim3(64), lds, st, a); break;
-        case 16: hipLaunchKernelGGL((k_apply<16, CPL>), g, dim3(64), lds, st, a); break;
-        case 20: hipLaunchKernelGGL((k_apply<20, CPL>), g, dim3(64), lds, st, a); break;
-        case 24: hipLaunchKernelGGL((k_apply<24, CPL>), g, dim3(64), lds, st, a); break;
-        case 28: hipLaunchKernelGGL((k_apply<28, CPL>), g, dim3(64), lds, st, a); break;
-        default: hipLaunchKernelGGL((k_apply<32, CPL>), g, dim3(64), lds, st, a); break;
+        case 4: hipLaunchKernelGGL((k_apply<4, CPL>), g, dim3(64), lds, st, a, nu, np); break;
+        case 8: hipLaunchKernelGGL((k_apply<8, CPL>), g, dim3(64), lds, st, a, nu, np); break;
+        case 12: hipLaunchKernelGGL((k_apply<12, CPL>), g, dim3(64), lds, st, a, nu, np); break;
+        case 16: hipLaunchKernelGGL((k_apply<16, CPL>), g, dim3(64), lds, st, a, nu, np); break;
+        case 20: hipLaunchKernelGGL((k_apply<20, CPL>), g, dim3(64), lds, st, a, nu, np); break;
+        case 24: hipLaunchKernelGGL((k_apply<24, CPL>), g, dim3(64), lds, st, a, nu, np); break;
+        case 28: hipLaunchKernelGGL((k_apply<28, CPL>), g, dim3(64), lds, st, a, nu, np); break;
+        default: hipLaunchKernelGGL((k_apply<32, CPL>), g, dim3(64), lds, st, a, nu, np); break;
     }
 }
 
@@ -479,12 +496,13 @@ int launch_apply(const ApplyArgs& a, uint32_t /*n_strips*/, uint32_t n_blocks, v
             (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
     }
-    const dim3 g((Td + 64 * cpl - 1) / (64 * cpl) * n_blocks, np);
+    const uint32_t nu = (Td + 64 * cpl - 1) / (64 * cpl) * n_blocks;
+    const dim3 g((nu + 7) / 8 * 8 * np);
     switch (cpl) {
-        case 1: launch_apply_cpl<1>(a, kc, g, lds, st); break;
-        case 2: launch_apply_cpl<2>(a, kc, g, lds, st); break;
-        case 4: launch_apply_cpl<4>(a, kc, g, lds, st); break;
-        default: launch_apply_cpl<5>(a, kc, g, lds, st); break;
+        case 1: launch_apply_cpl<1>(a, kc, g, lds, st, nu, np); break;
+        case 2: launch_apply_cpl<2>(a, kc, g, lds, st, nu, np); break;
+        case 4: launch_apply_cpl<4>(a, kc, g, lds, st, nu, np); break;
+        default: launch_apply_cpl<5>(a, kc, g, lds, st, nu, np); break;
     }
     return (int)hipGetLastError();
 }
