@@ -152,8 +152,13 @@ def _erase_and_decode(rq, gpu, src, out, K, T, N, n_erase, rng):
     return data, st, erased_lists, rep_lists
 
 
+# BASELINE.json configs 2-4 and the mixed stream of config 5 (K in {128, 512, 2048} x T in {256, 1200},
+# N = K + K/10 + 8, 5 % of N erased)
 @pytest.mark.parametrize("K,T,N,n_blocks,n_erase", [(1024, 1200, 1100, 4, 55), (256, 1200, 282, 8, 14),
-                                                     (64, 1200, 80, 16, 8), (2048, 256, 2200, 2, 110)])
+                                                     (64, 1200, 80, 16, 8), (2048, 256, 2200, 2, 110),
+                                                     (128, 256, 148, 8, 7), (128, 1200, 148, 8, 7),
+                                                     (512, 256, 571, 4, 29), (512, 1200, 571, 4, 29),
+                                                     (2048, 1200, 2260, 2, 113)])
 def test_batch_decode_round_trip(gpu, rq, oracle, K, T, N, n_blocks, n_erase):
     rng = np.random.default_rng(K + n_erase)
     esis = list(range(K, N))
