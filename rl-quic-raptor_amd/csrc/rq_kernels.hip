@@ -129,63 +129,85 @@ __device__ __forceinline__ void gf_tables(uint8_t* ex, uint8_t* lg) {
 // bytes, then the identity part (byte e + j).  Each step picks the lowest unused lane with a nonzero
 // coefficient (ballot), scales its row by the inverse, stores the eight alpha^b multiples of the
 // scaled row, and every other lane XORs in the multiples its own coefficient's bits select.
-constexpr uint32_t S64_W = 36;  // dwords per LDS row (128 B + 16 B pad; 16-B aligned for b128 access)
-
-__global__ void __launch_bounds__(64) k_solve64(SolveArgs a) {
-    __shared__ __attribute__((aligned(16))) uint32_t rows[64 * S64_W];
-    __shared__ __attribute__((aligned(16))) uint4 mult[8][8];  // alpha^b * scaled pivot row, 8 quads
+// One wave per block, RPL rows per lane: lane j owns received repairs j + 64q (q < RPL) as LDS rows of
+// 128*RPL bytes: e coefficient bytes, then the identity part (byte e + row).  RPL = 1 takes blocks with
+// e <= 64 on their first 64 received repairs; RPL = 2 takes the blocks it deferred (e <= 128, first 128
+// repairs).  Each step picks the lowest unused row with a nonzero coefficient (ballot), scales it by
+// the inverse, stores the eight alpha^b multiples of the scaled row, and every other row XORs in the
+// multiples its own coefficient's bits select (one v_bitop3 per bit and dword).
+template <int RPL>
+__global__ void __launch_bounds__(64) k_solve_fast(SolveArgs a) {
+    constexpr uint32_t NROWS = 64 * RPL, WQ = 8 * RPL, SW = 32 * RPL + 4;  // quads per row, row stride
+    __shared__ __attribute__((aligned(16))) uint32_t rows[NROWS * SW];
+    __shared__ __attribute__((aligned(16))) uint4 mult[8][WQ];  // alpha^b * scaled pivot row
     __shared__ uint8_t ex[512], lg[256];
-    __shared__ uint8_t pivl[64];
-    __shared__ uint32_t Es[64];
+    __shared__ uint8_t pivl[NROWS];
+    __shared__ uint32_t Es[NROWS];
     const uint32_t b = a.blk_map[blockIdx.x];
     const uint32_t lane = threadIdx.x;
+    if (RPL > 1 && a.status[b] != ST_FALLBACK) return;  // the wide pass takes deferred blocks only
     const uint32_t e = a.erased_off[b + 1] - a.erased_off[b];
     const uint32_t nr = a.rep_off[b + 1] - a.rep_off[b];
-    if (e > 64) {
+    if (e > NROWS) {
         if (lane == 0) a.status[b] = ST_FALLBACK;
         return;
     }
-    const uint32_t nrow = min(nr, 64u);
+    const uint32_t nrow = min(nr, NROWS);
     const uint32_t* E = a.erased + a.erased_off[b];
     const uint32_t* U = a.rep_uidx + a.rep_off[b];
-    if (lane < e) Es[lane] = E[lane];
+    for (uint32_t i = lane; i < e; i += 64) Es[i] = E[i];
     gf_tables(ex, lg);
-    uint32_t* my = rows + lane * S64_W;
-    uint4* my4 = reinterpret_cast<uint4*>(my);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) my4[q] = make_uint4(0, 0, 0, 0);
+    for (int q = 0; q < RPL; ++q) {
+        uint4* r4 = reinterpret_cast<uint4*>(rows + (lane + 64 * q) * SW);
+#pragma unroll
+        for (int w = 0; w < (int)WQ; ++w) r4[w] = make_uint4(0, 0, 0, 0);
+    }
     __syncthreads();
-    if (lane < nrow) {  // row gather: eight independent L2 loads in flight per step
-        uint8_t* myb = reinterpret_cast<uint8_t*>(my);
-        const uint8_t* mr = a.mrep + (size_t)U[lane] * a.mrep_stride;
-        uint32_t k = 0;
-        for (; k + 8 <= e; k += 8) {
-            uint8_t v[8];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) v[i] = mr[Es[k + i]];
+    for (int q = 0; q < RPL; ++q) {
+        const uint32_t row = lane + 64 * q;
+        if (row < nrow) {  // row gather: eight independent L2 loads in flight per step
+            uint8_t* myb = reinterpret_cast<uint8_t*>(rows + row * SW);
+            const uint8_t* mr = a.mrep + (size_t)U[row] * a.mrep_stride;
+            uint32_t k = 0;
+            for (; k + 8 <= e; k += 8) {
+                uint8_t v[8];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) myb[k + i] = v[i];
+                for (int i = 0; i < 8; ++i) v[i] = mr[Es[k + i]];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) myb[k + i] = v[i];
+            }
+            for (; k < e; ++k) myb[k] = mr[Es[k]];
+            myb[e + row] = 1;
         }
-        for (; k < e; ++k) myb[k] = mr[Es[k]];
-        myb[e + lane] = 1;
     }
     __syncthreads();
     const uint32_t q1 = (e + nrow + 15) >> 4;  // quads holding live columns
-    bool used = lane >= nrow;
+    bool used[RPL];
+#pragma unroll
+    for (int q = 0; q < RPL; ++q) used[q] = lane + 64 * q >= nrow;
     for (uint32_t k = 0; k < e; ++k) {
-        const uint32_t f = (my[k >> 2] >> ((k & 3) * 8)) & 0xFFu;
-        const uint64_t bal = __ballot(f != 0 && !used);
-        if (bal == 0) {
+        uint32_t f[RPL];
+        uint32_t p = 0xFFFFFFFFu;
+#pragma unroll
+        for (int q = RPL - 1; q >= 0; --q) {
+            f[q] = (rows[(lane + 64 * q) * SW + (k >> 2)] >> ((k & 3) * 8)) & 0xFFu;
+            const uint64_t bal = __ballot(f[q] != 0 && !used[q]);
+            if (bal) p = 64 * q + (uint32_t)__ffsll((unsigned long long)bal) - 1;
+        }
+        if (p == 0xFFFFFFFFu) {
             if (lane == 0) a.status[b] = (nr > nrow) ? ST_FALLBACK : 0;
             return;
         }
-        const uint32_t p = (uint32_t)__ffsll((unsigned long long)bal) - 1;
-        if (lane == p) used = true;
+#pragma unroll
+        for (int q = 0; q < RPL; ++q)
+            if (lane + 64 * q == p) used[q] = true;
         if (lane == 0) pivl[k] = (uint8_t)p;
-        const uint32_t fp = __shfl(f, p);
+        const uint32_t fp = (rows[p * SW + (k >> 2)] >> ((k & 3) * 8)) & 0xFFu;
         const uint32_t inv = ex[255 - lg[fp]];
-        if (lane < 32) {  // scaled pivot row and its alpha multiples
-            uint32_t x = rows[p * S64_W + lane], r = 0;
+        for (uint32_t d = lane; d < 32 * RPL; d += 64) {  // scaled pivot row and its alpha multiples
+            uint32_t x = rows[p * SW + d], r = 0;
 #pragma unroll
             for (int bt = 0; bt < 8; ++bt) {
                 if ((inv >> bt) & 1u) r ^= x;
@@ -194,30 +216,34 @@ __global__ void __launch_bounds__(64) k_solve64(SolveArgs a) {
             uint32_t* mflat = reinterpret_cast<uint32_t*>(mult);
 #pragma unroll
             for (int bt = 0; bt < 8; ++bt) {
-                mflat[bt * 32 + lane] = r;
+                mflat[bt * 32 * RPL + d] = r;
                 r = xtime4(r);
             }
         }
         __syncthreads();
         // columns < k are zero in the pivot row (all are earlier pivot columns): start at quad k/16
         const uint32_t q0 = k >> 4;
-        if (lane == p) {
-            for (uint32_t q = q0; q < q1; ++q) my4[q] = mult[0][q];
-        } else if (f) {
-            uint32_t msk[8];
 #pragma unroll
-            for (int bt = 0; bt < 8; ++bt) msk[bt] = 0u - ((f >> bt) & 1u);
-            for (uint32_t q = q0; q < q1; ++q) {
-                uint4 r = my4[q];
+        for (int q = 0; q < RPL; ++q) {
+            uint4* my4 = reinterpret_cast<uint4*>(rows + (lane + 64 * q) * SW);
+            if (lane + 64 * q == p) {
+                for (uint32_t w = q0; w < q1; ++w) my4[w] = mult[0][w];
+            } else if (f[q]) {
+                uint32_t msk[8];
 #pragma unroll
-                for (int bt = 0; bt < 8; ++bt) {
-                    const uint4 m = mult[bt][q];
-                    r.x ^= m.x & msk[bt];
-                    r.y ^= m.y & msk[bt];
-                    r.z ^= m.z & msk[bt];
-                    r.w ^= m.w & msk[bt];
+                for (int bt = 0; bt < 8; ++bt) msk[bt] = 0u - ((f[q] >> bt) & 1u);
+                for (uint32_t w = q0; w < q1; ++w) {
+                    uint4 r = my4[w];
+#pragma unroll
+                    for (int bt = 0; bt < 8; ++bt) {
+                        const uint4 m = mult[bt][w];
+                        r.x = bitop_xand(r.x, m.x, msk[bt]);
+                        r.y = bitop_xand(r.y, m.y, msk[bt]);
+                        r.z = bitop_xand(r.z, m.z, msk[bt]);
+                        r.w = bitop_xand(r.w, m.w, msk[bt]);
+                    }
+                    my4[w] = r;
                 }
-                my4[q] = r;
             }
         }
         __syncthreads();
@@ -229,12 +255,12 @@ __global__ void __launch_bounds__(64) k_solve64(SolveArgs a) {
     for (uint32_t m = lane; m < e; m += 64) XP[m] = pivl[m];
     for (uint32_t idx = lane; idx < e * e; idx += 64) {
         const uint32_t m = idx / e, k = idx - m * e;
-        xc[m * a.xc_stride + k] = rb[pivl[k] * S64_W * 4 + e + pivl[m]];
+        xc[m * a.xc_stride + k] = rb[pivl[k] * SW * 4 + e + pivl[m]];
     }
     if (lane == 0) a.status[b] = 1;
 }
 
-// General solver (any e, nr with nr*(e+nr) bytes in LDS) for the blocks k_solve64 deferred.
+// General solver (any e, nr with nr*(e+nr) bytes in LDS) for the blocks the fast solvers deferred.
 __global__ void __launch_bounds__(256) k_solve(SolveArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
     __shared__ uint8_t ex[512], lg[256];
@@ -299,9 +325,11 @@ __global__ void __launch_bounds__(256) k_solve(SolveArgs a) {
 }
 
 int launch_solve(const SolveArgs& a, uint32_t n_blocks, uint32_t lds_bytes, bool need_general, void* stream) {
-    hipLaunchKernelGGL(k_solve64, dim3(n_blocks), dim3(64), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(k_solve_fast<1>, dim3(n_blocks), dim3(64), 0, (hipStream_t)stream, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !need_general) return (int)e;
+    hipLaunchKernelGGL(k_solve_fast<2>, dim3(n_blocks), dim3(64), 0, (hipStream_t)stream, a);
+    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)k_solve, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
