@@ -504,7 +504,8 @@ struct Policy {
 };
 
 // Diagnostic builds (wrong bytes, timing only): RQHIP_DIAG bit 1 drops global scratch traffic,
-// 2 drops LDS spill traffic, 4 replaces source loads by register writes, 8 drops output stores.
+// 2 drops LDS spill traffic, 4 replaces source loads by register writes, 8 drops output stores,
+// 16 loads source rows in increasing row order (wrong rows; measures the cost of the random order).
 static uint32_t diag_mask() {
     const char* e = std::getenv("RQHIP_DIAG");
     return e ? (uint32_t)std::atoi(e) : 0u;
@@ -611,6 +612,7 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
     s += ".Lloop:\n";
     for (const char* p : pro_iter) put(p);
     int sr = 0;
+    uint32_t src_seq = 0;
     auto srot = [&]() { sr = (sr + 1) & 7; return 40 + sr; };
     for (const MInst& m : mp.ins) {
         switch (m.op) {
@@ -632,6 +634,7 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
             case MI_ZERO:
                 std::snprintf(buf, sizeof buf, "v_mov_b32_e32 v%d, 0", m.d); line(buf); break;
             case MI_LDSRC: {
+                const uint32_t row = (diag & 16) ? (src_seq++ % mp.K) : m.imm;
                 if (diag & 4) {
                     std::snprintf(buf, sizeof buf, is_agpr(m.d) ? "v_accvgpr_write_b32 %s, v%d" : "v_mov_b32_e32 %s, v%d",
                                   R(m.d), V_SRCOFF);
@@ -639,7 +642,7 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
                     break;
                 }
                 const int q = srot();
-                std::snprintf(buf, sizeof buf, "s_mul_i32 s%d, s12, %u", q, m.imm); line(buf);
+                std::snprintf(buf, sizeof buf, "s_mul_i32 s%d, s12, %u", q, row); line(buf);
                 std::snprintf(buf, sizeof buf, "buffer_load_dword %s, v%d, s[24:27], s%d offen%s", R(m.d), V_SRCOFF, q, pol.src.c_str()); line(buf);
                 break;
             }
