@@ -103,6 +103,20 @@ typedef struct {
 } rq_decode_desc;
 int rq_decode_batch(const rq_decode_desc* d);
 
+/* ---------------- batched, host-memory API (fecquic windows) ------------
+ * The batch path for callers without device memory (the cgo shim): the same descriptors, with
+ * src/out (encode) and data/repair (decode) in HOST memory; `stream` and `c_out` are not used.
+ * Blocks are split contiguously over the devices of device_mask (bit d = HIP device d; 0 = the
+ * calling thread's device), one host thread per device, no device-to-device traffic.  Each device
+ * pipelines H2D, kernels and D2H over two internal streams in chunks of blocks.  Synchronous.
+ * Pinned buffers (hipHostMalloc / hipHostRegister) copy at full PCIe rate; pageable ones work.
+ * Decode uploads each data block once and downloads only the recovered rows (e*T bytes per
+ * block) into `data`; blocks whose status is not 1 are left as they were.
+ * Replaces: the per-block GenSymbol loop of fecquic's sender window (go/fecquic/transfer.go:166-268)
+ * and the per-block Decode of the receiver workers (go/fecquic/rxbuf.go:336-377). */
+int rq_encode_batch_host(const rq_encode_desc* d, uint32_t device_mask);
+int rq_decode_batch_host(const rq_decode_desc* d, uint32_t device_mask);
+
 /* ---------------- device control ---------------- */
 int rq_device_count(void);
 int rq_set_device(int device);      /* selects the HIP device for subsequent calls on this thread */

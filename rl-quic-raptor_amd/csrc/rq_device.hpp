@@ -26,6 +26,7 @@ struct ZeroArgs {
     uint8_t* data;
     uint64_t data_stride;
     uint32_t T, n;
+    uint8_t* pack;              // k_pack_rows: row i of the list -> pack + i*T
 };
 
 struct SolveArgs {
@@ -68,6 +69,9 @@ struct ApplyArgs {
 
 // Launchers (rq_kernels.hip).  Return hipError_t as int.
 int launch_zero_rows(const ZeroArgs& a, void* stream);
+// Host-memory decode: copy the recovered rows (the same (blk, row) list) into a dense buffer so only
+// e*T bytes per block travel back over PCIe.
+int launch_pack_rows(const ZeroArgs& a, void* stream);
 // Fast one-wave solve (e <= 64, first 64 received repairs), then the general solver for the
 // blocks it deferred (lds_bytes sized for the largest e + nr of the batch).
 int launch_solve(const SolveArgs& a, uint32_t n_blocks, uint32_t lds_bytes, bool need_general, void* stream);

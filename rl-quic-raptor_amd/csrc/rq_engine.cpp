@@ -15,6 +15,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/rqhip.h"
@@ -98,7 +99,14 @@ struct HostBuf {
 // stream gets its own scratch / index / syndrome buffers (calls on one stream are ordered).
 struct Workspace {
     DevBuf idx, r0, xb, xt, xp, scratch;
-    HostBuf h_idx, h_status;
+    DevBuf pk;                      // host-memory decode: recovered rows, packed for the D2H
+    HostBuf h_idx, h_status, h_pack;
+};
+
+// Host-memory batch API: device staging of one pipeline stage (one internal stream).
+struct Stage {
+    hipStream_t s = nullptr;
+    DevBuf in, out;                 // encode: source chunk / repairs; decode: data chunk / repairs
 };
 
 struct DevCtx {
@@ -108,6 +116,7 @@ struct DevCtx {
     bool tables = false;
     std::map<std::string, std::unique_ptr<ColKernel>> colk;  // keyed by (K', K, outputs)
     std::map<void*, std::unique_ptr<Workspace>> ws;
+    Stage stage[2];
     Workspace* wsp(void* stream) {
         auto& w = ws[stream];
         if (!w) w.reset(new Workspace());
@@ -350,10 +359,18 @@ int ensure_mrep(DevCtx* ctx, ColKernel* k, void* stream) {
 
 constexpr uint32_t MAX_E = 255;  // decode-solve limits (LDS-resident [M | I])
 
+// Optional decode output for host-memory batches: the recovered rows of `blocks` (the solved
+// blocks, ascending; their erased rows in erased[] order) packed T bytes apart in pinned memory.
+struct PackOut {
+    const uint8_t* rows = nullptr;
+    std::vector<uint32_t> blocks;
+};
+
 // Batched syndrome decode.  Caller holds ctx->mu.  Host arrays as in rq_decode_desc.
 int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, void* data, uint64_t data_stride,
                   const uint32_t* n_erased, const uint32_t* erased, const uint32_t* n_repair,
-                  const uint32_t* repair_esi, const void* repair, int32_t* status, void* stream) {
+                  const uint32_t* repair_esi, const void* repair, int32_t* status, void* stream,
+                  PackOut* po = nullptr) {
     int rc;
     std::vector<uint32_t> blk_map, eoff(n_blocks + 1, 0), roff(n_blocks + 1, 0);
     size_t max_lds_solve = 0;
@@ -438,7 +455,7 @@ int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, v
     // 1) erased rows := 0, then r0 = the column program on every block (syndromes s = r ^ r0)
     ZeroArgs z;
     z.blk = di + o_zb; z.row = di + o_zr; z.data = static_cast<uint8_t*>(data); z.data_stride = data_stride;
-    z.T = T; z.n = nz;
+    z.T = T; z.n = nz; z.pack = nullptr;
     if (launch_zero_rows(z, stream)) return fail(RQ_ERR_DEVICE, "k_zero_rows launch failed");
     if ((rc = launch_col(ctx, k, T, n_blocks, data, data_stride, w->r0.p, (uint64_t)uni.size() * T, stream)))
         return rc;
@@ -478,11 +495,165 @@ int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, v
     ap.max_e = max_e;
     ap.xc_stride = xc_stride;
     if (launch_apply(ap, (T / 4 + 63) / 64, nw, stream)) return fail(RQ_ERR_DEVICE, "k_apply launch failed");
+    if (po) {
+        const size_t bytes = (size_t)nz * T;
+        if ((rc = w->pk.ensure(bytes)) || (rc = w->h_pack.ensure(bytes))) return rc;
+        z.pack = w->pk.as<uint8_t>();
+        if (launch_pack_rows(z, stream)) return fail(RQ_ERR_DEVICE, "k_pack_rows launch failed");
+        HIP_TRY(hipMemcpyAsync(w->h_pack.p, w->pk.p, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
+        po->rows = static_cast<const uint8_t*>(w->h_pack.p);
+        po->blocks = blk_map;
+    }
     int32_t* st = static_cast<int32_t*>(w->h_status.p);
     HIP_TRY(hipMemcpyAsync(st, w->idx.as<uint32_t>() + o_st, n_blocks * 4, hipMemcpyDeviceToHost,
                            (hipStream_t)stream));
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
     for (uint32_t b : blk_map) status[b] = st[b];
+    return RQ_OK;
+}
+
+// ---------------- host-memory batches (rq_encode_batch_host / rq_decode_batch_host) ----------------
+// Blocks per pipeline chunk: enough 64-column items to fill every resident wave slot about twice
+// (a chunk is one persistent launch), and at least a quarter of the shard so the H2D of one chunk
+// overlaps the kernels of the other.
+uint32_t chunk_blocks(const DevCtx* ctx, uint32_t T, uint32_t n_blocks) {
+    const uint32_t items_per_block = (T / 4 + 63) / 64;
+    const uint32_t fill = (2 * 4 * ctx->n_cu + items_per_block - 1) / items_per_block;
+    return std::max<uint32_t>(1, std::min(n_blocks, std::max(fill, (n_blocks + 3) / 4)));
+}
+
+int ensure_stages(DevCtx* ctx) {
+    for (Stage& s : ctx->stage)
+        if (!s.s) HIP_TRY(hipStreamCreateWithFlags(&s.s, hipStreamNonBlocking));
+    return RQ_OK;
+}
+
+// Copy n_rows rows of `width` bytes between strided layouts (one copy when both are dense).
+int copy_rows(void* dst, uint64_t dpitch, const void* src, uint64_t spitch, uint64_t width, uint32_t n_rows,
+              hipMemcpyKind kind, hipStream_t s) {
+    if (!n_rows || !width) return RQ_OK;
+    if (dpitch == width && spitch == width) {
+        HIP_TRY(hipMemcpyAsync(dst, src, width * n_rows, kind, s));
+        return RQ_OK;
+    }
+    for (uint32_t r = 0; r < n_rows; ++r)
+        HIP_TRY(hipMemcpyAsync(static_cast<uint8_t*>(dst) + r * dpitch, static_cast<const uint8_t*>(src) + r * spitch,
+                               width, kind, s));
+    return RQ_OK;
+}
+
+// One device's shard [b0, b1) of a host-memory encode: chunk c runs on stage c&1 (H2D source,
+// column program, D2H repairs); calls on one stream are ordered, so a stage's buffers are reused
+// only after its previous chunk finished.
+int encode_host_shard(int dev, const rq_encode_desc& d, const Params& p, uint32_t b0, uint32_t b1) {
+    g_device = dev;
+    DevCtx* ctx;
+    int rc = get_ctx(&ctx);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if ((rc = ensure_stages(ctx))) return rc;
+    const uint64_t in_b = (uint64_t)d.K * d.T, out_b = (uint64_t)d.n_esi * d.T;
+    const uint32_t cb = chunk_blocks(ctx, d.T, b1 - b0);
+    for (uint32_t c = 0, b = b0; b < b1; ++c, b += cb) {
+        Stage& st = ctx->stage[c & 1];
+        const uint32_t nb = std::min(cb, b1 - b);
+        if ((rc = st.in.ensure(cb * in_b)) || (rc = st.out.ensure(cb * out_b))) return rc;
+        const uint8_t* src = static_cast<const uint8_t*>(d.src) + b * d.src_stride;
+        uint8_t* out = static_cast<uint8_t*>(d.out) + b * d.out_stride;
+        if ((rc = copy_rows(st.in.p, in_b, src, d.src_stride, in_b, nb, hipMemcpyHostToDevice, st.s)) ||
+            (rc = encode_locked(ctx, p, d.T, nb, st.in.p, in_b, d.esi, d.n_esi, st.out.p, out_b, st.s)) ||
+            (rc = copy_rows(out, d.out_stride, st.out.p, out_b, out_b, nb, hipMemcpyDeviceToHost, st.s)))
+            return rc;
+    }
+    for (Stage& st : ctx->stage) HIP_TRY(hipStreamSynchronize(st.s));
+    return RQ_OK;
+}
+
+// One device's shard of a host-memory decode.  Per chunk: upload the data blocks and their received
+// repair rows (the next chunk's upload is queued on the other stage before this chunk's decode, so
+// it overlaps the kernels), decode, download only the recovered rows and scatter them into the
+// caller's buffer for the blocks that decoded.
+int decode_host_shard(int dev, const rq_decode_desc& d, const Params& p, uint32_t b0, uint32_t b1,
+                      const std::vector<uint64_t>& eoff, const std::vector<uint64_t>& roff) {
+    g_device = dev;
+    DevCtx* ctx;
+    int rc = get_ctx(&ctx);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if ((rc = ensure_stages(ctx))) return rc;
+    const uint64_t blk_b = (uint64_t)d.K * d.T;
+    const uint32_t cb = chunk_blocks(ctx, d.T, b1 - b0);
+    uint32_t max_rep = 0;
+    for (uint32_t b = b0; b < b1; b += cb)
+        max_rep = std::max<uint32_t>(max_rep, (uint32_t)(roff[std::min(b1, b + cb)] - roff[b]));
+    auto upload = [&](uint32_t c) -> int {
+        Stage& st = ctx->stage[c & 1];
+        const uint32_t b = b0 + c * cb, nb = std::min(cb, b1 - b);
+        int r;
+        if ((r = st.in.ensure(cb * blk_b)) || (r = st.out.ensure((size_t)max_rep * d.T))) return r;
+        if ((r = copy_rows(st.in.p, blk_b, static_cast<const uint8_t*>(d.data) + b * d.data_stride, d.data_stride,
+                           blk_b, nb, hipMemcpyHostToDevice, st.s)))
+            return r;
+        const uint64_t nr = roff[b + nb] - roff[b];
+        if (nr) HIP_TRY(hipMemcpyAsync(st.out.p, static_cast<const uint8_t*>(d.repair) + roff[b] * d.T, nr * d.T,
+                                       hipMemcpyHostToDevice, st.s));
+        return RQ_OK;
+    };
+    const uint32_t n_chunks = (b1 - b0 + cb - 1) / cb;
+    if ((rc = upload(0))) return rc;
+    for (uint32_t c = 0; c < n_chunks; ++c) {
+        if (c + 1 < n_chunks && (rc = upload(c + 1))) return rc;
+        Stage& st = ctx->stage[c & 1];
+        const uint32_t b = b0 + c * cb, nb = std::min(cb, b1 - b);
+        PackOut po;
+        if ((rc = decode_locked(ctx, p, d.T, nb, st.in.p, blk_b, d.n_erased + b, d.erased + eoff[b], d.n_repair + b,
+                                d.repair_esi + roff[b], st.out.p, d.status + b, st.s, &po)))
+            return rc;
+        size_t r = 0;
+        for (uint32_t lb : po.blocks) {
+            const uint32_t gb = b + lb;
+            uint8_t* dst = static_cast<uint8_t*>(d.data) + gb * d.data_stride;
+            for (uint64_t i = eoff[gb]; i < eoff[gb + 1]; ++i, ++r)
+                if (d.status[gb] == 1) std::memcpy(dst + (uint64_t)d.erased[i] * d.T, po.rows + r * d.T, d.T);
+        }
+    }
+    return RQ_OK;
+}
+
+// Split [0, n_blocks) contiguously over the devices of device_mask (0: the calling thread's
+// device) and run `shard(dev, b0, b1)` on one host thread per device.
+template <class F>
+int run_sharded(uint32_t device_mask, uint32_t n_blocks, F shard) {
+    std::vector<int> devs;
+    if (device_mask == 0) {
+        int dev;
+        int rc = current_device(&dev);
+        if (rc) return rc;
+        devs.push_back(dev);
+    } else {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(RQ_ERR_DEVICE, "no HIP device available");
+        for (int i = 0; i < 32; ++i)
+            if (device_mask >> i & 1u) {
+                if (i >= n) return fail(RQ_ERR_BAD_ARG, "device_mask names a device that does not exist");
+                devs.push_back(i);
+            }
+    }
+    const uint32_t nd = std::min<uint32_t>((uint32_t)devs.size(), n_blocks);
+    if (nd <= 1) return shard(devs[0], 0u, n_blocks);
+    std::vector<int> rcs(nd, RQ_OK);
+    std::vector<std::string> errs(nd);
+    std::vector<std::thread> th;
+    for (uint32_t i = 0; i < nd; ++i) {
+        const uint32_t b0 = (uint32_t)((uint64_t)n_blocks * i / nd), b1 = (uint32_t)((uint64_t)n_blocks * (i + 1) / nd);
+        th.emplace_back([&, i, b0, b1] {
+            rcs[i] = shard(devs[i], b0, b1);
+            if (rcs[i]) errs[i] = g_err;
+        });
+    }
+    for (auto& t : th) t.join();
+    for (uint32_t i = 0; i < nd; ++i)
+        if (rcs[i]) return fail(rcs[i], errs[i]);
     return RQ_OK;
 }
 
@@ -653,6 +824,40 @@ int rq_decode_batch(const rq_decode_desc* d) {
     std::lock_guard<std::mutex> lk(ctx->mu);
     return decode_locked(ctx, p, d->T, d->n_blocks, d->data, d->data_stride, d->n_erased, d->erased, d->n_repair,
                          d->repair_esi, d->repair, d->status, d->stream);
+}
+
+int rq_encode_batch_host(const rq_encode_desc* d, uint32_t device_mask) {
+    if (!d || d->T == 0) return fail(RQ_ERR_SYMBOL_SIZE_ZERO, "symbol size cannot be zero");
+    if (d->T % 4 || d->K == 0 || (!d->src && d->n_blocks)) return fail(RQ_ERR_BAD_ARG, "bad encode descriptor (T % 4, K, src)");
+    if (d->n_blocks == 0 || d->n_esi == 0) return RQ_OK;
+    if (!d->esi || !d->out) return fail(RQ_ERR_BAD_ARG, "n_esi without esi/out");
+    if (d->src_stride < (uint64_t)d->K * d->T || d->out_stride < (uint64_t)d->n_esi * d->T)
+        return fail(RQ_ERR_BAD_ARG, "stride smaller than a block");
+    if (d->c_out) return fail(RQ_ERR_BAD_ARG, "c_out is not supported by the host-memory batch");
+    Params p;
+    int rc = params_for_K(d->K, &p);
+    if (rc) return fail(rc, "k is too big");
+    return run_sharded(device_mask, d->n_blocks,
+                       [&](int dev, uint32_t b0, uint32_t b1) { return encode_host_shard(dev, *d, p, b0, b1); });
+}
+
+int rq_decode_batch_host(const rq_decode_desc* d, uint32_t device_mask) {
+    if (!d || d->T == 0) return fail(RQ_ERR_SYMBOL_SIZE_ZERO, "symbol size cannot be zero");
+    if (d->T % 4 || d->K == 0) return fail(RQ_ERR_BAD_ARG, "bad decode descriptor (T % 4, K)");
+    if (d->n_blocks == 0) return RQ_OK;
+    if (!d->data || !d->n_erased || !d->n_repair || !d->status) return fail(RQ_ERR_BAD_ARG, "null decode array");
+    if (d->data_stride < (uint64_t)d->K * d->T) return fail(RQ_ERR_BAD_ARG, "stride smaller than a block");
+    Params p;
+    int rc = params_for_K(d->K, &p);
+    if (rc) return fail(rc, "k is too big");
+    std::vector<uint64_t> eoff(d->n_blocks + 1, 0), roff(d->n_blocks + 1, 0);
+    for (uint32_t b = 0; b < d->n_blocks; ++b) {
+        eoff[b + 1] = eoff[b] + d->n_erased[b];
+        roff[b + 1] = roff[b] + d->n_repair[b];
+    }
+    return run_sharded(device_mask, d->n_blocks, [&](int dev, uint32_t b0, uint32_t b1) {
+        return decode_host_shard(dev, *d, p, b0, b1, eoff, roff);
+    });
 }
 
 // ---------------- per-object encoder (CreateEncoder / GenSymbol) ----------------

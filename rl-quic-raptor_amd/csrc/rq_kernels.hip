@@ -104,6 +104,21 @@ int launch_zero_rows(const ZeroArgs& a, void* stream) {
     return (int)hipGetLastError();
 }
 
+// grid = (n rows), 64 threads: recovered row i -> pack + i*T (dense D2H staging).
+__global__ void __launch_bounds__(64) k_pack_rows(ZeroArgs a) {
+    const uint32_t i = blockIdx.x;
+    if (i >= a.n) return;
+    const uint32_t* r4 = reinterpret_cast<const uint32_t*>(a.data + (size_t)a.blk[i] * a.data_stride + (size_t)a.row[i] * a.T);
+    uint32_t* p4 = reinterpret_cast<uint32_t*>(a.pack + (size_t)i * a.T);
+    for (uint32_t c = threadIdx.x; c < a.T / 4; c += 64) p4[c] = r4[c];
+}
+
+int launch_pack_rows(const ZeroArgs& a, void* stream) {
+    if (a.n == 0) return 0;
+    hipLaunchKernelGGL(k_pack_rows, dim3(a.n), dim3(64), 0, (hipStream_t)stream, a);
+    return (int)hipGetLastError();
+}
+
 // ------------------------------ decode: per-block GF(256) solve ------------------------------
 // M[j][k] = mrep[uidx_j][e_k] (received repair j, erased source e_k); Gauss-Jordan on [M | I]
 // (replaces GaussianElimination, RQ/discmath/gauss.go:7-45, on the e erased columns only):

@@ -38,7 +38,7 @@ EXPORTED = (
     "rq_strerror", "rq_last_error", "rq_params", "rq_encoder_create", "rq_encoder_k",
     "rq_encoder_symbol_size", "rq_encoder_symbol", "rq_encoder_symbols", "rq_encoder_free",
     "rq_decoder_create", "rq_decoder_k", "rq_decoder_add", "rq_decoder_decode", "rq_decoder_free",
-    "rq_encode_batch", "rq_decode_batch", "rq_device_count", "rq_set_device",
+    "rq_encode_batch", "rq_decode_batch", "rq_encode_batch_host", "rq_decode_batch_host", "rq_device_count", "rq_set_device",
     "rq_debug_colprog_eval", "rq_debug_colprog_emulate", "rq_debug_colprog_assemble",
 )
 
@@ -98,6 +98,8 @@ def lib():
             "rq_decoder_free": ([vp], None),
             "rq_encode_batch": ([ctypes.POINTER(EncodeDesc)], ctypes.c_int),
             "rq_decode_batch": ([ctypes.POINTER(DecodeDesc)], ctypes.c_int),
+            "rq_encode_batch_host": ([ctypes.POINTER(EncodeDesc), ctypes.c_uint32], ctypes.c_int),
+            "rq_decode_batch_host": ([ctypes.POINTER(DecodeDesc), ctypes.c_uint32], ctypes.c_int),
             "rq_device_count": ([], ctypes.c_int),
             "rq_set_device": ([ctypes.c_int], ctypes.c_int),
             "rq_debug_colprog_eval": ([ctypes.c_uint32, ctypes.c_uint32, u32p, ctypes.c_uint32, vp, vp, u32p],
@@ -371,3 +373,38 @@ class DecodeBatch:
                        stream=_stream_ptr(stream))
         _check(lib().rq_decode_batch(ctypes.byref(d)))
         return self.status
+
+
+# ------------------------------------------------------------------ host-memory batch API
+def _host_rows(a):
+    """(pointer, bytes between rows) of a 2-D uint8 host buffer: numpy array or CPU torch tensor
+    (pinned with .pin_memory() for full PCIe rate)."""
+    if hasattr(a, "data_ptr"):
+        assert not a.is_cuda and a.element_size() == 1 and a.stride(1) == 1
+        return a.data_ptr(), a.stride(0)
+    assert a.dtype.itemsize == 1 and a.strides[1] == 1
+    return a.ctypes.data, a.strides[0]
+
+
+def encode_batch_host(src, K, T, esis, out, device_mask=0):
+    """rq_encode_batch_host: src [n_blocks, >=K*T] and out [n_blocks, >=len(esis)*T] in host memory;
+    blocks are split over the devices of device_mask (0: the current device).  Synchronous."""
+    sp, ss = _host_rows(src)
+    op, os_ = _host_rows(out)
+    esi_arr = (ctypes.c_uint32 * max(len(esis), 1))(*esis)
+    d = EncodeDesc(T=T, K=K, n_blocks=src.shape[0], src=sp, src_stride=ss, n_esi=len(esis), esi=esi_arr,
+                   out=op, out_stride=os_, c_out=None, c_stride=0, stream=None)
+    _check(lib().rq_encode_batch_host(ctypes.byref(d), ctypes.c_uint32(device_mask)))
+
+
+def decode_batch_host(db, data, repair, device_mask=0):
+    """rq_decode_batch_host with the descriptor arrays of a DecodeBatch: data [n_blocks, >=K*T] (host;
+    recovered rows written in place), repair [n_rows, T] (host, repair_esi order).  Returns status."""
+    P32 = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+    dp, ds = _host_rows(data)
+    rp, _ = _host_rows(repair)
+    d = DecodeDesc(T=db.T, K=db.K, n_blocks=db.n_blocks, data=dp, data_stride=ds, n_erased=P32(db.n_erased),
+                   erased=P32(db.erased), n_repair=P32(db.n_repair), repair_esi=P32(db.repair_esi), repair=rp,
+                   status=db.status.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), stream=None)
+    _check(lib().rq_decode_batch_host(ctypes.byref(d), ctypes.c_uint32(device_mask)))
+    return db.status

@@ -77,3 +77,13 @@ def test_device_paths_fail_loudly_without_gpu(rq):
     with pytest.raises(rq.RaptorQError) as ei:
         rq.NewRaptorQEncoder(b"x" * 100, 1, 10)
     assert ei.value.code == rq.RQ_ERR_DEVICE
+    # the host-memory batch path has no CPU fallback either
+    import numpy as np
+    src, out = np.zeros((2, 64 * 64), np.uint8), np.zeros((2, 64), np.uint8)
+    with pytest.raises(rq.RaptorQError) as ei:
+        rq.encode_batch_host(src, 64, 64, [64], out)
+    assert ei.value.code == rq.RQ_ERR_DEVICE
+    db = rq.DecodeBatch(64, 64, [[1], [2]], [[64], [64]])
+    with pytest.raises(rq.RaptorQError) as ei:
+        rq.decode_batch_host(db, np.zeros((2, 64 * 64), np.uint8), np.zeros((2, 64), np.uint8))
+    assert ei.value.code == rq.RQ_ERR_DEVICE

@@ -1,0 +1,95 @@
+"""GPU parity of the host-memory batch API (rq_encode_batch_host / rq_decode_batch_host): the path a
+cgo caller without device memory takes (fecquic sender windows and receiver workers, SURVEY.md
+sec. 8f rank 1).  Results must equal the device-resident batch API's bit for bit, across several
+pipeline chunks, strided and pageable or pinned host buffers."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _device_encode(rq, gpu, src_h, K, T, esis):
+    src = torch.from_numpy(np.ascontiguousarray(src_h[:, :K * T])).to(gpu)
+    out = torch.empty((src.shape[0], len(esis) * T), dtype=torch.uint8, device=gpu)
+    rq.encode_batch(src, K, T, esis, out)
+    torch.cuda.synchronize()
+    return out.cpu().numpy()
+
+
+def test_host_encode_matches_device_batch(gpu, rq):
+    # 1000 blocks at T=1200: three pipeline chunks (>= 410 blocks each) on the two internal streams
+    K, T, R, nb = 64, 1200, 16, 1000
+    esis = list(range(K, K + R))
+    rng = np.random.default_rng(31)
+    src = rng.integers(0, 256, (nb, K * T), dtype=np.uint8)            # pageable
+    ref = _device_encode(rq, gpu, src, K, T, esis)
+    out = torch.zeros((nb, R * T), dtype=torch.uint8).pin_memory()    # pinned
+    rq.encode_batch_host(src, K, T, esis, out)
+    assert np.array_equal(out.numpy(), ref)
+    # strided source rows (a wider host buffer) and strided repair rows: per-block copies
+    wide = np.zeros((nb, K * T + 64), np.uint8)
+    wide[:, :K * T] = src
+    out2 = np.full((nb, R * T + 128), 7, np.uint8)
+    rq.encode_batch_host(wide, K, T, esis, out2[:, :])
+    assert np.array_equal(out2[:, :R * T], ref)
+    assert (out2[:, R * T:] == 7).all()
+
+
+def test_host_encode_bench_shape(gpu, rq):
+    # the bench block shape (K=1024, T=1200, 76 repairs) on a small batch
+    K, T, R, nb = 1024, 1200, 76, 8
+    esis = list(range(K, K + R))
+    src = np.random.default_rng(5).integers(0, 256, (nb, K * T), dtype=np.uint8)
+    out = np.zeros((nb, R * T), np.uint8)
+    rq.encode_batch_host(src, K, T, esis, out, device_mask=1)
+    assert np.array_equal(out, _device_encode(rq, gpu, src, K, T, esis))
+
+
+@pytest.mark.parametrize("K,T,N,nb,n_erase", [(64, 1200, 80, 1000, 8), (1024, 1200, 1100, 12, 55),
+                                               (128, 256, 148, 40, 7)])
+def test_host_decode_round_trip(gpu, rq, K, T, N, nb, n_erase):
+    R = N - K
+    esis = list(range(K, N))
+    rng = np.random.default_rng(K * 7 + nb)
+    src = rng.integers(0, 256, (nb, K * T), dtype=np.uint8)
+    rep_all = _device_encode(rq, gpu, src, K, T, esis).reshape(nb, R, T)
+    er, rl, rows = [], [], []
+    for b in range(nb):
+        lost = set(rng.choice(N, n_erase, replace=False).tolist())
+        er.append(sorted(i for i in lost if i < K))
+        rl.append([e for e in esis if e not in lost])
+        rows.extend(rep_all[b, e - K] for e in rl[-1])
+    # one block with too few symbols: status RQ_ERR_NOT_ENOUGH, its rows untouched
+    er[1] = list(range(R + 1))
+    rl[1] = esis
+    rows = [rep_all[b, e - K] for b in range(nb) for e in rl[b]]
+    repair = torch.from_numpy(np.stack(rows)).pin_memory()
+    data = torch.from_numpy(src.copy()).pin_memory()
+    d3 = data.numpy().reshape(nb, K, T)
+    for b in range(nb):
+        d3[b, er[b]] = 0xA5
+    before = data.numpy().copy()
+    db = rq.DecodeBatch(K, T, er, rl)
+    st = rq.decode_batch_host(db, data, repair).copy()
+    assert st[1] == rq.RQ_ERR_NOT_ENOUGH
+    assert np.array_equal(data.numpy()[1], before[1])
+    ok = st == 1
+    assert ok.sum() >= nb - 2 - nb // 20
+    assert np.array_equal(data.numpy()[ok], src[ok])
+    assert np.array_equal(data.numpy()[~ok], before[~ok])
+    # same statuses as the device-resident batch
+    dd = torch.from_numpy(before).to(gpu)
+    db2 = rq.DecodeBatch(K, T, er, rl)
+    st2 = db2.run(dd, repair.to(gpu))
+    torch.cuda.synchronize()
+    assert np.array_equal(st, st2)
+
+
+def test_host_batch_bad_device_mask(gpu, rq):
+    K, T = 64, 64
+    src = np.zeros((1, K * T), np.uint8)
+    out = np.zeros((1, T), np.uint8)
+    with pytest.raises(rq.RaptorQError) as ei:
+        rq.encode_batch_host(src, K, T, [K], out, device_mask=1 << 31)
+    assert ei.value.code == rq.RQ_ERR_BAD_ARG
