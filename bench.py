@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--erase", type=float, default=0.05)
     ap.add_argument("--cpu-sample", type=int, default=20, help="blocks in the CPU baseline sample (0 = skip)")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--sync-decode", action="store_true", help="time rq_decode_batch (host sync per step) "
+                    "instead of rq_decode_batch_async")
     ap.add_argument("--dist-backend", default="nccl", help="process-group backend for the timing collectives "
                     "(nccl = RCCL; gloo lets several ranks share one GPU for a functional rehearsal)")
     return ap.parse_args()
@@ -145,9 +147,10 @@ def main():
         good = torch.tensor(st == 1, device=dev)
         assert torch.equal(data[good], src[good]), "decode mismatch"
 
+    # timed path: rq_decode_batch_async (statuses land in pinned memory; no host sync per step)
     for _ in range(args.warmup):
         rqhip.encode_batch(src, K, T, esis, rep, stream=stream)
-        db.run(data, recv, stream=stream)
+        (db.run if args.sync_decode else db.run_async)(data, recv, stream=stream)
     torch.cuda.synchronize()
 
     if dist is not None:
@@ -159,13 +162,14 @@ def main():
         ev[s][0].record(stream)
         rqhip.encode_batch(src, K, T, esis, rep, stream=stream)
         ev[s][1].record(stream)
-        db.run(data, recv, stream=stream)
+        st_async = (db.run if args.sync_decode else db.run_async)(data, recv, stream=stream)
         ev[s][2].record(stream)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     dt = rqshard.max_over_ranks(time.perf_counter() - t0, dist, coll_dev)
+    assert np.array_equal(st_async, st), "async decode statuses differ"
     enc_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1, _ in ev]))
     dec_ms = float(np.mean([e1.elapsed_time(e2) for _, e1, e2 in ev]))
     total_blocks = rqshard.sum_over_ranks(B, dist, coll_dev)

@@ -102,6 +102,11 @@ typedef struct {
     void* stream;
 } rq_decode_desc;
 int rq_decode_batch(const rq_decode_desc* d);
+/* The same without the final synchronisation: returns once the work is queued on d->stream, and
+ * d->status, which must be pinned host memory (hipHostMalloc), holds the per-block results once
+ * the stream has reached the end of this call's work (ST_PENDING = -100 until then for the blocks
+ * that go to the solver).  Lets a caller queue the next batch while this one runs. */
+int rq_decode_batch_async(const rq_decode_desc* d);
 
 /* ---------------- batched, host-memory API (fecquic windows) ------------
  * The batch path for callers without device memory (the cgo shim): the same descriptors, with

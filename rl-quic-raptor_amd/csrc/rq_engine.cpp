@@ -98,9 +98,17 @@ struct HostBuf {
 // Per-stream workspaces: kernels of calls on different streams may run concurrently, so every
 // stream gets its own scratch / index / syndrome buffers (calls on one stream are ordered).
 struct Workspace {
-    DevBuf idx, r0, xb, xt, xp, scratch;
+    DevBuf r0, xb, xt, xp, scratch;
     DevBuf pk;                      // host-memory decode: recovered rows, packed for the D2H
-    HostBuf h_idx, h_status, h_pack;
+    HostBuf h_status, h_pack;
+    // decode descriptors, double-buffered so that rq_decode_batch_async can return before its upload
+    // ran: call n uses set n % 2; the host refills a set's pinned staging only after that set's
+    // previous upload completed (`up`), and reallocates its device copy only once the kernels that
+    // read it are done (`used`)
+    DevBuf idx[2];
+    HostBuf h_idx[2];
+    hipEvent_t up[2] = {nullptr, nullptr}, used[2] = {nullptr, nullptr};
+    uint32_t flip = 0;
 };
 
 // Host-memory batch API: device staging of one pipeline stage (one internal stream).
@@ -370,7 +378,7 @@ struct PackOut {
 int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, void* data, uint64_t data_stride,
                   const uint32_t* n_erased, const uint32_t* erased, const uint32_t* n_repair,
                   const uint32_t* repair_esi, const void* repair, int32_t* status, void* stream,
-                  PackOut* po = nullptr) {
+                  PackOut* po = nullptr, bool async = false) {
     int rc;
     std::vector<uint32_t> blk_map, eoff(n_blocks + 1, 0), roff(n_blocks + 1, 0);
     size_t max_lds_solve = 0;
@@ -428,8 +436,8 @@ int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, v
             idx.push_back(it != uni.end() && *it == x ? (uint32_t)(it - uni.begin()) : 0u);
         }
     }
-    const size_t o_st = idx.size();
-    idx.resize(idx.size() + n_blocks, 0);
+    const size_t o_st = idx.size();  // device status: host-decided values, ST_PENDING for the rest
+    for (uint32_t b = 0; b < n_blocks; ++b) idx.push_back((uint32_t)status[b]);
     const size_t o_zb = idx.size();
     uint32_t nz = 0;
     for (uint32_t b : blk_map)
@@ -437,15 +445,25 @@ int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, v
     const size_t o_zr = idx.size();
     for (uint32_t b : blk_map)
         for (uint32_t i = eoff[b]; i < eoff[b + 1]; ++i) idx.push_back(erased[i]);
-    // descriptor upload through pinned staging: the copy is queued behind the caller's work on the
-    // stream (e.g. the encode that produced `repair`) without blocking this thread
+    // descriptor upload through pinned staging, queued behind the caller's work on the stream (e.g.
+    // the encode that produced `repair`) without blocking this thread.  (A separate copy stream
+    // overlapping the upload with that work measured slower with rq_decode_batch_async.)
     Workspace* w = ctx->wsp(stream);
-    if ((rc = w->idx.ensure(idx.size() * 4)) || (rc = w->h_idx.ensure(idx.size() * 4)) ||
-        (rc = w->h_status.ensure((size_t)n_blocks * 4)))
-        return rc;
-    std::memcpy(w->h_idx.p, idx.data(), idx.size() * 4);
-    HIP_TRY(hipMemcpyAsync(w->idx.p, w->h_idx.p, idx.size() * 4, hipMemcpyHostToDevice, (hipStream_t)stream));
-    const uint32_t* di = w->idx.as<uint32_t>();
+    const uint32_t set = w->flip++ & 1u;
+    if (!w->up[0]) {
+        for (int i = 0; i < 2; ++i) {
+            HIP_TRY(hipEventCreateWithFlags(&w->up[i], hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&w->used[i], hipEventDisableTiming));
+        }
+    }
+    HIP_TRY(hipEventSynchronize(w->up[set]));  // the staging's previous upload has been read
+    if ((rc = w->h_idx[set].ensure(idx.size() * 4)) || (rc = w->h_status.ensure((size_t)n_blocks * 4))) return rc;
+    if (w->idx[set].cap < idx.size() * 4) HIP_TRY(hipEventSynchronize(w->used[set]));  // realloc: set idle
+    if ((rc = w->idx[set].ensure(idx.size() * 4))) return rc;
+    std::memcpy(w->h_idx[set].p, idx.data(), idx.size() * 4);
+    HIP_TRY(hipMemcpyAsync(w->idx[set].p, w->h_idx[set].p, idx.size() * 4, hipMemcpyHostToDevice, (hipStream_t)stream));
+    HIP_TRY(hipEventRecord(w->up[set], (hipStream_t)stream));
+    const uint32_t* di = w->idx[set].as<uint32_t>();
     const uint32_t xc_stride = 64 * ((max_e + 63) / 64);
     if ((rc = w->r0.ensure((size_t)n_blocks * uni.size() * T))) return rc;
     if ((rc = w->xb.ensure((size_t)nw * max_e * xc_stride))) return rc;
@@ -470,7 +488,7 @@ int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, v
     s.mrep_stride = k->mrep_stride;
     s.xcoef = w->xb.as<uint8_t>();
     s.xpiv = w->xp.as<uint16_t>();
-    s.status = reinterpret_cast<int32_t*>(w->idx.as<uint32_t>() + o_st);
+    s.status = reinterpret_cast<int32_t*>(w->idx[set].as<uint32_t>() + o_st);
     s.max_e = max_e;
     s.xc_stride = xc_stride;
     if (launch_solve(s, nw, (uint32_t)((max_lds_solve + 15) & ~size_t(15)), need_general, stream))
@@ -504,9 +522,16 @@ int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, v
         po->rows = static_cast<const uint8_t*>(w->h_pack.p);
         po->blocks = blk_map;
     }
+    if (async) {  // statuses land in the caller's pinned array when the stream gets here
+        HIP_TRY(hipMemcpyAsync(status, w->idx[set].as<uint32_t>() + o_st, n_blocks * 4, hipMemcpyDeviceToHost,
+                               (hipStream_t)stream));
+        HIP_TRY(hipEventRecord(w->used[set], (hipStream_t)stream));
+        return RQ_OK;
+    }
     int32_t* st = static_cast<int32_t*>(w->h_status.p);
-    HIP_TRY(hipMemcpyAsync(st, w->idx.as<uint32_t>() + o_st, n_blocks * 4, hipMemcpyDeviceToHost,
+    HIP_TRY(hipMemcpyAsync(st, w->idx[set].as<uint32_t>() + o_st, n_blocks * 4, hipMemcpyDeviceToHost,
                            (hipStream_t)stream));
+    HIP_TRY(hipEventRecord(w->used[set], (hipStream_t)stream));
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
     for (uint32_t b : blk_map) status[b] = st[b];
     return RQ_OK;
@@ -824,6 +849,25 @@ int rq_decode_batch(const rq_decode_desc* d) {
     std::lock_guard<std::mutex> lk(ctx->mu);
     return decode_locked(ctx, p, d->T, d->n_blocks, d->data, d->data_stride, d->n_erased, d->erased, d->n_repair,
                          d->repair_esi, d->repair, d->status, d->stream);
+}
+
+int rq_decode_batch_async(const rq_decode_desc* d) {
+    if (!d || d->T == 0) return fail(RQ_ERR_SYMBOL_SIZE_ZERO, "symbol size cannot be zero");
+    if (d->T % 4 || d->K == 0) return fail(RQ_ERR_BAD_ARG, "bad decode descriptor (T % 4, K)");
+    if (d->n_blocks == 0) return RQ_OK;
+    hipPointerAttribute_t pa;
+    if (!d->status || hipPointerGetAttributes(&pa, d->status) != hipSuccess || pa.type != hipMemoryTypeHost) {
+        (void)hipGetLastError();
+        return fail(RQ_ERR_BAD_ARG, "rq_decode_batch_async: status must be pinned host memory");
+    }
+    Params p;
+    int rc = params_for_K(d->K, &p);
+    if (rc) return fail(rc, "k is too big");
+    DevCtx* ctx;
+    if ((rc = get_ctx(&ctx))) return rc;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    return decode_locked(ctx, p, d->T, d->n_blocks, d->data, d->data_stride, d->n_erased, d->erased, d->n_repair,
+                         d->repair_esi, d->repair, d->status, d->stream, nullptr, true);
 }
 
 int rq_encode_batch_host(const rq_encode_desc* d, uint32_t device_mask) {

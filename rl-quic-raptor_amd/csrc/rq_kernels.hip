@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 
 #include "rfc6330_tables.h"
 #include "rq_device.hpp"
@@ -530,6 +531,8 @@ int launch_apply(const ApplyArgs& a, uint32_t /*n_strips*/, uint32_t n_blocks, v
     // ~20 KB of LDS when possible (two waves per SIMD): e = 52 -> 3 slices of 20
     const uint32_t e = std::max<uint32_t>(a.max_e, 1);
     uint32_t cap = std::max<uint32_t>(4, std::min<uint32_t>(32, (21504 / (20 * e)) & ~3u));
+    static const uint32_t cap_env = std::getenv("RQHIP_APPLY_CAP") ? (uint32_t)std::atoi(std::getenv("RQHIP_APPLY_CAP")) : 0;
+    if (cap_env) cap = std::min<uint32_t>(32, cap_env);
     const uint32_t np = (e + cap - 1) / cap, kc = (((e + np - 1) / np) + 3) & ~3u;
     const size_t lds = (size_t)e * kc * 20 + (size_t)e * 8;
     static bool attr = false;

@@ -38,7 +38,7 @@ EXPORTED = (
     "rq_strerror", "rq_last_error", "rq_params", "rq_encoder_create", "rq_encoder_k",
     "rq_encoder_symbol_size", "rq_encoder_symbol", "rq_encoder_symbols", "rq_encoder_free",
     "rq_decoder_create", "rq_decoder_k", "rq_decoder_add", "rq_decoder_decode", "rq_decoder_free",
-    "rq_encode_batch", "rq_decode_batch", "rq_encode_batch_host", "rq_decode_batch_host", "rq_device_count", "rq_set_device",
+    "rq_encode_batch", "rq_decode_batch", "rq_decode_batch_async", "rq_encode_batch_host", "rq_decode_batch_host", "rq_device_count", "rq_set_device",
     "rq_debug_colprog_eval", "rq_debug_colprog_emulate", "rq_debug_colprog_assemble",
 )
 
@@ -98,6 +98,7 @@ def lib():
             "rq_decoder_free": ([vp], None),
             "rq_encode_batch": ([ctypes.POINTER(EncodeDesc)], ctypes.c_int),
             "rq_decode_batch": ([ctypes.POINTER(DecodeDesc)], ctypes.c_int),
+            "rq_decode_batch_async": ([ctypes.POINTER(DecodeDesc)], ctypes.c_int),
             "rq_encode_batch_host": ([ctypes.POINTER(EncodeDesc), ctypes.c_uint32], ctypes.c_int),
             "rq_decode_batch_host": ([ctypes.POINTER(DecodeDesc), ctypes.c_uint32], ctypes.c_int),
             "rq_device_count": ([], ctypes.c_int),
@@ -339,12 +340,23 @@ def _stream_ptr(stream):
     return ctypes.c_void_p(stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream))
 
 
+_esi_cache = {}
+
+
+def _esi_array(esis):
+    key = tuple(esis)
+    arr = _esi_cache.get(key)
+    if arr is None:
+        if len(_esi_cache) > 64:
+            _esi_cache.clear()
+        arr = _esi_cache[key] = (ctypes.c_uint32 * max(len(esis), 1))(*esis)
+    return arr
+
+
 def encode_batch(src, K, T, esis, out, c_out=None, stream=None):
     """src: uint8 CUDA tensor [n_blocks, K*T] (contiguous rows); out: [n_blocks, len(esis)*T]."""
-    n_blocks = src.shape[0]
-    esi_arr = (ctypes.c_uint32 * max(len(esis), 1))(*esis)
-    d = EncodeDesc(T=T, K=K, n_blocks=n_blocks, src=src.data_ptr(), src_stride=src.stride(0),
-                   n_esi=len(esis), esi=esi_arr, out=out.data_ptr() if out is not None else None,
+    d = EncodeDesc(T=T, K=K, n_blocks=src.shape[0], src=src.data_ptr(), src_stride=src.stride(0),
+                   n_esi=len(esis), esi=_esi_array(esis), out=out.data_ptr() if out is not None else None,
                    out_stride=out.stride(0) if out is not None else 0,
                    c_out=c_out.data_ptr() if c_out is not None else None,
                    c_stride=c_out.stride(0) if c_out is not None else 0, stream=_stream_ptr(stream))
@@ -363,16 +375,31 @@ class DecodeBatch:
         self.n_repair = np.array([len(r) for r in repair_lists], np.uint32)
         self.repair_esi = np.concatenate([np.asarray(r, np.uint32) for r in repair_lists] + [np.zeros(1, np.uint32)])
         self.status = np.zeros(self.n_blocks, np.int32)
+        self._pinned = None
+        P32 = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+        self._ptrs = (P32(self.n_erased), P32(self.erased), P32(self.n_repair), P32(self.repair_esi))
+
+    def _desc(self, data, repair, status, stream):
+        ne, er, nr, re_ = self._ptrs
+        return DecodeDesc(T=self.T, K=self.K, n_blocks=self.n_blocks, data=data.data_ptr(),
+                          data_stride=data.stride(0), n_erased=ne, erased=er, n_repair=nr, repair_esi=re_,
+                          repair=repair.data_ptr(), status=status.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                          stream=_stream_ptr(stream))
 
     def run(self, data, repair, stream=None):
-        P32 = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
-        d = DecodeDesc(T=self.T, K=self.K, n_blocks=self.n_blocks, data=data.data_ptr(),
-                       data_stride=data.stride(0), n_erased=P32(self.n_erased), erased=P32(self.erased),
-                       n_repair=P32(self.n_repair), repair_esi=P32(self.repair_esi),
-                       repair=repair.data_ptr(), status=self.status.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
-                       stream=_stream_ptr(stream))
-        _check(lib().rq_decode_batch(ctypes.byref(d)))
+        """rq_decode_batch: synchronous, returns the status array."""
+        _check(lib().rq_decode_batch(ctypes.byref(self._desc(data, repair, self.status, stream))))
         return self.status
+
+    def run_async(self, data, repair, stream=None):
+        """rq_decode_batch_async: queues the decode and returns its pinned status array, valid once
+        the stream has completed the work."""
+        if self._pinned is None:
+            import torch
+            self._pinned = torch.zeros(self.n_blocks, dtype=torch.int32).pin_memory()
+        st = self._pinned.numpy()
+        _check(lib().rq_decode_batch_async(ctypes.byref(self._desc(data, repair, st, stream))))
+        return st
 
 
 # ------------------------------------------------------------------ host-memory batch API

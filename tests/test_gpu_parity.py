@@ -221,3 +221,39 @@ def test_concurrent_streams_independent(gpu, rq):
             rq.encode_batch(src[i], K, T, esis, out[i], stream=s)
     torch.cuda.synchronize()
     assert torch.equal(out, ref)
+
+
+def test_decode_async_back_to_back(gpu, rq):
+    """rq_decode_batch_async: three batches queued back to back on one stream without a host sync
+    (double-buffered descriptors, copy-stream upload) give the synchronous call's statuses and bytes."""
+    K, T, N, nb = 256, 1200, 282, 16
+    esis = list(range(K, N))
+    rng = np.random.default_rng(77)
+    src, out = _batch_encode(rq, gpu, K, T, nb, esis, 3)
+    runs = []
+    for it in range(3):
+        er, rl, rows = [], [], []
+        for b in range(nb):
+            lost = set(rng.choice(N, 14 + it, replace=False).tolist())
+            er.append(sorted(i for i in lost if i < K))
+            rl.append([e for e in esis if e not in lost])
+            rows.extend((b, e - K) for e in rl[-1])
+        rep = out.view(nb, N - K, T)[torch.tensor([b for b, _ in rows], device=gpu),
+                                     torch.tensor([r for _, r in rows], device=gpu)].contiguous()
+        data = src.clone()
+        for b in range(nb):
+            for i in er[b]:
+                data[b, i * T:(i + 1) * T] = 0x5A
+        runs.append((rq.DecodeBatch(K, T, er, rl), data, rep))
+    stream = torch.cuda.current_stream(gpu)
+    sts = [db.run_async(data, rep, stream=stream) for db, data, rep in runs]
+    torch.cuda.synchronize()
+    for (db, data, rep), st in zip(runs, sts):
+        assert (st == 1).all(), st
+        assert torch.equal(data, src)
+    # the same batch synchronously: identical statuses
+    db, data, rep = runs[0]
+    assert np.array_equal(db.run(data, rep), sts[0])
+    # the async call refuses pageable status memory
+    d = db._desc(data, rep, np.zeros(nb, np.int32), None)
+    assert rq.lib().rq_decode_batch_async(d) == rq.RQ_ERR_BAD_ARG
