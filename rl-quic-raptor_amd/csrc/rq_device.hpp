@@ -56,8 +56,6 @@ struct ApplyArgs {
     const uint8_t* r0;          // n_union rows of T bytes per block
     uint32_t n_union;
     const uint8_t* xcoef;
-    uint32_t* xtab;             // per (block, m, k): v_perm tables of c = X[k][m] (k_xtab), 5 dwords:
-                                // c*{0..3}, c*{4..7}, c*{0,8,16,24}, c*{32,40,48,56}, c*{0,64,128,192}
     const uint16_t* xpiv;
     const int32_t* status;
     uint8_t* data;

@@ -98,7 +98,7 @@ struct HostBuf {
 // Per-stream workspaces: kernels of calls on different streams may run concurrently, so every
 // stream gets its own scratch / index / syndrome buffers (calls on one stream are ordered).
 struct Workspace {
-    DevBuf r0, xb, xt, xp, scratch;
+    DevBuf r0, xb, xp, scratch;
     DevBuf pk;                      // host-memory decode: recovered rows, packed for the D2H
     HostBuf h_status, h_pack;
     // decode descriptors, double-buffered so that rq_decode_batch_async can return before its upload
@@ -467,7 +467,6 @@ int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, v
     const uint32_t xc_stride = 64 * ((max_e + 63) / 64);
     if ((rc = w->r0.ensure((size_t)n_blocks * uni.size() * T))) return rc;
     if ((rc = w->xb.ensure((size_t)nw * max_e * xc_stride))) return rc;
-    if ((rc = w->xt.ensure((size_t)nw * max_e * xc_stride * 20))) return rc;
     if ((rc = w->xp.ensure((size_t)nw * max_e * 2))) return rc;
 
     // 1) erased rows := 0, then r0 = the column program on every block (syndromes s = r ^ r0)
@@ -504,7 +503,6 @@ int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, v
     ap.r0 = w->r0.as<uint8_t>();
     ap.n_union = (uint32_t)uni.size();
     ap.xcoef = s.xcoef;
-    ap.xtab = w->xt.as<uint32_t>();
     ap.xpiv = s.xpiv;
     ap.status = s.status;
     ap.data = static_cast<uint8_t*>(data);

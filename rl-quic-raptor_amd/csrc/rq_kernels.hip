@@ -362,31 +362,22 @@ int launch_solve(const SolveArgs& a, uint32_t n_blocks, uint32_t lds_bytes, bool
 // XORs per dword: 5 VALU per mul-add instead of 8 bit-selects (replaces asmSSSE3MulAdd's nibble
 // pshufb, RQ/discmath/optimizations.s:36-78, with CDNA4's byte permute).
 
-// Tables for every coefficient of every solved block: 5 dwords per (m, k), k fastest.
-__global__ void __launch_bounds__(256) k_xtab(ApplyArgs a) {
-    __shared__ uint8_t ex[512], lg[256];
-    const uint32_t bi = blockIdx.x, b = a.blk_map[bi];
-    if (a.status[b] != 1) return;
-    gf_tables(ex, lg);
-    __syncthreads();
-    const uint32_t e = a.erased_off[b + 1] - a.erased_off[b];
-    const uint8_t* xc = a.xcoef + (size_t)bi * a.max_e * a.xc_stride;
-    uint32_t* xt = a.xtab + (size_t)bi * a.max_e * a.xc_stride * 5;
-    for (uint32_t idx = threadIdx.x; idx < e * e; idx += blockDim.x) {
-        const uint32_t m = idx / e, k = idx - m * e;
-        const uint8_t c = xc[m * a.xc_stride + k];
-        uint32_t t[5];
-        for (int w = 0; w < 5; ++w) {
-            uint32_t v = 0;
-            for (int i = 0; i < 4; ++i) {
-                const uint32_t x = w < 2 ? (uint32_t)(w * 4 + i) : w < 4 ? (uint32_t)((w - 2) * 4 + i) * 8 : (uint32_t)i * 64;
-                v |= (uint32_t)gmul_t(lg, ex, c, (uint8_t)x) << (8 * i);
-            }
-            t[w] = v;
-        }
-        uint32_t* d = xt + ((size_t)m * a.xc_stride + k) * 5;
-        for (int w = 0; w < 5; ++w) d[w] = t[w];
-    }
+// The five v_perm tables of a coefficient c (byte lanes): c*{0..3}, c*{4..7}, c*{0,8,16,24},
+// c*{32,40,48,56}, c*{0,64,128,192}, from the eight alpha^i multiples of c.
+__device__ __forceinline__ uint8_t xtime1(uint32_t x) { return (uint8_t)((x << 1) ^ ((x & 0x80u) ? 0x1Du : 0u)); }
+
+__device__ __forceinline__ void perm_tables(uint32_t c, uint4* A, uint32_t* B) {
+    uint32_t m[8];
+    m[0] = c;
+#pragma unroll
+    for (int i = 1; i < 8; ++i) m[i] = xtime1(m[i - 1]);
+    auto lo = [&](uint32_t x) { return ((x & 1u) ? m[0] : 0u) ^ ((x & 2u) ? m[1] : 0u) ^ ((x & 4u) ? m[2] : 0u); };
+    auto pack = [](uint32_t a, uint32_t b, uint32_t c2, uint32_t d) { return a | (b << 8) | (c2 << 16) | (d << 24); };
+    A->x = pack(0, lo(1), lo(2), lo(3));
+    A->y = pack(lo(4), lo(5), lo(6), lo(7));
+    A->z = pack(0, m[3], m[4], m[3] ^ m[4]);
+    A->w = pack(m[5], m[5] ^ m[3], m[5] ^ m[4], m[5] ^ m[4] ^ m[3]);
+    *B = pack(0, m[6], m[7], m[6] ^ m[7]);
 }
 
 // One wave per (unit = solved block x strip, output slice of KC).  Workgroup w maps to slice
@@ -394,7 +385,7 @@ __global__ void __launch_bounds__(256) k_xtab(ApplyArgs a) {
 // dealt to the 8 XCDs round-robin) and are dispatched together, so their common syndrome rows are
 // read from HBM once and hit L2 after.  Each lane owns CPL dword columns (64 apart: every
 // load/store instruction is one contiguous 256-B segment).  The slice's tables for all m are
-// staged in LDS: A = the four 8-entry halves (b128), B = the 2-bit table.
+// built from X straight into LDS (perm_tables): A = the four 8-entry halves (b128), B = the 2-bit table.
 template <int KC, int CPL>
 __global__ void __launch_bounds__(64) k_apply(ApplyArgs a, uint32_t n_units, uint32_t np) {
     extern __shared__ __attribute__((aligned(16))) uint32_t xsh[];
@@ -419,17 +410,14 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a, uint32_t n_units, uin
     uint32_t* tB = xsh + (size_t)e * KC * 4;                     // [m][KC]
     uint32_t* offr = tB + (size_t)e * KC;
     uint32_t* off0 = offr + e;
-    const uint32_t* xt = a.xtab + (size_t)bi * a.max_e * a.xc_stride * 5;
+    const uint8_t* xc = a.xcoef + (size_t)bi * a.max_e * a.xc_stride;
     for (uint32_t idx = lane; idx < e * KC; idx += 64) {
         const uint32_t m = idx / KC, k = idx - m * KC;
-        if (k0 + k < e) {
-            const uint32_t* src = xt + ((size_t)m * a.xc_stride + k0 + k) * 5;
-            tA[idx] = make_uint4(src[0], src[1], src[2], src[3]);
-            tB[idx] = src[4];
-        } else {
-            tA[idx] = make_uint4(0, 0, 0, 0);
-            tB[idx] = 0;
-        }
+        uint4 A = make_uint4(0, 0, 0, 0);
+        uint32_t B = 0;
+        if (k0 + k < e) perm_tables(xc[(size_t)m * a.xc_stride + k0 + k], &A, &B);
+        tA[idx] = A;
+        tB[idx] = B;
     }
     for (uint32_t m = lane; m < e; m += 64) {
         const uint32_t j = r0b + XP[m];
@@ -520,17 +508,17 @@ static void launch_apply_cpl(const ApplyArgs& a, uint32_t kc, dim3 g, size_t lds
 
 int launch_apply(const ApplyArgs& a, uint32_t /*n_strips*/, uint32_t n_blocks, void* stream) {
     const hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_xtab, dim3(n_blocks), dim3(256), 0, st, a);
     const uint32_t Td = a.T / 4;
     uint32_t cpl = 1, best = 0xFFFFFFFFu;  // fewest padded columns, then the widest lanes
     for (uint32_t c : {1u, 2u, 4u, 5u}) {
         const uint32_t w = 64 * c, pad = (Td + w - 1) / w * w - Td;
         if (pad <= best) { best = pad; cpl = c; }
     }
-    // balanced slices of KC outputs, KC <= 32 and the slice's tables (20 B per coefficient) within
-    // ~20 KB of LDS when possible (two waves per SIMD): e = 52 -> 3 slices of 20
+    // balanced slices of KC <= 8 outputs (measured at e ~ 58, K=1024 T=1200: KC 4/8/12/16/20/28 ->
+    // 244/210/238/254/282/324 us; small slices keep the accumulators few, so more waves fit per SIMD),
+    // the slice's tables (20 B per coefficient) within ~20 KB of LDS
     const uint32_t e = std::max<uint32_t>(a.max_e, 1);
-    uint32_t cap = std::max<uint32_t>(4, std::min<uint32_t>(32, (21504 / (20 * e)) & ~3u));
+    uint32_t cap = std::max<uint32_t>(4, std::min<uint32_t>(8, (21504 / (20 * e)) & ~3u));
     static const uint32_t cap_env = std::getenv("RQHIP_APPLY_CAP") ? (uint32_t)std::atoi(std::getenv("RQHIP_APPLY_CAP")) : 0;
     if (cap_env) cap = std::min<uint32_t>(32, cap_env);
     const uint32_t np = (e + cap - 1) / cap, kc = (((e + np - 1) / np) + 3) & ~3u;
