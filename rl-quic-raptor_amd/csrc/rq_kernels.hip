@@ -90,33 +90,37 @@ __device__ __forceinline__ void d_for_cols(const DevParams& p, uint32_t X, F&& f
 }
 
 // ------------------------------ decode: zero the erased source rows --------------------------
-// grid = (n erased rows), 64 threads: the syndrome pass reads erased rows as zero.
-__global__ void __launch_bounds__(64) k_zero_rows(ZeroArgs a) {
-    const uint32_t i = blockIdx.x;
+// One wave per erased row, four rows per workgroup: the syndrome pass reads erased rows as zero.
+__global__ void __launch_bounds__(256) k_zero_rows(ZeroArgs a) {
+    const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (i >= a.n) return;
-    uint8_t* row = a.data + (size_t)a.blk[i] * a.data_stride + (size_t)a.row[i] * a.T;
-    uint32_t* r4 = reinterpret_cast<uint32_t*>(row);
-    for (uint32_t c = threadIdx.x; c < a.T / 4; c += 64) r4[c] = 0;
+    uint4* r16 = reinterpret_cast<uint4*>(a.data + (size_t)a.blk[i] * a.data_stride + (size_t)a.row[i] * a.T);
+    uint32_t* r4 = reinterpret_cast<uint32_t*>(r16);
+    if ((a.T & 15) == 0 && ((uintptr_t)r16 & 15) == 0) {
+        for (uint32_t c = lane; c < a.T / 16; c += 64) r16[c] = make_uint4(0, 0, 0, 0);
+    } else {
+        for (uint32_t c = lane; c < a.T / 4; c += 64) r4[c] = 0;
+    }
 }
 
 int launch_zero_rows(const ZeroArgs& a, void* stream) {
     if (a.n == 0) return 0;
-    hipLaunchKernelGGL(k_zero_rows, dim3(a.n), dim3(64), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(k_zero_rows, dim3((a.n + 3) / 4), dim3(256), 0, (hipStream_t)stream, a);
     return (int)hipGetLastError();
 }
 
-// grid = (n rows), 64 threads: recovered row i -> pack + i*T (dense D2H staging).
-__global__ void __launch_bounds__(64) k_pack_rows(ZeroArgs a) {
-    const uint32_t i = blockIdx.x;
+// Recovered row i of the same list -> pack + i*T (dense D2H staging), one wave per row.
+__global__ void __launch_bounds__(256) k_pack_rows(ZeroArgs a) {
+    const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (i >= a.n) return;
     const uint32_t* r4 = reinterpret_cast<const uint32_t*>(a.data + (size_t)a.blk[i] * a.data_stride + (size_t)a.row[i] * a.T);
     uint32_t* p4 = reinterpret_cast<uint32_t*>(a.pack + (size_t)i * a.T);
-    for (uint32_t c = threadIdx.x; c < a.T / 4; c += 64) p4[c] = r4[c];
+    for (uint32_t c = lane; c < a.T / 4; c += 64) p4[c] = r4[c];
 }
 
 int launch_pack_rows(const ZeroArgs& a, void* stream) {
     if (a.n == 0) return 0;
-    hipLaunchKernelGGL(k_pack_rows, dim3(a.n), dim3(64), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(k_pack_rows, dim3((a.n + 3) / 4), dim3(256), 0, (hipStream_t)stream, a);
     return (int)hipGetLastError();
 }
 
@@ -130,29 +134,40 @@ __device__ __forceinline__ uint8_t gmul_t(const uint8_t* lg, const uint8_t* ex, 
     return (a && b) ? ex[lg[a] + lg[b]] : (uint8_t)0;
 }
 
-__device__ __forceinline__ void gf_tables(uint8_t* ex, uint8_t* lg) {
-    if (threadIdx.x == 0) {
-        uint32_t x = 1;
-        for (int i = 0; i < 255; ++i) {
-            ex[i] = (uint8_t)x; ex[i + 255] = (uint8_t)x; lg[x] = (uint8_t)i;
-            x <<= 1; if (x & 0x100) x ^= 0x11D;
-        }
-        ex[510] = ex[0]; ex[511] = ex[1]; lg[0] = 0;
+// GF(256) exp/log tables (poly 0x11D, alpha = 2), constant-initialised in device memory and copied
+// into LDS by the blocks that need them.
+struct GfTabs {
+    uint8_t ex[512];
+    uint8_t lg[256];
+};
+constexpr GfTabs make_gf_tabs() {
+    GfTabs t{};
+    uint32_t x = 1;
+    for (int i = 0; i < 255; ++i) {
+        t.ex[i] = (uint8_t)x; t.ex[i + 255] = (uint8_t)x; t.lg[x] = (uint8_t)i;
+        x <<= 1; if (x & 0x100) x ^= 0x11D;
     }
+    t.ex[510] = t.ex[0]; t.ex[511] = t.ex[1];
+    return t;
+}
+__device__ const GfTabs kGf = make_gf_tabs();
+
+__device__ __forceinline__ void gf_tables_copy(uint8_t* ex, uint8_t* lg) {
+    for (uint32_t i = threadIdx.x; i < 512; i += blockDim.x) ex[i] = kGf.ex[i];
+    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) lg[i] = kGf.lg[i];
 }
 
-// One wave per block.  Lane j owns received repair j (j < 64) as a 128-byte LDS row: e coefficient
-// bytes, then the identity part (byte e + j).  Each step picks the lowest unused lane with a nonzero
-// coefficient (ballot), scales its row by the inverse, stores the eight alpha^b multiples of the
-// scaled row, and every other lane XORs in the multiples its own coefficient's bits select.
-// One wave per block, RPL rows per lane: lane j owns received repairs j + 64q (q < RPL) as LDS rows of
-// 128*RPL bytes: e coefficient bytes, then the identity part (byte e + row).  RPL = 1 takes blocks with
-// e <= 64 on their first 64 received repairs; RPL = 2 takes the blocks it deferred (e <= 128, first 128
-// repairs).  Each step picks the lowest unused row with a nonzero coefficient (ballot), scales it by
-// the inverse, stores the eight alpha^b multiples of the scaled row, and every other row XORs in the
-// multiples its own coefficient's bits select (one v_bitop3 per bit and dword).
+// Four waves per block, RPL rows per lane: lane j of every wave holds received repairs j + 64q
+// (q < RPL) as LDS rows of 128*RPL bytes: e coefficient bytes, then the identity part (byte e + row);
+// wave g updates the 16-byte quads g, g+4, ... of every row.  RPL = 1 takes blocks with e <= 64 on
+// their first 64 received repairs; RPL = 2 takes the blocks it deferred (e <= 128, first 128
+// repairs).  Each step picks the lowest unused row with a nonzero coefficient (ballot: every wave
+// sees all rows and picks the same one), scales it by the inverse and stores its eight alpha^b
+// multiples (one byte per thread, exp/log tables), and every other row XORs in the multiples its own
+// coefficient's bits select (one v_bitop3 per bit and dword).
 template <int RPL>
-__global__ void __launch_bounds__(64) k_solve_fast(SolveArgs a) {
+__global__ void __launch_bounds__(256) k_solve_fast(SolveArgs a) {
+    constexpr uint32_t NW = 4, NT = 64 * NW;
     constexpr uint32_t NROWS = 64 * RPL, WQ = 8 * RPL, SW = 32 * RPL + 4;  // quads per row, row stride
     __shared__ __attribute__((aligned(16))) uint32_t rows[NROWS * SW];
     __shared__ __attribute__((aligned(16))) uint4 mult[8][WQ];  // alpha^b * scaled pivot row
@@ -160,42 +175,29 @@ __global__ void __launch_bounds__(64) k_solve_fast(SolveArgs a) {
     __shared__ uint8_t pivl[NROWS];
     __shared__ uint32_t Es[NROWS];
     const uint32_t b = a.blk_map[blockIdx.x];
-    const uint32_t lane = threadIdx.x;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
     if (RPL > 1 && a.status[b] != ST_FALLBACK) return;  // the wide pass takes deferred blocks only
     const uint32_t e = a.erased_off[b + 1] - a.erased_off[b];
     const uint32_t nr = a.rep_off[b + 1] - a.rep_off[b];
     if (e > NROWS) {
-        if (lane == 0) a.status[b] = ST_FALLBACK;
+        if (tid == 0) a.status[b] = ST_FALLBACK;
         return;
     }
     const uint32_t nrow = min(nr, NROWS);
     const uint32_t* E = a.erased + a.erased_off[b];
     const uint32_t* U = a.rep_uidx + a.rep_off[b];
-    for (uint32_t i = lane; i < e; i += 64) Es[i] = E[i];
-    gf_tables(ex, lg);
-#pragma unroll
-    for (int q = 0; q < RPL; ++q) {
-        uint4* r4 = reinterpret_cast<uint4*>(rows + (lane + 64 * q) * SW);
-#pragma unroll
-        for (int w = 0; w < (int)WQ; ++w) r4[w] = make_uint4(0, 0, 0, 0);
-    }
+    for (uint32_t i = tid; i < e; i += NT) Es[i] = E[i];
+    gf_tables_copy(ex, lg);
+    for (uint32_t i = tid; i < NROWS * SW; i += NT) rows[i] = 0;
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < RPL; ++q) {
         const uint32_t row = lane + 64 * q;
-        if (row < nrow) {  // row gather: eight independent L2 loads in flight per step
+        if (row < nrow) {  // row gather: wave g takes columns g, g+4, ...
             uint8_t* myb = reinterpret_cast<uint8_t*>(rows + row * SW);
             const uint8_t* mr = a.mrep + (size_t)U[row] * a.mrep_stride;
-            uint32_t k = 0;
-            for (; k + 8 <= e; k += 8) {
-                uint8_t v[8];
-#pragma unroll
-                for (int i = 0; i < 8; ++i) v[i] = mr[Es[k + i]];
-#pragma unroll
-                for (int i = 0; i < 8; ++i) myb[k + i] = v[i];
-            }
-            for (; k < e; ++k) myb[k] = mr[Es[k]];
-            myb[e + row] = 1;
+            for (uint32_t k = g; k < e; k += NW) myb[k] = mr[Es[k]];
+            if (g == 0) myb[e + row] = 1;
         }
     }
     __syncthreads();
@@ -203,6 +205,8 @@ __global__ void __launch_bounds__(64) k_solve_fast(SolveArgs a) {
     bool used[RPL];
 #pragma unroll
     for (int q = 0; q < RPL; ++q) used[q] = lane + 64 * q >= nrow;
+    uint8_t* mb = reinterpret_cast<uint8_t*>(mult);
+    const uint8_t* rb = reinterpret_cast<const uint8_t*>(rows);
     for (uint32_t k = 0; k < e; ++k) {
         uint32_t f[RPL];
         uint32_t p = 0xFFFFFFFFu;
@@ -212,29 +216,22 @@ __global__ void __launch_bounds__(64) k_solve_fast(SolveArgs a) {
             const uint64_t bal = __ballot(f[q] != 0 && !used[q]);
             if (bal) p = 64 * q + (uint32_t)__ffsll((unsigned long long)bal) - 1;
         }
-        if (p == 0xFFFFFFFFu) {
-            if (lane == 0) a.status[b] = (nr > nrow) ? ST_FALLBACK : 0;
+        if (p == 0xFFFFFFFFu) {  // uniform over the block: every wave saw the same rows
+            if (tid == 0) a.status[b] = (nr > nrow) ? ST_FALLBACK : 0;
             return;
         }
 #pragma unroll
         for (int q = 0; q < RPL; ++q)
             if (lane + 64 * q == p) used[q] = true;
-        if (lane == 0) pivl[k] = (uint8_t)p;
-        const uint32_t fp = (rows[p * SW + (k >> 2)] >> ((k & 3) * 8)) & 0xFFu;
-        const uint32_t inv = ex[255 - lg[fp]];
-        for (uint32_t d = lane; d < 32 * RPL; d += 64) {  // scaled pivot row and its alpha multiples
-            uint32_t x = rows[p * SW + d], r = 0;
+        if (tid == 0) pivl[k] = (uint8_t)p;
+        // scaled pivot row and its alpha multiples: alpha^bt * x / x_k = exp(log x - log x_k + bt)
+        const uint32_t lginv = 255u - lg[rb[p * SW * 4 + k]];
+        for (uint32_t pos = tid; pos < 128 * RPL; pos += NT) {
+            const uint32_t x = rb[p * SW * 4 + pos];
+            uint32_t t = lg[x] + lginv;
+            t = t >= 255u ? t - 255u : t;
 #pragma unroll
-            for (int bt = 0; bt < 8; ++bt) {
-                if ((inv >> bt) & 1u) r ^= x;
-                x = xtime4(x);
-            }
-            uint32_t* mflat = reinterpret_cast<uint32_t*>(mult);
-#pragma unroll
-            for (int bt = 0; bt < 8; ++bt) {
-                mflat[bt * 32 * RPL + d] = r;
-                r = xtime4(r);
-            }
+            for (int bt = 0; bt < 8; ++bt) mb[bt * WQ * 16 + pos] = x ? ex[t + bt] : (uint8_t)0;
         }
         __syncthreads();
         // columns < k are zero in the pivot row (all are earlier pivot columns): start at quad k/16
@@ -243,12 +240,12 @@ __global__ void __launch_bounds__(64) k_solve_fast(SolveArgs a) {
         for (int q = 0; q < RPL; ++q) {
             uint4* my4 = reinterpret_cast<uint4*>(rows + (lane + 64 * q) * SW);
             if (lane + 64 * q == p) {
-                for (uint32_t w = q0; w < q1; ++w) my4[w] = mult[0][w];
+                for (uint32_t w = q0 + g; w < q1; w += NW) my4[w] = mult[0][w];
             } else if (f[q]) {
                 uint32_t msk[8];
 #pragma unroll
                 for (int bt = 0; bt < 8; ++bt) msk[bt] = 0u - ((f[q] >> bt) & 1u);
-                for (uint32_t w = q0; w < q1; ++w) {
+                for (uint32_t w = q0 + g; w < q1; w += NW) {
                     uint4 r = my4[w];
 #pragma unroll
                     for (int bt = 0; bt < 8; ++bt) {
@@ -267,13 +264,12 @@ __global__ void __launch_bounds__(64) k_solve_fast(SolveArgs a) {
     // X[k][m] = identity byte (e + piv_m) of pivot row piv_k
     uint8_t* xc = a.xcoef + (size_t)blockIdx.x * a.max_e * a.xc_stride;
     uint16_t* XP = a.xpiv + (size_t)blockIdx.x * a.max_e;
-    const uint8_t* rb = reinterpret_cast<const uint8_t*>(rows);
-    for (uint32_t m = lane; m < e; m += 64) XP[m] = pivl[m];
-    for (uint32_t idx = lane; idx < e * e; idx += 64) {
+    for (uint32_t m = tid; m < e; m += NT) XP[m] = pivl[m];
+    for (uint32_t idx = tid; idx < e * e; idx += NT) {
         const uint32_t m = idx / e, k = idx - m * e;
         xc[m * a.xc_stride + k] = rb[pivl[k] * SW * 4 + e + pivl[m]];
     }
-    if (lane == 0) a.status[b] = 1;
+    if (tid == 0) a.status[b] = 1;
 }
 
 // General solver (any e, nr with nr*(e+nr) bytes in LDS) for the blocks the fast solvers deferred.
@@ -291,7 +287,7 @@ __global__ void __launch_bounds__(256) k_solve(SolveArgs a) {
     const uint32_t* E = a.erased + a.erased_off[b];
     const uint32_t* U = a.rep_uidx + a.rep_off[b];
     const uint32_t ws = e + nr;
-    gf_tables(ex, lg);
+    gf_tables_copy(ex, lg);
     for (uint32_t r = tid; r < nr; r += nthr) rowid[r] = (uint16_t)r;
     for (uint32_t idx = tid; idx < nr * ws; idx += nthr) {
         const uint32_t j = idx / ws, k = idx - j * ws;
@@ -341,10 +337,10 @@ __global__ void __launch_bounds__(256) k_solve(SolveArgs a) {
 }
 
 int launch_solve(const SolveArgs& a, uint32_t n_blocks, uint32_t lds_bytes, bool need_general, void* stream) {
-    hipLaunchKernelGGL(k_solve_fast<1>, dim3(n_blocks), dim3(64), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(k_solve_fast<1>, dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !need_general) return (int)e;
-    hipLaunchKernelGGL(k_solve_fast<2>, dim3(n_blocks), dim3(64), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(k_solve_fast<2>, dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a);
     if ((e = hipGetLastError()) != hipSuccess) return (int)e;
     static bool attr = false;
     if (!attr) {
