@@ -50,6 +50,10 @@ struct Allocator {
     Allocator(const ColIR& i, const AllocOpts& op, MProg* m, std::string* e) : ir(i), o(op), mp(m), err(e) {}
 
     uint32_t nu(uint32_t v) const { return uptr[v] < uses[v].size() ? uses[v][uptr[v]] : INF; }
+    // a source row always has its home copy in the source buffer: evicted, it is re-read from there
+    // instead of being written to scratch
+    bool is_src(uint32_t v) const { return ir.nodes[v].k == IR_LOAD; }
+    bool has_copy(uint32_t v) const { return slot[v] >= 0 || lslot[v] >= 0 || is_src(v); }
 
     void emit(uint8_t op, int d = -1, int a = -1, int b = -1, int c = -1, uint32_t imm = 0) {
         MInst m;
@@ -157,17 +161,19 @@ struct Allocator {
                 const int t = Reserved(o.n_vgpr).t1;
                 lds_res.erase(std::prev(lds_res.end()));
                 if (dma_seq[w]) { wait_seq(dma_seq[w]); dma_seq[w] = 0; }
-                const uint64_t q = issue_lgkm();
-                emit(MI_LDLD, t, -1, -1, -1, (uint32_t)s);
-                mp->st.ldld++;
-                wait_lseq(q);
                 lslot[w] = -1;
-                to_global(w, t);
+                if (!is_src(w)) {  // a source row is simply dropped: it is re-read from the source
+                    const uint64_t q = issue_lgkm();
+                    emit(MI_LDLD, t, -1, -1, -1, (uint32_t)s);
+                    mp->st.ldld++;
+                    wait_lseq(q);
+                    to_global(w, t);
+                }
                 mp->st.migrate++;
                 lds_put((uint32_t)v, r, s);
             }
         }
-        if (slot[v] < 0 && lslot[v] < 0) to_global((uint32_t)v, r);
+        if (!has_copy((uint32_t)v)) to_global((uint32_t)v, r);
         reg[v] = -1;
         owner[r] = -1;
         reload_q.push({nu((uint32_t)v), (uint32_t)v});
@@ -248,6 +254,15 @@ struct Allocator {
             owner[r] = (int32_t)v; reg[v] = (int16_t)r;
             return;
         }
+        if (slot[v] < 0) {  // a dropped source row: read it again from the source buffer
+            const uint64_t q = issue_vmem();
+            emit(MI_LDSRC, r, -1, -1, -1, ir.nodes[v].imm);
+            mp->st.spld++;
+            inflight[r] = q;
+            pend_loads.push_back({q, r});
+            owner[r] = (int32_t)v; reg[v] = (int16_t)r;
+            return;
+        }
         const int32_t s = slot[v];
         wait_seq(slot_st[s]);
         const uint64_t q = issue_vmem();
@@ -288,7 +303,7 @@ struct Allocator {
     int to_vgpr(uint32_t v) {
         int r = reg[v];
         if (r < 0) {  // not prefetched: synchronous reload
-            if (slot[v] < 0 && lslot[v] < 0) { fail("colasm: value lost"); return 0; }
+            if (!has_copy(v)) { fail("colasm: value lost"); return 0; }
             const int t = take_vgpr();
             reload_into(v, t);
             mp->st.sync_reload++;
@@ -362,7 +377,7 @@ struct Allocator {
             while (!reload_q.empty() && reload_q.top().first <= i + o.la_reload) {
                 const HE e = reload_q.top();
                 const uint32_t v = e.second;
-                if (reg[v] >= 0 || (slot[v] < 0 && lslot[v] < 0) || nu(v) != e.first) { reload_q.pop(); continue; }
+                if (reg[v] >= 0 || !has_copy(v) || nu(v) != e.first) { reload_q.pop(); continue; }
                 if (seq - retired >= o.max_vmem && e.first > i + 8) break;
                 const int r = take_any(e.first);
                 if (r < 0) break;
@@ -382,7 +397,7 @@ struct Allocator {
                     const uint32_t v = n.a;
                     int r = reg[v];
                     if (r < 0) {
-                        if (slot[v] < 0 && lslot[v] < 0) { fail("colasm: store of a lost value"); break; }
+                        if (!has_copy(v)) { fail("colasm: store of a lost value"); break; }
                         r = take_vgpr();
                         reload_into(v, r);
                         mp->st.sync_reload++;
