@@ -149,7 +149,7 @@ struct Allocator {
     // global scratch when its own next use is nearer (through the reserved temp VGPR).
     void spill_out(int r) {
         const int32_t v = owner[r];
-        if (slot[v] < 0 && lslot[v] < 0 && o.n_lds) {
+        if (slot[v] < 0 && lslot[v] < 0 && o.n_lds && (o.src_lds || !is_src((uint32_t)v))) {
             const uint32_t n = nu((uint32_t)v);
             if (!free_lslots.empty()) {
                 const int32_t s = free_lslots.back();
@@ -180,11 +180,12 @@ struct Allocator {
     }
     int victim(int lo, int hi) const {  // max-next-use resident value in [lo, hi), unpinned, not in flight
         int best = -1;
-        uint32_t bn = 0;
+        uint64_t bn = 0;
         for (int r = lo; r < hi; ++r) {
             const int32_t v = owner[r];
             if (v < 0 || pinned[r] || busy(r)) continue;
-            const uint32_t n = nu((uint32_t)v);
+            // source rows leave for free (no store): their next use counts src_bias % as far
+            const uint64_t n = (uint64_t)nu((uint32_t)v) * (is_src((uint32_t)v) ? o.src_bias : 100u);
             if (best < 0 || n > bn) { best = r; bn = n; }
         }
         return best;

@@ -58,6 +58,8 @@ struct AllocOpts {
     uint32_t n_lds = 156;        // LDS spill slots per wave (256 B each; 4 waves/CU -> 40 KB; <= 512)
     uint32_t lds_horizon = 200;  // push an LDS resident out only if its next use is this much further
     uint32_t la_dma = 0;         // look-ahead (IR nodes) for LDS-DMA source staging (0 = off)
+    uint32_t src_bias = 100;     // victim choice: a source row's next use counts this % as far
+    uint32_t src_lds = 1;        // evicted source rows may take LDS slots (else dropped at once)
 };
 
 struct MProg {

@@ -203,6 +203,8 @@ const AllocOpts& alloc_options() {
         }
         if (const char* h = std::getenv("RQHIP_LDS_HORIZON")) r.lds_horizon = (uint32_t)std::atoi(h);
         if (const char* h = std::getenv("RQHIP_LA_DMA")) r.la_dma = (uint32_t)std::atoi(h);
+        if (const char* h = std::getenv("RQHIP_SRC_BIAS")) r.src_bias = (uint32_t)std::atoi(h);
+        if (const char* h = std::getenv("RQHIP_SRC_LDS")) r.src_lds = (uint32_t)std::atoi(h);
         return r;
     }();
     return o;
