@@ -9,9 +9,7 @@
 #include "rq_colprog.hpp"
 
 #include <algorithm>
-#include <cstdlib>
 #include <cstring>
-#include <set>
 
 namespace rq {
 
@@ -348,135 +346,6 @@ struct Acc {
     }
 };
 
-// ---- register-pressure list scheduling ----
-// Reorders the IR (any topological order computes the same bytes) so that fewer values are live
-// at once: among the ready nodes, take the one whose result adds the fewest live values (operands
-// it consumes for the last time count against its own result); ties keep the construction order,
-// which is already demand-driven.  Mode 2 additionally holds source loads back until a node that
-// needs them is otherwise ready (a load is pulled in by its first consumer).
-uint32_t sched_mode() {
-    static const uint32_t m = [] {
-        const char* e = std::getenv("RQHIP_SCHED");
-        return e ? (uint32_t)std::atoi(e) : 0u;
-    }();
-    return m;
-}
-
-uint32_t push_mode() {
-    static const uint32_t m = [] {
-        const char* e = std::getenv("RQHIP_PUSH");
-        return e ? (uint32_t)std::atoi(e) : 0u;
-    }();
-    return m;
-}
-
-void schedule_pressure(ColIR* ir, uint32_t mode) {
-    const uint32_t n = (uint32_t)ir->nodes.size();
-    std::vector<std::vector<uint32_t>> cons(n);    // value -> unique consumer nodes
-    std::vector<uint32_t> missing(n, 0), rem(n, 0);
-    for (uint32_t i = 0; i < n; ++i) {
-        const IrNode& d = ir->nodes[i];
-        uint32_t ops[3] = {d.a, d.b, d.c};
-        for (int q = 0; q < 3; ++q) {
-            const uint32_t x = ops[q];
-            if (x == NOVAL) continue;
-            bool dup = false;
-            for (int p = 0; p < q; ++p) dup |= (ops[p] == x);
-            if (dup) continue;
-            cons[x].push_back(i);
-            ++missing[i];
-        }
-    }
-    for (uint32_t v = 0; v < n; ++v) rem[v] = (uint32_t)cons[v].size();
-    std::vector<uint8_t> done(n, 0), inready(n, 0);
-    auto delta = [&](uint32_t i) -> int {
-        const IrNode& d = ir->nodes[i];
-        int k = (d.k == IR_STORE || cons[i].empty()) ? 0 : 1;
-        uint32_t ops[3] = {d.a, d.b, d.c};
-        for (int q = 0; q < 3; ++q) {
-            const uint32_t x = ops[q];
-            if (x == NOVAL) continue;
-            bool dup = false;
-            for (int p = 0; p < q; ++p) dup |= (ops[p] == x);
-            if (!dup && rem[x] == 1) --k;
-        }
-        return k;
-    };
-    std::set<std::pair<int, uint32_t>> ready;      // (delta, original index)
-    std::vector<int> key(n, 0);
-    auto push = [&](uint32_t i) {
-        key[i] = delta(i);
-        ready.insert({key[i], i});
-        inready[i] = 1;
-    };
-    // mode 2: loads enter the ready set only when a consumer has nothing else missing
-    auto is_load = [&](uint32_t i) { return ir->nodes[i].k == IR_LOAD; };
-    for (uint32_t i = 0; i < n; ++i)
-        if (missing[i] == 0 && !(mode == 2 && is_load(i))) push(i);
-    std::vector<uint32_t> order;
-    order.reserve(n);
-    auto wake_loads = [&](uint32_t c) {  // mode 2: consumer c waits only for loads -> release them
-        if (mode != 2 || done[c]) return;
-        const IrNode& d = ir->nodes[c];
-        uint32_t need = 0, loads = 0;
-        for (uint32_t x : {d.a, d.b, d.c}) {
-            if (x == NOVAL || done[x]) continue;
-            ++need;
-            if (is_load(x)) ++loads;
-        }
-        if (need == 0 || need != loads) return;
-        for (uint32_t x : {d.a, d.b, d.c})
-            if (x != NOVAL && !done[x] && !inready[x]) push(x);
-    };
-    if (mode == 2)
-        for (uint32_t i = 0; i < n; ++i)
-            if (!is_load(i) && missing[i]) wake_loads(i);
-    while (!ready.empty()) {
-        const uint32_t i = ready.begin()->second;
-        ready.erase(ready.begin());
-        inready[i] = 0;
-        done[i] = 1;
-        order.push_back(i);
-        const IrNode& d = ir->nodes[i];
-        uint32_t ops[3] = {d.a, d.b, d.c};
-        for (int q = 0; q < 3; ++q) {
-            const uint32_t x = ops[q];
-            if (x == NOVAL) continue;
-            bool dup = false;
-            for (int p = 0; p < q; ++p) dup |= (ops[p] == x);
-            if (dup) continue;
-            if (--rem[x] == 1) {  // its last consumer now frees it: re-key that consumer
-                for (uint32_t c : cons[x])
-                    if (!done[c] && inready[c]) {
-                        ready.erase({key[c], c});
-                        key[c] = delta(c);
-                        ready.insert({key[c], c});
-                    }
-            }
-        }
-        for (uint32_t c : cons[i]) {
-            if (--missing[c] == 0) push(c);
-            else wake_loads(c);
-        }
-    }
-    if (order.size() != n) return;  // not a DAG (cannot happen): keep the construction order
-    std::vector<uint32_t> pos(n);
-    for (uint32_t j = 0; j < n; ++j) pos[order[j]] = j;
-    std::vector<IrNode> out(n);
-    for (uint32_t j = 0; j < n; ++j) {
-        IrNode d = ir->nodes[order[j]];
-        for (uint32_t* x : {&d.a, &d.b, &d.c})
-            if (*x != NOVAL) *x = pos[*x];
-        out[j] = d;
-    }
-    for (uint32_t& ph : ir->phase_start) {
-        uint32_t m = n;
-        for (uint32_t i = ph; i < n; ++i) m = std::min(m, pos[i]);
-        ph = m;
-    }
-    ir->nodes.swap(out);
-}
-
 // Output specification: the set of C columns XORed (XOR semantics) or a source row.
 struct OutDesc {
     bool source = false;
@@ -518,14 +387,10 @@ bool build(const Params& p, const std::vector<OutDesc>& outs, ColIR* ir, std::st
             }
             std::vector<uint32_t> t;
             t.push_back(D(e.piv_row[k]));
-            for (uint32_t j : e.deps[k])
-                if (!push_edge(j, k)) t.push_back(y[j]);
-            t.push_back(yacc[k].get(B));
+            for (uint32_t j : e.deps[k]) t.push_back(y[j]);
             y[k] = B.xsum(t);
             ystate[k] = 2;
             stk.pop_back();
-            for (uint32_t d : dependents[k])
-                if (push_edge(k, d)) yacc[d].push(B, y[k]);
         }
         return y[k0];
     };
@@ -663,7 +528,6 @@ bool build(const Params& p, const std::vector<OutDesc>& outs, ColIR* ir, std::st
         ir->nodes.swap(kept);
         std::memcpy(ir->phase_start, new_ph, sizeof new_ph);
     }
-    if (sched_mode()) schedule_pressure(ir, sched_mode());
     auto& st = ir->st;
     for (const IrNode& n : ir->nodes) {
         switch (n.k) {

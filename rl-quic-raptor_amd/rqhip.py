@@ -74,7 +74,14 @@ def lib():
     global _lib
     if _lib is None:
         if not LIB_PATH.exists():
-            raise RaptorQError(RQ_ERR_DEVICE, "librqhip.so not built (run `make -C rl-quic-raptor_amd`)")
+            # build on demand (hipcc cross-compiles gfx950 without a device); a failed build
+            # raises -- there is no CPU fallback behind this library
+            try:
+                build()
+            except (OSError, subprocess.CalledProcessError) as ex:
+                raise RaptorQError(RQ_ERR_DEVICE, "librqhip.so could not be built: %s" % ex) from ex
+            if not LIB_PATH.exists():
+                raise RaptorQError(RQ_ERR_DEVICE, "librqhip.so not built (run `make -C rl-quic-raptor_amd`)")
         L = ctypes.CDLL(str(LIB_PATH))
         u8p = ctypes.POINTER(ctypes.c_uint8)
         u16p = ctypes.POINTER(ctypes.c_uint16)
