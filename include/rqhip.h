@@ -97,8 +97,9 @@ typedef struct {
     const uint32_t* n_repair;    /* (host) [n_blocks] received repair symbols per block        */
     const uint32_t* repair_esi;  /* (host) concatenated repair ESIs (>= K), unique per block   */
     const void* repair;          /* (device) repair rows (T bytes each) in repair_esi order     */
-    int32_t* status;             /* (host out) [n_blocks]: 1 decoded, 0 rank-deficient,
-                                    RQ_ERR_NOT_ENOUGH if received < K, RQ_ERR_UNSUPPORTED       */
+    int32_t* status;             /* (host out) [n_blocks]: 1 decoded, 0 rank-deficient (every
+                                    received symbol considered), RQ_ERR_NOT_ENOUGH if received < K.
+                                    Any erasure count and any number of received repairs.       */
     void* stream;
 } rq_decode_desc;
 int rq_decode_batch(const rq_decode_desc* d);
@@ -148,6 +149,10 @@ int rq_debug_colprog_emulate(uint32_t K, uint32_t T, const uint32_t* esi, uint32
                              size_t* asm_len);
 /* Assemble the column program in process (amd_comgr) and return the code object size. */
 int rq_debug_colprog_assemble(uint32_t K, const uint32_t* esi, uint32_t n_out, size_t* code_bytes);
+/* Synchronous decodes first solve each block on its first e + margin received repairs (default 8)
+ * and re-solve on all of them only if that subset is rank-deficient.  Sets the margin (tests force
+ * the second pass with 0) and returns the previous one.  Results never depend on it. */
+uint32_t rq_debug_decode_margin(uint32_t margin);
 
 #ifdef __cplusplus
 }

@@ -13,6 +13,8 @@
 
 namespace rq {
 
+int g_lab = 0;  // experiment knob (lab tools only)
+
 namespace {
 
 using Bits = std::vector<uint64_t>;
@@ -103,6 +105,19 @@ bool eliminate(const Params& p, Elim* e, std::string* err) {
     };
     for (;;) {
         int32_t r = -1;
+        if ((g_lab & 1) && true) {
+            // lab: among degree-1 rows, the one whose active column is smallest
+            auto& bk = bucket[1];
+            uint32_t bestc = UINT32_MAX; size_t bi = 0;
+            for (size_t q = bhead[1]; q < bk.size(); ++q) {
+                const uint32_t x = bk[q];
+                if (rdone[x] || cnt[x] != 1) continue;
+                uint32_t ac = UINT32_MAX;
+                for (uint32_t c : rows[x]) if (cstate[c] == ACTIVE) { ac = c; break; }
+                if (ac < bestc) { bestc = ac; r = (int32_t)x; bi = q; }
+            }
+            if (r >= 0) { std::swap(bk[bi], bk[bhead[1]]); bhead[1]++; }
+        }
         for (uint32_t b = 1; b < 64 && r < 0; ++b) {
             auto& bk = bucket[b];
             while (bhead[b] < bk.size()) {

@@ -5,7 +5,15 @@
 // outputs) (rq_colprog.hpp, rq_colasm.hpp).  These kernels are the decode-side helpers around it
 // and the per-object GenSymbol gather.
 #pragma once
+#include <cstddef>
 #include <cstdint>
+
+#ifndef __host__
+#define __host__
+#endif
+#ifndef __device__
+#define __device__
+#endif
 
 namespace rq {
 
@@ -29,22 +37,32 @@ struct ZeroArgs {
     uint8_t* pack;              // k_pack_rows: row i of the list -> pack + i*T
 };
 
+// Per solved block bi (block b = blk_map[bi], e erased rows): X (e x xs bytes, xs = x_stride(e))
+// at xcoef + 64 * xoff[bi], X[k][m] at row m, byte k; the e received repairs it combines (indices
+// within the block) at xpiv + erased_off[b].
+__host__ __device__ inline uint32_t x_stride(uint32_t e) { return 64u * ((e + 63u) / 64u); }
+
 struct SolveArgs {
     const uint32_t* blk_map;    // grid.x -> block index
     const uint32_t* erased_off; // per block ranges into erased[]
     const uint32_t* erased;
-    const uint32_t* rep_off;    // per block ranges into rep_uidx[]
+    const uint32_t* rep_off;    // per block: first received repair row in rep_uidx[] / recv
+    const uint32_t* rep_cnt;    // per block: received repairs the solvers may use (the first rep_cnt[b])
     const uint32_t* rep_uidx;
     const uint8_t* mrep;
     uint32_t mrep_stride;
-    uint8_t* xcoef;             // per solved block: X[k][m] at xcoef[(m * xc_stride) + k]
-    uint16_t* xpiv;             // per solved block max_e received-repair indices (within the block)
+    uint8_t* xcoef;             // X of solved block bi at xcoef + 64 * xoff[bi]
+    const uint32_t* xoff;
+    uint16_t* xpiv;             // xpiv[erased_off[b] + m]: received repair (index within block b) of X row m
     int32_t* status;            // per block: 1 ok, 0 rank-deficient, ST_FALLBACK (general solver)
-    uint32_t max_e;
-    uint32_t xc_stride;         // bytes per m row of xcoef (64 * ceil(max_e / 64))
+    uint8_t* gws;               // general solver: basis of block bi at gws + 64 * goff[bi] when e > lds_e
+    const uint32_t* goff;
+    uint32_t lds_e;             // largest e whose basis the general solver keeps in LDS
 };
 constexpr int32_t ST_PENDING = -100;   // queued for the solver
-constexpr int32_t ST_FALLBACK = -101;  // beyond the one-wave solver: general solver decides
+constexpr int32_t ST_FALLBACK = -101;  // beyond the fast solvers: the general solver decides
+// General-solver basis row width (coefficients then combination of selected rows), 16-byte aligned.
+__host__ __device__ inline uint32_t basis_width(uint32_t e) { return (2u * e + 15u) & ~15u; }
 
 struct ApplyArgs {
     const uint32_t* blk_map;
@@ -56,13 +74,13 @@ struct ApplyArgs {
     const uint8_t* r0;          // n_union rows of T bytes per block
     uint32_t n_union;
     const uint8_t* xcoef;
+    const uint32_t* xoff;
     const uint16_t* xpiv;
     const int32_t* status;
     uint8_t* data;
     uint64_t data_stride;
     uint32_t T;
-    uint32_t max_e;
-    uint32_t xc_stride;
+    uint32_t max_e;             // largest e of the batch (slice sizing)
 };
 
 // Launchers (rq_kernels.hip).  Return hipError_t as int.
@@ -70,12 +88,15 @@ int launch_zero_rows(const ZeroArgs& a, void* stream);
 // Host-memory decode: copy the recovered rows (the same (blk, row) list) into a dense buffer so only
 // e*T bytes per block travel back over PCIe.
 int launch_pack_rows(const ZeroArgs& a, void* stream);
-// Fast one-wave solve (e <= 64, first 64 received repairs), then the general solver for the
-// blocks it deferred (lds_bytes sized for the largest e + nr of the batch).
-int launch_solve(const SolveArgs& a, uint32_t n_blocks, uint32_t lds_bytes, bool need_general, void* stream);
+// Fast solves (e <= 64 on the first 64 received repairs, e <= 128 on the first 128), then the
+// general solver (any e, every received repair) for the blocks they deferred.
+int launch_solve(const SolveArgs& a, uint32_t n_blocks, bool need_general, uint32_t max_lds_e, void* stream);
 int launch_apply(const ApplyArgs& a, uint32_t n_strips, uint32_t n_blocks, void* stream);
 int launch_gather(const DevParams& p, const uint8_t* C, uint32_t T, const uint32_t* esi, uint32_t n, uint8_t* out,
                   void* stream);
+// General-solver working set for e erased rows; the largest e it keeps in LDS.
+size_t solve_ws_bytes(uint32_t e);
+uint32_t solve_lds_e_max();
 int upload_tables();  // rand / degree tables to __constant__ memory (once per device)
 
 }  // namespace rq

@@ -98,7 +98,7 @@ struct HostBuf {
 // Per-stream workspaces: kernels of calls on different streams may run concurrently, so every
 // stream gets its own scratch / index / syndrome buffers (calls on one stream are ordered).
 struct Workspace {
-    DevBuf r0, xb, xp, scratch;
+    DevBuf r0, xb, xp, gws, scratch;
     DevBuf pk;                      // host-memory decode: recovered rows, packed for the D2H
     HostBuf h_status, h_pack;
     // decode descriptors, double-buffered so that rq_decode_batch_async can return before its upload
@@ -367,77 +367,83 @@ int ensure_mrep(DevCtx* ctx, ColKernel* k, void* stream) {
     return RQ_OK;
 }
 
-constexpr uint32_t MAX_E = 255;  // decode-solve limits (LDS-resident [M | I])
-
-// Optional decode output for host-memory batches: the recovered rows of `blocks` (the solved
-// blocks, ascending; their erased rows in erased[] order) packed T bytes apart in pinned memory.
+// Optional decode output for host-memory batches: the recovered rows of `blocks` (the blocks that
+// decoded, in the order they did; each block's erased rows in erased[] order), T bytes apart.
 struct PackOut {
-    const uint8_t* rows = nullptr;
+    std::vector<uint8_t> rows;
     std::vector<uint32_t> blocks;
 };
 
-// Batched syndrome decode.  Caller holds ctx->mu.  Host arrays as in rq_decode_desc.
-int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, void* data, uint64_t data_stride,
-                  const uint32_t* n_erased, const uint32_t* erased, const uint32_t* n_repair,
-                  const uint32_t* repair_esi, const void* repair, int32_t* status, void* stream,
-                  PackOut* po = nullptr, bool async = false) {
+// Synchronous decodes offer the solvers the first e + SUBSET_MARGIN received repairs of a block
+// first: any e independent received rows determine x_E, so the subset changes no byte, and it keeps
+// the column program's output set (and r0) small.  A block whose subset is rank-deficient while it
+// received more repairs is solved again on all of them, so ok/fail matches the reference, which
+// solves with every held symbol (RQ/decoder.go:93-121).
+uint32_t g_subset_margin = 8;  // rq_debug_decode_margin lets the tests force the second pass
+
+uint32_t lds_e_max() {
+    static const uint32_t v = solve_lds_e_max();
+    return v;
+}
+
+// One solve pass over the blocks of `blocks` (each pending; cnt[b] = candidate repairs offered).
+// Caller holds ctx->mu.  Host arrays as in rq_decode_desc.
+int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, void* data, uint64_t data_stride,
+                const std::vector<uint32_t>& eoff, const uint32_t* erased, const std::vector<uint32_t>& roff,
+                const uint32_t* repair_esi, const std::vector<uint32_t>& cnt, const std::vector<uint32_t>& blk_map,
+                const void* repair, int32_t* status, void* stream, PackOut* po, bool async) {
     int rc;
-    std::vector<uint32_t> blk_map, eoff(n_blocks + 1, 0), roff(n_blocks + 1, 0);
-    size_t max_lds_solve = 0;
-    uint32_t max_e = 0;
-    bool need_general = false;  // some block may exceed the one-wave solver (e or nr > 64)
-    for (uint32_t b = 0; b < n_blocks; ++b) {
-        eoff[b + 1] = eoff[b] + n_erased[b];
-        roff[b + 1] = roff[b] + n_repair[b];
-    }
-    std::vector<uint32_t> cand;
-    for (uint32_t b = 0; b < n_blocks; ++b) {
-        const uint32_t e = n_erased[b], nr = n_repair[b];
-        for (uint32_t i = eoff[b]; i < eoff[b + 1]; ++i)
-            if (erased[i] >= p.K) return fail(RQ_ERR_BAD_ARG, "erased ESI >= K");
-        for (uint32_t i = roff[b]; i < roff[b + 1]; ++i)
-            if (repair_esi[i] < p.K) return fail(RQ_ERR_BAD_ARG, "repair ESI < K");
-        if ((p.K - e) + nr < p.K) { status[b] = RQ_ERR_NOT_ENOUGH; continue; }
-        if (e == 0) { status[b] = 1; continue; }
-        const size_t need = (size_t)nr * (e + nr);
-        if (e > MAX_E || nr > 255 || need > 140 * 1024) { status[b] = RQ_ERR_UNSUPPORTED; continue; }
-        status[b] = ST_PENDING;
-        need_general |= (e > 64 || nr > 64);
-        blk_map.push_back(b);
-        max_lds_solve = std::max(max_lds_solve, need);
-        max_e = std::max(max_e, e);
-        cand.insert(cand.end(), repair_esi + roff[b], repair_esi + roff[b + 1]);
-    }
     const uint32_t nw = (uint32_t)blk_map.size();
-    if (nw == 0) return RQ_OK;
+    uint32_t max_e = 0, max_lds_e = 0;
+    bool need_general = false;  // some block may reach the general solver (e or candidates > 64)
+    std::vector<uint32_t> cand;
+    std::vector<uint32_t> xoff(nw), goff(nw);
+    uint64_t xo = 0, go = 0;
+    for (uint32_t bi = 0; bi < nw; ++bi) {
+        const uint32_t b = blk_map[bi], e = eoff[b + 1] - eoff[b];
+        max_e = std::max(max_e, e);
+        if (e <= lds_e_max()) max_lds_e = std::max(max_lds_e, e);
+        need_general |= (e > 64 || cnt[b] > 64);
+        cand.insert(cand.end(), repair_esi + roff[b], repair_esi + roff[b] + cnt[b]);
+        xoff[bi] = (uint32_t)xo;
+        xo += ((uint64_t)e * x_stride(e) + 63) / 64;
+        goff[bi] = (uint32_t)go;
+        if (e > lds_e_max()) go += (solve_ws_bytes(e) + 63) / 64;
+    }
+    if (xo >= (1ull << 32) || go >= (1ull << 32)) return fail(RQ_ERR_UNSUPPORTED, "decode workspace beyond 256 GiB");
     const std::vector<uint32_t> uni = decode_union(p.K, cand);
     ColKernel* k;
     if ((rc = get_col_kernel(ctx, p, uni.data(), (uint32_t)uni.size(), false, &k))) return rc;
     if ((rc = ensure_mrep(ctx, k, stream))) return rc;
-    // union index of every received repair: direct for a dense union, binary search otherwise
+    // union index of every candidate repair: direct for a dense union, binary search otherwise
     const bool dense_uni = uni.back() - uni.front() + 1 == uni.size();
     const size_t n_er = eoff[n_blocks], n_rep = roff[n_blocks];
-    // index workspace: blk_map | eoff | roff | erased | rep_uidx | status | zero (blk, row) lists
+    // index workspace: blk_map | eoff | roff | cnt | erased | rep_uidx | status | zero (blk, row) | xoff | goff
     std::vector<uint32_t> idx;
-    idx.reserve(nw + 2 * (n_blocks + 1) + n_er * 3 + n_rep + n_blocks);
+    idx.reserve(nw * 3 + 3 * (n_blocks + 1) + n_er * 3 + n_rep + n_blocks);
     const size_t o_map = 0;
     idx.insert(idx.end(), blk_map.begin(), blk_map.end());
     const size_t o_eoff = idx.size();
     idx.insert(idx.end(), eoff.begin(), eoff.end());
     const size_t o_roff = idx.size();
     idx.insert(idx.end(), roff.begin(), roff.end());
+    const size_t o_cnt = idx.size();
+    idx.insert(idx.end(), cnt.begin(), cnt.end());
     const size_t o_er = idx.size();
     idx.insert(idx.end(), erased, erased + n_er);
     const size_t o_ru = idx.size();
-    for (size_t i = 0; i < n_rep; ++i) {
-        const uint32_t x = repair_esi[i];
-        if (dense_uni) {
-            idx.push_back(x >= uni.front() && x - uni.front() < uni.size() ? x - uni.front() : 0u);
-        } else {
-            const auto it = std::lower_bound(uni.begin(), uni.end(), x);
-            idx.push_back(it != uni.end() && *it == x ? (uint32_t)(it - uni.begin()) : 0u);
+    idx.resize(idx.size() + n_rep, 0);
+    for (uint32_t b : blk_map)
+        for (uint32_t i = roff[b]; i < roff[b] + cnt[b]; ++i) {
+            const uint32_t x = repair_esi[i];
+            uint32_t u;
+            if (dense_uni) {
+                u = x - uni.front();
+            } else {
+                u = (uint32_t)(std::lower_bound(uni.begin(), uni.end(), x) - uni.begin());
+            }
+            idx[o_ru + i] = u;
         }
-    }
     const size_t o_st = idx.size();  // device status: host-decided values, ST_PENDING for the rest
     for (uint32_t b = 0; b < n_blocks; ++b) idx.push_back((uint32_t)status[b]);
     const size_t o_zb = idx.size();
@@ -447,6 +453,10 @@ int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, v
     const size_t o_zr = idx.size();
     for (uint32_t b : blk_map)
         for (uint32_t i = eoff[b]; i < eoff[b + 1]; ++i) idx.push_back(erased[i]);
+    const size_t o_xo = idx.size();
+    idx.insert(idx.end(), xoff.begin(), xoff.end());
+    const size_t o_go = idx.size();
+    idx.insert(idx.end(), goff.begin(), goff.end());
     // descriptor upload through pinned staging, queued behind the caller's work on the stream (e.g.
     // the encode that produced `repair`) without blocking this thread.  (A separate copy stream
     // overlapping the upload with that work measured slower with rq_decode_batch_async.)
@@ -466,10 +476,10 @@ int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, v
     HIP_TRY(hipMemcpyAsync(w->idx[set].p, w->h_idx[set].p, idx.size() * 4, hipMemcpyHostToDevice, (hipStream_t)stream));
     HIP_TRY(hipEventRecord(w->up[set], (hipStream_t)stream));
     const uint32_t* di = w->idx[set].as<uint32_t>();
-    const uint32_t xc_stride = 64 * ((max_e + 63) / 64);
     if ((rc = w->r0.ensure((size_t)n_blocks * uni.size() * T))) return rc;
-    if ((rc = w->xb.ensure((size_t)nw * max_e * xc_stride))) return rc;
-    if ((rc = w->xp.ensure((size_t)nw * max_e * 2))) return rc;
+    if ((rc = w->xb.ensure((size_t)xo * 64))) return rc;
+    if ((rc = w->xp.ensure(std::max<size_t>(n_er, 1) * 2))) return rc;
+    if (go && (rc = w->gws.ensure((size_t)go * 64))) return rc;
 
     // 1) erased rows := 0, then r0 = the column program on every block (syndromes s = r ^ r0)
     ZeroArgs z;
@@ -484,16 +494,18 @@ int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, v
     s.erased_off = di + o_eoff;
     s.erased = di + o_er;
     s.rep_off = di + o_roff;
+    s.rep_cnt = di + o_cnt;
     s.rep_uidx = di + o_ru;
     s.mrep = k->mrep.as<uint8_t>();
     s.mrep_stride = k->mrep_stride;
     s.xcoef = w->xb.as<uint8_t>();
+    s.xoff = di + o_xo;
     s.xpiv = w->xp.as<uint16_t>();
     s.status = reinterpret_cast<int32_t*>(w->idx[set].as<uint32_t>() + o_st);
-    s.max_e = max_e;
-    s.xc_stride = xc_stride;
-    if (launch_solve(s, nw, (uint32_t)((max_lds_solve + 15) & ~size_t(15)), need_general, stream))
-        return fail(RQ_ERR_DEVICE, "k_solve launch failed");
+    s.gws = w->gws.as<uint8_t>();
+    s.goff = di + o_go;
+    s.lds_e = lds_e_max();
+    if (launch_solve(s, nw, need_general, max_lds_e, stream)) return fail(RQ_ERR_DEVICE, "k_solve launch failed");
     // 3) apply: x_E = X * s
     ApplyArgs ap;
     ap.blk_map = di + o_map;
@@ -505,22 +517,20 @@ int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, v
     ap.r0 = w->r0.as<uint8_t>();
     ap.n_union = (uint32_t)uni.size();
     ap.xcoef = s.xcoef;
+    ap.xoff = s.xoff;
     ap.xpiv = s.xpiv;
     ap.status = s.status;
     ap.data = static_cast<uint8_t*>(data);
     ap.data_stride = data_stride;
     ap.T = T;
     ap.max_e = max_e;
-    ap.xc_stride = xc_stride;
     if (launch_apply(ap, (T / 4 + 63) / 64, nw, stream)) return fail(RQ_ERR_DEVICE, "k_apply launch failed");
+    const size_t pack_bytes = (size_t)nz * T;
     if (po) {
-        const size_t bytes = (size_t)nz * T;
-        if ((rc = w->pk.ensure(bytes)) || (rc = w->h_pack.ensure(bytes))) return rc;
+        if ((rc = w->pk.ensure(pack_bytes)) || (rc = w->h_pack.ensure(pack_bytes))) return rc;
         z.pack = w->pk.as<uint8_t>();
         if (launch_pack_rows(z, stream)) return fail(RQ_ERR_DEVICE, "k_pack_rows launch failed");
-        HIP_TRY(hipMemcpyAsync(w->h_pack.p, w->pk.p, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
-        po->rows = static_cast<const uint8_t*>(w->h_pack.p);
-        po->blocks = blk_map;
+        HIP_TRY(hipMemcpyAsync(w->h_pack.p, w->pk.p, pack_bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
     }
     if (async) {  // statuses land in the caller's pinned array when the stream gets here
         HIP_TRY(hipMemcpyAsync(status, w->idx[set].as<uint32_t>() + o_st, n_blocks * 4, hipMemcpyDeviceToHost,
@@ -534,7 +544,61 @@ int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, v
     HIP_TRY(hipEventRecord(w->used[set], (hipStream_t)stream));
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
     for (uint32_t b : blk_map) status[b] = st[b];
+    if (po) {
+        const uint8_t* rows = static_cast<const uint8_t*>(w->h_pack.p);
+        size_t r = 0;
+        for (uint32_t b : blk_map) {
+            const size_t nb = (size_t)(eoff[b + 1] - eoff[b]) * T;
+            if (status[b] == 1) {
+                po->blocks.push_back(b);
+                po->rows.insert(po->rows.end(), rows + r, rows + r + nb);
+            }
+            r += nb;
+        }
+    }
     return RQ_OK;
+}
+
+// Batched syndrome decode.  Caller holds ctx->mu.  Host arrays as in rq_decode_desc.  Sync calls run
+// the subset pass and, for blocks whose subset was rank-deficient, the all-repairs pass (see
+// g_subset_margin); async calls offer every received repair in one pass (no host decision between
+// passes).
+int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, void* data, uint64_t data_stride,
+                  const uint32_t* n_erased, const uint32_t* erased, const uint32_t* n_repair,
+                  const uint32_t* repair_esi, const void* repair, int32_t* status, void* stream,
+                  PackOut* po = nullptr, bool async = false) {
+    std::vector<uint32_t> eoff(n_blocks + 1, 0), roff(n_blocks + 1, 0);
+    for (uint32_t b = 0; b < n_blocks; ++b) {
+        eoff[b + 1] = eoff[b] + n_erased[b];
+        roff[b + 1] = roff[b] + n_repair[b];
+    }
+    std::vector<uint32_t> blk_map, cnt(n_blocks, 0);
+    for (uint32_t b = 0; b < n_blocks; ++b) {
+        const uint32_t e = n_erased[b], nr = n_repair[b];
+        for (uint32_t i = eoff[b]; i < eoff[b + 1]; ++i)
+            if (erased[i] >= p.K) return fail(RQ_ERR_BAD_ARG, "erased ESI >= K");
+        for (uint32_t i = roff[b]; i < roff[b + 1]; ++i)
+            if (repair_esi[i] < p.K) return fail(RQ_ERR_BAD_ARG, "repair ESI < K");
+        if (e > nr) { status[b] = RQ_ERR_NOT_ENOUGH; continue; }  // (K - e) + nr < K held symbols
+        if (e == 0) { status[b] = 1; continue; }
+        status[b] = ST_PENDING;
+        cnt[b] = async ? nr : std::min(nr, e + g_subset_margin);
+        blk_map.push_back(b);
+    }
+    if (blk_map.empty()) return RQ_OK;
+    int rc = decode_pass(ctx, p, T, n_blocks, data, data_stride, eoff, erased, roff, repair_esi, cnt, blk_map, repair,
+                         status, stream, po, async);
+    if (rc || async) return rc;
+    std::vector<uint32_t> again;
+    for (uint32_t b : blk_map)
+        if (status[b] == 0 && cnt[b] < n_repair[b]) {
+            cnt[b] = n_repair[b];
+            status[b] = ST_PENDING;
+            again.push_back(b);
+        }
+    if (again.empty()) return RQ_OK;
+    return decode_pass(ctx, p, T, n_blocks, data, data_stride, eoff, erased, roff, repair_esi, cnt, again, repair,
+                       status, stream, po, false);
 }
 
 // ---------------- host-memory batches (rq_encode_batch_host / rq_decode_batch_host) ----------------
@@ -634,12 +698,12 @@ int decode_host_shard(int dev, const rq_decode_desc& d, const Params& p, uint32_
         if ((rc = decode_locked(ctx, p, d.T, nb, st.in.p, blk_b, d.n_erased + b, d.erased + eoff[b], d.n_repair + b,
                                 d.repair_esi + roff[b], st.out.p, d.status + b, st.s, &po)))
             return rc;
-        size_t r = 0;
+        size_t r = 0;  // po holds the recovered rows of the blocks that decoded
         for (uint32_t lb : po.blocks) {
             const uint32_t gb = b + lb;
             uint8_t* dst = static_cast<uint8_t*>(d.data) + gb * d.data_stride;
             for (uint64_t i = eoff[gb]; i < eoff[gb + 1]; ++i, ++r)
-                if (d.status[gb] == 1) std::memcpy(dst + (uint64_t)d.erased[i] * d.T, po.rows + r * d.T, d.T);
+                std::memcpy(dst + (uint64_t)d.erased[i] * d.T, po.rows.data() + r * d.T, d.T);
         }
     }
     return RQ_OK;
@@ -818,6 +882,12 @@ int rq_debug_colprog_assemble(uint32_t K, const uint32_t* esi, uint32_t n_out, s
     if (!comgr_assemble(emit_colprog_asm(mp, "rq_colprog"), &co, &err)) return fail(RQ_ERR_PLAN, err);
     if (code_bytes) *code_bytes = co.size();
     return RQ_OK;
+}
+
+uint32_t rq_debug_decode_margin(uint32_t margin) {
+    const uint32_t old = g_subset_margin;
+    g_subset_margin = margin;
+    return old;
 }
 
 int rq_encode_batch(const rq_encode_desc* d) {
@@ -1050,7 +1120,6 @@ int rq_decoder_decode(rq_dec* d, uint8_t* out, int* ok) {
         int32_t st = 0;
         rc = decode_locked(ctx, d->p, Tp, 1, dd.p, data.size(), &ne, erased.data(), &nr, resi.data(), dr.p, &st, nullptr);
         if (rc) return rc;
-        if (st == RQ_ERR_UNSUPPORTED) return fail(RQ_ERR_UNSUPPORTED, "erasure pattern beyond the device solver limits");
         if (st != 1) return RQ_OK;  // rank-deficient: (false, nil, nil)
         HIP_TRY(hipMemcpy(data.data(), dd.p, data.size(), hipMemcpyDeviceToHost));
         for (uint32_t i : erased) std::memcpy(&d->fast[(size_t)i * T], &data[(size_t)i * Tp], T);

@@ -178,7 +178,7 @@ __global__ void __launch_bounds__(256) k_solve_fast(SolveArgs a) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
     if (RPL > 1 && a.status[b] != ST_FALLBACK) return;  // the wide pass takes deferred blocks only
     const uint32_t e = a.erased_off[b + 1] - a.erased_off[b];
-    const uint32_t nr = a.rep_off[b + 1] - a.rep_off[b];
+    const uint32_t nr = a.rep_cnt[b];
     if (e > NROWS) {
         if (tid == 0) a.status[b] = ST_FALLBACK;
         return;
@@ -262,81 +262,112 @@ __global__ void __launch_bounds__(256) k_solve_fast(SolveArgs a) {
         __syncthreads();
     }
     // X[k][m] = identity byte (e + piv_m) of pivot row piv_k
-    uint8_t* xc = a.xcoef + (size_t)blockIdx.x * a.max_e * a.xc_stride;
-    uint16_t* XP = a.xpiv + (size_t)blockIdx.x * a.max_e;
+    uint8_t* xc = a.xcoef + 64ull * a.xoff[blockIdx.x];
+    const uint32_t xs = x_stride(e);
+    uint16_t* XP = a.xpiv + a.erased_off[b];
     for (uint32_t m = tid; m < e; m += NT) XP[m] = pivl[m];
     for (uint32_t idx = tid; idx < e * e; idx += NT) {
         const uint32_t m = idx / e, k = idx - m * e;
-        xc[m * a.xc_stride + k] = rb[pivl[k] * SW * 4 + e + pivl[m]];
+        xc[m * xs + k] = rb[pivl[k] * SW * 4 + e + pivl[m]];
     }
     if (tid == 0) a.status[b] = 1;
 }
 
-// General solver (any e, nr with nr*(e+nr) bytes in LDS) for the blocks the fast solvers deferred.
+// General solver for the blocks the fast solvers deferred: any e, every received repair.  The
+// received rows are taken in order and reduced against a Gauss-Jordan basis of the rows kept so far
+// (basis row i: pivot column pc[i], coefficients zero on every other pivot column, then the
+// combination of selected received rows it stands for); a row that reduces to zero is dependent and
+// skipped, the others extend the basis, until e rows are kept (rank e: the block decodes, and X is
+// the combination part) or the rows run out (rank-deficient: Decode returns (false, nil, nil),
+// RQ/decoder.go:120-121).  The working set is e x 2e bytes whatever the number of received repairs:
+// in LDS for e <= lds_e, else in a global workspace.  Replaces GaussianElimination
+// (RQ/discmath/gauss.go:7-45) on the e erased columns.
 __global__ void __launch_bounds__(256) k_solve(SolveArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
     __shared__ uint8_t ex[512], lg[256];
-    __shared__ uint8_t fac[256];
-    __shared__ uint16_t rowid[256];
     __shared__ int piv;
-    const uint32_t b = a.blk_map[blockIdx.x];
+    const uint32_t bi = blockIdx.x, b = a.blk_map[bi];
     if (a.status[b] != ST_FALLBACK) return;
     const uint32_t tid = threadIdx.x, nthr = blockDim.x;
     const uint32_t e = a.erased_off[b + 1] - a.erased_off[b];
-    const uint32_t nr = a.rep_off[b + 1] - a.rep_off[b];
+    const uint32_t nr = a.rep_cnt[b];
     const uint32_t* E = a.erased + a.erased_off[b];
     const uint32_t* U = a.rep_uidx + a.rep_off[b];
-    const uint32_t ws = e + nr;
+    const uint32_t W2 = basis_width(e);
+    // v (W2) | coefficient of v on each basis row (e) | pc (e x u16) | rowid (e x u16) | basis (e x W2):
+    // in LDS for e <= lds_e, else in this block's global workspace (solve_ws_bytes(e))
+    uint8_t* v = (e <= a.lds_e) ? sm : a.gws + 64ull * a.goff[bi];
+    uint8_t* cf = v + W2;
+    uint16_t* pc = reinterpret_cast<uint16_t*>(cf + ((e + 15) & ~15u));
+    uint16_t* rowid = pc + ((e + 7) & ~7u);
+    uint8_t* A = reinterpret_cast<uint8_t*>(rowid + ((e + 7) & ~7u));
     gf_tables_copy(ex, lg);
-    for (uint32_t r = tid; r < nr; r += nthr) rowid[r] = (uint16_t)r;
-    for (uint32_t idx = tid; idx < nr * ws; idx += nthr) {
-        const uint32_t j = idx / ws, k = idx - j * ws;
-        sm[idx] = (k < e) ? a.mrep[(size_t)U[j] * a.mrep_stride + E[k]] : (uint8_t)(k - e == j);
-    }
     __syncthreads();
-    for (uint32_t k = 0; k < e; ++k) {
-        if (tid == 0) piv = (int)nr;
+    auto gm = [&](uint8_t x, uint8_t y) -> uint8_t { return (x && y) ? ex[lg[x] + lg[y]] : (uint8_t)0; };
+    uint32_t np = 0;
+    for (uint32_t j = 0; j < nr && np < e; ++j) {
+        const uint8_t* mr = a.mrep + (size_t)U[j] * a.mrep_stride;
+        for (uint32_t c = tid; c < W2; c += nthr) v[c] = (c < e) ? mr[E[c]] : (uint8_t)(c == e + np);
         __syncthreads();
-        for (uint32_t r = k + tid; r < nr; r += nthr)
-            if (sm[r * ws + k]) atomicMin(&piv, (int)r);
+        for (uint32_t i = tid; i < np; i += nthr) cf[i] = v[pc[i]];
+        if (tid == 0) piv = (int)e;
+        __syncthreads();
+        // v ^= sum_i cf[i] * basis_i (basis rows vanish on each other's pivot columns)
+        for (uint32_t c = tid; c < W2; c += nthr) {
+            uint8_t x = v[c];
+            for (uint32_t i = 0; i < np; ++i) {
+                const uint8_t f = cf[i];
+                if (f) x ^= gm(f, A[(size_t)i * W2 + c]);
+            }
+            v[c] = x;
+            if (c < e && x) atomicMin(&piv, (int)c);
+        }
         __syncthreads();
         const uint32_t p = (uint32_t)piv;
-        if (p >= nr) {
-            if (tid == 0) a.status[b] = 0;
-            return;
-        }
-        if (p != k) {
-            for (uint32_t c = tid; c < ws; c += nthr) {
-                const uint8_t t = sm[p * ws + c]; sm[p * ws + c] = sm[k * ws + c]; sm[k * ws + c] = t;
-            }
-            if (tid == 0) { const uint16_t t = rowid[p]; rowid[p] = rowid[k]; rowid[k] = t; }
+        if (p >= e) {  // dependent on the rows kept so far
             __syncthreads();
+            continue;
         }
-        const uint8_t pv = sm[k * ws + k];
-        const uint8_t inv = ex[255 - lg[pv]];
+        const uint8_t inv = ex[255 - lg[v[p]]];
         __syncthreads();
-        for (uint32_t c = k + tid; c < ws; c += nthr) sm[k * ws + c] = gmul_t(lg, ex, sm[k * ws + c], inv);
-        for (uint32_t r = tid; r < nr; r += nthr) fac[r] = (r == k) ? 0 : sm[r * ws + k];
+        for (uint32_t c = tid; c < W2; c += nthr) v[c] = gm(v[c], inv);
         __syncthreads();
-        for (uint32_t idx = tid; idx < nr * (ws - k); idx += nthr) {
-            const uint32_t r = idx / (ws - k), c = k + (idx - r * (ws - k));
-            const uint8_t f = fac[r];
-            if (f) sm[r * ws + c] ^= gmul_t(lg, ex, f, sm[k * ws + c]);
+        // clear column p from the basis, then append v
+        for (size_t idx = tid; idx < (size_t)np * W2; idx += nthr) {
+            const uint32_t i = (uint32_t)(idx / W2), c = (uint32_t)(idx - (size_t)i * W2);
+            const uint8_t f = A[(size_t)i * W2 + p];
+            if (f && c != p) A[idx] ^= gm(f, v[c]);
         }
+        __syncthreads();
+        for (uint32_t i = tid; i < np; i += nthr) A[(size_t)i * W2 + p] = 0;
+        for (uint32_t c = tid; c < W2; c += nthr) A[(size_t)np * W2 + c] = v[c];
+        if (tid == 0) { pc[np] = (uint16_t)p; rowid[np] = (uint16_t)j; }
+        ++np;
         __syncthreads();
     }
-    uint8_t* xc = a.xcoef + (size_t)blockIdx.x * a.max_e * a.xc_stride;
-    uint16_t* XP = a.xpiv + (size_t)blockIdx.x * a.max_e;
+    if (np < e) {
+        if (tid == 0) a.status[b] = 0;
+        return;
+    }
+    // basis row i solves erased column pc[i]: x_pc[i] = sum_m A[i][e + m] s_rowid[m]
+    uint8_t* xc = a.xcoef + 64ull * a.xoff[bi];
+    const uint32_t xs = x_stride(e);
+    uint16_t* XP = a.xpiv + a.erased_off[b];
     for (uint32_t m = tid; m < e; m += nthr) XP[m] = rowid[m];
-    __syncthreads();
-    for (uint32_t idx = tid; idx < e * e; idx += nthr) {
-        const uint32_t m = idx / e, k = idx - m * e;
-        xc[m * a.xc_stride + k] = sm[k * ws + e + rowid[m]];
+    for (size_t idx = tid; idx < (size_t)e * e; idx += nthr) {
+        const uint32_t i = (uint32_t)(idx / e), m = (uint32_t)(idx - (size_t)i * e);
+        xc[(size_t)m * xs + pc[i]] = A[(size_t)i * W2 + e + m];
     }
     if (tid == 0) a.status[b] = 1;
 }
 
-int launch_solve(const SolveArgs& a, uint32_t n_blocks, uint32_t lds_bytes, bool need_general, void* stream) {
+// k_solve's working set for e erased rows (LDS when e <= lds_e, else global workspace).
+size_t solve_ws_bytes(uint32_t e) {
+    const uint32_t W2 = basis_width(e);
+    return W2 + ((e + 15) & ~15u) + 4 * ((e + 7) & ~7u) + (size_t)e * W2;
+}
+
+int launch_solve(const SolveArgs& a, uint32_t n_blocks, bool need_general, uint32_t max_lds_e, void* stream) {
     hipLaunchKernelGGL(k_solve_fast<1>, dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !need_general) return (int)e;
@@ -347,8 +378,15 @@ int launch_solve(const SolveArgs& a, uint32_t n_blocks, uint32_t lds_bytes, bool
         (void)hipFuncSetAttribute((const void*)k_solve, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
         attr = true;
     }
-    hipLaunchKernelGGL(k_solve, dim3(n_blocks), dim3(256), lds_bytes, (hipStream_t)stream, a);
+    const size_t lds = solve_ws_bytes(std::min<uint32_t>(max_lds_e, a.lds_e));
+    hipLaunchKernelGGL(k_solve, dim3(n_blocks), dim3(256), lds, (hipStream_t)stream, a);
     return (int)hipGetLastError();
+}
+
+uint32_t solve_lds_e_max() {
+    uint32_t e = 1;
+    while (solve_ws_bytes(e + 1) <= 140 * 1024) ++e;
+    return e;
 }
 
 // ------------------------------ decode: x_E = X * s ------------------------------------------
@@ -380,10 +418,11 @@ __device__ __forceinline__ void perm_tables(uint32_t c, uint4* A, uint32_t* B) {
 // (w / 8) % np of unit (w / 8np) * 8 + w % 8: the slices of one unit share an XCD (workgroups are
 // dealt to the 8 XCDs round-robin) and are dispatched together, so their common syndrome rows are
 // read from HBM once and hit L2 after.  Each lane owns CPL dword columns (64 apart: every
-// load/store instruction is one contiguous 256-B segment).  The slice's tables for all m are
-// built from X straight into LDS (perm_tables): A = the four 8-entry halves (b128), B = the 2-bit table.
+// load/store instruction is one contiguous 256-B segment).  The slice's tables are built from X
+// straight into LDS (perm_tables: A = the four 8-entry halves (b128), B = the 2-bit table), for
+// MC syndromes m at a time (one chunk whenever e <= MC).
 template <int KC, int CPL>
-__global__ void __launch_bounds__(64) k_apply(ApplyArgs a, uint32_t n_units, uint32_t np) {
+__global__ void __launch_bounds__(64) k_apply(ApplyArgs a, uint32_t n_units, uint32_t np, uint32_t MC) {
     extern __shared__ __attribute__((aligned(16))) uint32_t xsh[];
     const uint32_t strips = ((a.T >> 2) + 64 * CPL - 1) / (64 * CPL);
     const uint32_t w = blockIdx.x, slice = (w / 8) % np, unit = (w / (8 * np)) * 8 + (w & 7);
@@ -397,30 +436,18 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a, uint32_t n_units, uin
     if (k0 >= e) return;
     const uint32_t Td = a.T >> 2;
     const uint32_t* E = a.erased + a.erased_off[b];
-    const uint16_t* XP = a.xpiv + (size_t)bi * a.max_e;
+    const uint16_t* XP = a.xpiv + a.erased_off[b];
     const uint32_t r0b = a.rep_off[b];
     const uint32_t* recv = reinterpret_cast<const uint32_t*>(a.recv);
     const uint32_t* r0 = reinterpret_cast<const uint32_t*>(a.r0) + (size_t)b * a.n_union * Td;
     uint8_t* blk = a.data + (size_t)b * a.data_stride;
-    uint4* tA = reinterpret_cast<uint4*>(xsh);                  // [m][KC]
-    uint32_t* tB = xsh + (size_t)e * KC * 4;                     // [m][KC]
-    uint32_t* offr = tB + (size_t)e * KC;
-    uint32_t* off0 = offr + e;
-    const uint8_t* xc = a.xcoef + (size_t)bi * a.max_e * a.xc_stride;
-    for (uint32_t idx = lane; idx < e * KC; idx += 64) {
-        const uint32_t m = idx / KC, k = idx - m * KC;
-        uint4 A = make_uint4(0, 0, 0, 0);
-        uint32_t B = 0;
-        if (k0 + k < e) perm_tables(xc[(size_t)m * a.xc_stride + k0 + k], &A, &B);
-        tA[idx] = A;
-        tB[idx] = B;
-    }
-    for (uint32_t m = lane; m < e; m += 64) {
-        const uint32_t j = r0b + XP[m];
-        offr[m] = j * Td;
-        off0[m] = a.rep_uidx[j] * Td;
-    }
-    __syncthreads();
+    const uint32_t mc_max = min(MC, e);
+    uint4* tA = reinterpret_cast<uint4*>(xsh);                  // [m - c0][KC]
+    uint32_t* tB = xsh + (size_t)mc_max * KC * 4;                // [m - c0][KC]
+    uint32_t* offr = tB + (size_t)mc_max * KC;                   // [m - c0], m < c0 + mc + 2
+    uint32_t* off0 = offr + mc_max + 2;
+    const uint8_t* xc = a.xcoef + 64ull * a.xoff[bi];
+    const uint32_t xs = x_stride(e);
     uint32_t col[CPL];
     bool live[CPL];
 #pragma unroll
@@ -436,42 +463,62 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a, uint32_t n_units, uin
         for (int j = 0; j < CPL; ++j) acc[k][j] = 0;
     // syndromes are loaded two m ahead (received row and r0 row, XORed on arrival)
     uint32_t ra[CPL], rb[CPL], na[CPL], nb[CPL];
-#pragma unroll
-    for (int j = 0; j < CPL; ++j) {
-        ra[j] = recv[(size_t)offr[0] + col[j]];
-        rb[j] = r0[(size_t)off0[0] + col[j]];
-        const uint32_t m1 = e > 1 ? 1 : 0;
-        na[j] = recv[(size_t)offr[m1] + col[j]];
-        nb[j] = r0[(size_t)off0[m1] + col[j]];
-    }
-    for (uint32_t m = 0; m < e; ++m) {
-        uint32_t s0[CPL], s1[CPL], s2[CPL];
-#pragma unroll
-        for (int j = 0; j < CPL; ++j) {
-            const uint32_t x = ra[j] ^ rb[j];
-            s0[j] = x & 0x07070707u;
-            s1[j] = (x >> 3) & 0x07070707u;
-            s2[j] = (x >> 6) & 0x03030303u;
-            ra[j] = na[j];
-            rb[j] = nb[j];
+    for (uint32_t c0 = 0; c0 < e; c0 += MC) {
+        const uint32_t mc = min(MC, e - c0);
+        __syncthreads();  // the previous chunk's tables are consumed
+        for (uint32_t idx = lane; idx < mc * KC; idx += 64) {
+            const uint32_t m = idx / KC, k = idx - m * KC;
+            uint4 A = make_uint4(0, 0, 0, 0);
+            uint32_t B = 0;
+            if (k0 + k < e) perm_tables(xc[(size_t)(c0 + m) * xs + k0 + k], &A, &B);
+            tA[idx] = A;
+            tB[idx] = B;
         }
-        if (m + 2 < e) {
+        for (uint32_t m = lane; m < mc + 2 && c0 + m < e; m += 64) {
+            const uint32_t j = r0b + XP[c0 + m];
+            offr[m] = j * Td;
+            off0[m] = a.rep_uidx[j] * Td;
+        }
+        __syncthreads();
+        if (c0 == 0) {
 #pragma unroll
             for (int j = 0; j < CPL; ++j) {
-                na[j] = recv[(size_t)offr[m + 2] + col[j]];
-                nb[j] = r0[(size_t)off0[m + 2] + col[j]];
+                ra[j] = recv[(size_t)offr[0] + col[j]];
+                rb[j] = r0[(size_t)off0[0] + col[j]];
+                const uint32_t m1 = e > 1 ? 1 : 0;
+                na[j] = recv[(size_t)offr[m1] + col[j]];
+                nb[j] = r0[(size_t)off0[m1] + col[j]];
             }
         }
-#pragma unroll
-        for (int k = 0; k < KC; ++k) {
-            const uint4 A = tA[m * KC + k];
-            const uint32_t B = tB[m * KC + k];
+        for (uint32_t m = 0; m < mc; ++m) {
+            uint32_t s0[CPL], s1[CPL], s2[CPL];
 #pragma unroll
             for (int j = 0; j < CPL; ++j) {
-                const uint32_t p0 = __builtin_amdgcn_perm(A.y, A.x, s0[j]);
-                const uint32_t p1 = __builtin_amdgcn_perm(A.w, A.z, s1[j]);
-                const uint32_t p2 = __builtin_amdgcn_perm(B, B, s2[j]);
-                acc[k][j] = xor3(acc[k][j], p0, p1) ^ p2;
+                const uint32_t x = ra[j] ^ rb[j];
+                s0[j] = x & 0x07070707u;
+                s1[j] = (x >> 3) & 0x07070707u;
+                s2[j] = (x >> 6) & 0x03030303u;
+                ra[j] = na[j];
+                rb[j] = nb[j];
+            }
+            if (c0 + m + 2 < e) {
+#pragma unroll
+                for (int j = 0; j < CPL; ++j) {
+                    na[j] = recv[(size_t)offr[m + 2] + col[j]];
+                    nb[j] = r0[(size_t)off0[m + 2] + col[j]];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < KC; ++k) {
+                const uint4 A = tA[m * KC + k];
+                const uint32_t B = tB[m * KC + k];
+#pragma unroll
+                for (int j = 0; j < CPL; ++j) {
+                    const uint32_t p0 = __builtin_amdgcn_perm(A.y, A.x, s0[j]);
+                    const uint32_t p1 = __builtin_amdgcn_perm(A.w, A.z, s1[j]);
+                    const uint32_t p2 = __builtin_amdgcn_perm(B, B, s2[j]);
+                    acc[k][j] = xor3(acc[k][j], p0, p1) ^ p2;
+                }
             }
         }
     }
@@ -489,16 +536,16 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a, uint32_t n_units, uin
 
 template <int CPL>
 static void launch_apply_cpl(const ApplyArgs& a, uint32_t kc, dim3 g, size_t lds, hipStream_t st, uint32_t nu,
-                             uint32_t np) {
+                             uint32_t np, uint32_t mc) {
     switch (kc) {
-        case 4: hipLaunchKernelGGL((k_apply<4, CPL>), g, dim3(64), lds, st, a, nu, np); break;
-        case 8: hipLaunchKernelGGL((k_apply<8, CPL>), g, dim3(64), lds, st, a, nu, np); break;
-        case 12: hipLaunchKernelGGL((k_apply<12, CPL>), g, dim3(64), lds, st, a, nu, np); break;
-        case 16: hipLaunchKernelGGL((k_apply<16, CPL>), g, dim3(64), lds, st, a, nu, np); break;
-        case 20: hipLaunchKernelGGL((k_apply<20, CPL>), g, dim3(64), lds, st, a, nu, np); break;
-        case 24: hipLaunchKernelGGL((k_apply<24, CPL>), g, dim3(64), lds, st, a, nu, np); break;
-        case 28: hipLaunchKernelGGL((k_apply<28, CPL>), g, dim3(64), lds, st, a, nu, np); break;
-        default: hipLaunchKernelGGL((k_apply<32, CPL>), g, dim3(64), lds, st, a, nu, np); break;
+        case 4: hipLaunchKernelGGL((k_apply<4, CPL>), g, dim3(64), lds, st, a, nu, np, mc); break;
+        case 8: hipLaunchKernelGGL((k_apply<8, CPL>), g, dim3(64), lds, st, a, nu, np, mc); break;
+        case 12: hipLaunchKernelGGL((k_apply<12, CPL>), g, dim3(64), lds, st, a, nu, np, mc); break;
+        case 16: hipLaunchKernelGGL((k_apply<16, CPL>), g, dim3(64), lds, st, a, nu, np, mc); break;
+        case 20: hipLaunchKernelGGL((k_apply<20, CPL>), g, dim3(64), lds, st, a, nu, np, mc); break;
+        case 24: hipLaunchKernelGGL((k_apply<24, CPL>), g, dim3(64), lds, st, a, nu, np, mc); break;
+        case 28: hipLaunchKernelGGL((k_apply<28, CPL>), g, dim3(64), lds, st, a, nu, np, mc); break;
+        default: hipLaunchKernelGGL((k_apply<32, CPL>), g, dim3(64), lds, st, a, nu, np, mc); break;
     }
 }
 
@@ -512,13 +559,12 @@ int launch_apply(const ApplyArgs& a, uint32_t /*n_strips*/, uint32_t n_blocks, v
     }
     // balanced slices of KC <= 8 outputs (measured at e ~ 58, K=1024 T=1200: KC 4/8/12/16/20/28 ->
     // 244/210/238/254/282/324 us; small slices keep the accumulators few, so more waves fit per SIMD),
-    // the slice's tables (20 B per coefficient) within ~20 KB of LDS
-    const uint32_t e = std::max<uint32_t>(a.max_e, 1);
-    uint32_t cap = std::max<uint32_t>(4, std::min<uint32_t>(8, (21504 / (20 * e)) & ~3u));
-    static const uint32_t cap_env = std::getenv("RQHIP_APPLY_CAP") ? (uint32_t)std::atoi(std::getenv("RQHIP_APPLY_CAP")) : 0;
-    if (cap_env) cap = std::min<uint32_t>(32, cap_env);
+    // the slice's tables (20 B per coefficient) for MC syndromes within ~20 KB of LDS
+    constexpr uint32_t MC = 256;
+    const uint32_t e = std::max<uint32_t>(a.max_e, 1), ec = std::min(e, MC);
+    const uint32_t cap = std::max<uint32_t>(4, std::min<uint32_t>(8, (21504 / (20 * ec)) & ~3u));
     const uint32_t np = (e + cap - 1) / cap, kc = (((e + np - 1) / np) + 3) & ~3u;
-    const size_t lds = (size_t)e * kc * 20 + (size_t)e * 8;
+    const size_t lds = (size_t)ec * kc * 20 + (size_t)(ec + 2) * 8;
     static bool attr = false;
     if (!attr) {  // slices of large e need more than the default 64 KB
         for (const void* f : {(const void*)k_apply<32, 1>, (const void*)k_apply<32, 2>, (const void*)k_apply<32, 4>,
@@ -529,10 +575,10 @@ int launch_apply(const ApplyArgs& a, uint32_t /*n_strips*/, uint32_t n_blocks, v
     const uint32_t nu = (Td + 64 * cpl - 1) / (64 * cpl) * n_blocks;
     const dim3 g((nu + 7) / 8 * 8 * np);
     switch (cpl) {
-        case 1: launch_apply_cpl<1>(a, kc, g, lds, st, nu, np); break;
-        case 2: launch_apply_cpl<2>(a, kc, g, lds, st, nu, np); break;
-        case 4: launch_apply_cpl<4>(a, kc, g, lds, st, nu, np); break;
-        default: launch_apply_cpl<5>(a, kc, g, lds, st, nu, np); break;
+        case 1: launch_apply_cpl<1>(a, kc, g, lds, st, nu, np, MC); break;
+        case 2: launch_apply_cpl<2>(a, kc, g, lds, st, nu, np, MC); break;
+        case 4: launch_apply_cpl<4>(a, kc, g, lds, st, nu, np, MC); break;
+        default: launch_apply_cpl<5>(a, kc, g, lds, st, nu, np, MC); break;
     }
     return (int)hipGetLastError();
 }

@@ -39,7 +39,7 @@ EXPORTED = (
     "rq_encoder_symbol_size", "rq_encoder_symbol", "rq_encoder_symbols", "rq_encoder_free",
     "rq_decoder_create", "rq_decoder_k", "rq_decoder_add", "rq_decoder_decode", "rq_decoder_free",
     "rq_encode_batch", "rq_decode_batch", "rq_decode_batch_async", "rq_encode_batch_host", "rq_decode_batch_host", "rq_device_count", "rq_set_device",
-    "rq_debug_colprog_eval", "rq_debug_colprog_emulate", "rq_debug_colprog_assemble",
+    "rq_debug_colprog_eval", "rq_debug_colprog_emulate", "rq_debug_colprog_assemble", "rq_debug_decode_margin",
 )
 
 
@@ -117,6 +117,7 @@ def lib():
                                          ctypes.c_int),
             "rq_debug_colprog_assemble": ([ctypes.c_uint32, u32p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_size_t)],
                                           ctypes.c_int),
+            "rq_debug_decode_margin": ([ctypes.c_uint32], ctypes.c_uint32),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)

@@ -170,20 +170,21 @@ def test_batch_decode_round_trip(gpu, rq, oracle, K, T, N, n_blocks, n_erase):
         if st[b] == 1:
             assert torch.equal(data[b], src[b]), b
     assert (st == 1).mean() > 0.5
-    # ok/fail parity with the oracle on one block
-    b = 0
-    src_h = src[b].cpu().numpy().tobytes()
-    ref_enc = oracle.OracleEncoder(src_h, T)
-    rdec = oracle.OracleDecoder(len(src_h), T)
-    for i in range(K):
-        if i not in el[b]:
-            rdec.add_symbol(i, ref_enc.gen_symbol(i).tobytes())
-    for e in rl[b]:
-        rdec.add_symbol(e, ref_enc.gen_symbol(e).tobytes())
-    ok, ref_out = rdec.decode()
-    assert ok == (st[b] == 1)
-    if ok:
-        assert data[b].cpu().numpy().tobytes() == ref_out
+    # ok/fail parity and bytes against the oracle: every block (the first two at K >= 1024, where
+    # the oracle's dense elimination takes seconds per block)
+    for b in range(n_blocks if K < 1024 else min(n_blocks, 2)):
+        src_h = src[b].cpu().numpy().tobytes()
+        ref_enc = oracle.OracleEncoder(src_h, T)
+        rdec = oracle.OracleDecoder(len(src_h), T)
+        for i in range(K):
+            if i not in el[b]:
+                rdec.add_symbol(i, ref_enc.gen_symbol(i).tobytes())
+        for e in rl[b]:
+            rdec.add_symbol(e, ref_enc.gen_symbol(e).tobytes())
+        ok, ref_out = rdec.decode()
+        assert ok == (st[b] == 1), b
+        if ok:
+            assert data[b].cpu().numpy().tobytes() == ref_out, b
 
 
 def test_batch_decode_not_enough_and_fast_path(gpu, rq):
