@@ -112,6 +112,7 @@ int rq_decode_batch_async(const rq_decode_desc* d);
 /* ---------------- batched, host-memory API (fecquic windows) ------------
  * The batch path for callers without device memory (the cgo shim): the same descriptors, with
  * src/out (encode) and data/repair (decode) in HOST memory; `stream` and `c_out` are not used.
+ * Any symbol size T (the device-resident API needs T % 4 == 0; here rows are padded in staging).
  * Blocks are split contiguously over the devices of device_mask (bit d = HIP device d; 0 = the
  * calling thread's device), one host thread per device, no device-to-device traffic.  Each device
  * pipelines H2D, kernels and D2H over two internal streams in chunks of blocks.  Synchronous.
@@ -122,6 +123,27 @@ int rq_decode_batch_async(const rq_decode_desc* d);
  * and the per-block Decode of the receiver workers (go/fecquic/rxbuf.go:336-377). */
 int rq_encode_batch_host(const rq_encode_desc* d, uint32_t device_mask);
 int rq_decode_batch_host(const rq_decode_desc* d, uint32_t device_mask);
+
+/* Host-memory decode of blocks that each live in their own buffers -- a receiver's per-block
+ * staging (go/fecquic/rxbuf.go keeps each block's symbols in its own slabs, :436-468): block b's
+ * K*T data bytes at data (received source rows in place, erased rows overwritten on success) and its
+ * n_repair received repair rows, consecutive, at repair, in repair_esi order.  All blocks of one call
+ * share K and T.  status as in rq_decode_desc.  Synchronous; device_mask as above. */
+typedef struct {
+    uint8_t* data;
+    const uint8_t* repair;
+    uint32_t n_erased;
+    const uint32_t* erased;
+    uint32_t n_repair;
+    const uint32_t* repair_esi;
+    int32_t status;              /* out */
+} rq_block_io;
+int rq_decode_blocks_host(uint32_t K, uint32_t T, rq_block_io* blocks, uint32_t n_blocks, uint32_t device_mask);
+
+/* Pinned (page-locked) host memory for ingest staging, so H2D copies run at full PCIe rate
+ * (hipHostMalloc).  NULL on failure. */
+void* rq_host_alloc(size_t bytes);
+void rq_host_free(void* p);
 
 /* ---------------- device control ---------------- */
 int rq_device_count(void);

@@ -5,7 +5,10 @@
 // There is no CPU fallback: every symbol the engine returns is computed on the GPU, by a
 // generated gfx950 code object (rq_colprog / rq_colasm) or by the kernels in rq_kernels.hip;
 // without a usable gfx950 device the calls fail with RQ_ERR_DEVICE.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -40,6 +43,10 @@ int fail(int code, const std::string& msg) {
     return code;
 }
 
+// Device row pitch for a T-byte symbol staged by the library: a multiple of 4 bytes (one dword per
+// lane) and at least 8 (the column program's block/column split needs T/4 >= 2).
+inline uint32_t pad_row(uint32_t T) { return T <= 8 ? 8u : (T + 3) & ~3u; }
+
 #define HIP_TRY(expr)                                                                        \
     do {                                                                                     \
         hipError_t e_ = (expr);                                                              \
@@ -73,6 +80,7 @@ struct ColKernel {
     uint32_t n_out = 0, n_slots = 0, n_ins = 0;
     uint32_t waves_per_cu = 4;     // residency of the code object (registers, LDS)
     MProg::Stats st{};
+    uint64_t last_use = 0;         // LRU clock of the per-device cache
     DevBuf mrep;                   // decode: outputs on the identity payload
     uint32_t mrep_stride = 0;
     ~ColKernel() { if (mod) (void)hipModuleUnload(mod); }
@@ -92,6 +100,7 @@ struct HostBuf {
         cap = want;
         return RQ_OK;
     }
+    template <class T> T* as() const { return static_cast<T*>(p); }
     ~HostBuf() { if (p) (void)hipHostFree(p); }
 };
 
@@ -122,9 +131,13 @@ struct DevCtx {
     uint32_t n_cu = 256;
     std::mutex mu;
     bool tables = false;
-    std::map<std::string, std::unique_ptr<ColKernel>> colk;  // keyed by (K', K, outputs)
+    std::map<std::string, std::unique_ptr<ColKernel>> colk;  // keyed by (K', K, outputs); LRU-bounded
+    uint64_t tick = 0;
     std::map<void*, std::unique_ptr<Workspace>> ws;
     Stage stage[2];
+    hipStream_t obj_stream = nullptr;  // per-object API: its own stream, pinned staging, device buffer
+    HostBuf obj_h;
+    DevBuf obj_d;
     Workspace* wsp(void* stream) {
         auto& w = ws[stream];
         if (!w) w.reset(new Workspace());
@@ -210,49 +223,155 @@ const AllocOpts& alloc_options() {
     return o;
 }
 
+// ---------------- on-disk cache of compiled column programs ----------------
+// A column program is a pure function of (this library build, K', K, outputs, allocation options), so
+// its code object and launch metadata are cached across processes under $RQHIP_CACHE_DIR (default
+// $XDG_CACHE_HOME/rqhip or ~/.cache/rqhip; "0" disables).  The key hashes the library's own file
+// bytes, so any rebuild starts a fresh cache.  Failures to read or write the cache only cost time.
+uint64_t fnv1a(const void* p, size_t n, uint64_t h = 1469598103934665603ull) {
+    const uint8_t* b = static_cast<const uint8_t*>(p);
+    for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 1099511628211ull;
+    return h;
+}
+
+const std::string& cache_dir() {
+    static const std::string d = [] {
+        std::string r;
+        if (const char* e = std::getenv("RQHIP_CACHE_DIR")) r = e;
+        else if (const char* x = std::getenv("XDG_CACHE_HOME")) r = std::string(x) + "/rqhip";
+        else if (const char* h = std::getenv("HOME")) r = std::string(h) + "/.cache/rqhip";
+        if (r == "0") r.clear();
+        return r;
+    }();
+    return d;
+}
+
+uint64_t library_hash() {
+    static const uint64_t h = [] {
+        Dl_info di;
+        uint64_t x = 0;
+        if (dladdr((const void*)&library_hash, &di) && di.dli_fname) {
+            if (FILE* f = std::fopen(di.dli_fname, "rb")) {
+                std::vector<char> buf(1 << 16);
+                size_t n;
+                x = 1469598103934665603ull;
+                while ((n = std::fread(buf.data(), 1, buf.size(), f)) > 0) x = fnv1a(buf.data(), n, x);
+                std::fclose(f);
+            }
+        }
+        return x;
+    }();
+    return h;
+}
+
+struct CacheHdr {
+    char magic[8];
+    uint32_t n_out, n_slots, n_ins, waves_per_cu, name_len, pad;
+    uint64_t co_len;
+    MProg::Stats st;
+};
+
+bool cache_load(const std::string& path, CacheHdr* h, std::string* name, std::vector<char>* co) {
+    FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f) return false;
+    bool ok = std::fread(h, sizeof *h, 1, f) == 1 && std::memcmp(h->magic, "RQCO0001", 8) == 0 && h->name_len < 256 &&
+              h->co_len < (1ull << 30);
+    if (ok) {
+        name->resize(h->name_len);
+        co->resize(h->co_len);
+        ok = std::fread(&(*name)[0], 1, h->name_len, f) == h->name_len &&
+             std::fread(co->data(), 1, h->co_len, f) == h->co_len;
+    }
+    std::fclose(f);
+    return ok;
+}
+
+void cache_store(const std::string& path, const CacheHdr& h, const std::string& name, const std::vector<char>& co) {
+    ::mkdir(cache_dir().c_str(), 0755);
+    const std::string tmp = path + ".tmp" + std::to_string(::getpid());
+    FILE* f = std::fopen(tmp.c_str(), "wb");
+    if (!f) return;
+    const bool ok = std::fwrite(&h, sizeof h, 1, f) == 1 && std::fwrite(name.data(), 1, name.size(), f) == name.size() &&
+                    std::fwrite(co.data(), 1, co.size(), f) == co.size();
+    std::fclose(f);
+    if (ok) std::rename(tmp.c_str(), path.c_str());
+    else std::remove(tmp.c_str());
+}
+
 // ---------------- column programs (the encode hot path) ----------------
 // Compile (once per device and (K', K, outputs)) the straight-line gfx950 program for the given
 // outputs: IR (rq_colprog.cpp) -> registers/scratch (rq_colasm.cpp) -> assembly -> code object
-// (amd_comgr, in process) -> hipModuleLoadData.  Caller holds ctx->mu.
+// (amd_comgr, in process) -> hipModuleLoadData, or take the code object from the disk cache.
+// Caller holds ctx->mu.
 int get_col_kernel(DevCtx* ctx, const Params& p, const uint32_t* esi, uint32_t n_esi, bool all_C, ColKernel** out) {
     std::string key = std::to_string(p.Kp) + ":" + std::to_string(p.K) + (all_C ? ":C" : ":E");
     if (!all_C) {
         key.reserve(key.size() + n_esi * 6);
         for (uint32_t i = 0; i < n_esi; ++i) key += "," + std::to_string(esi[i]);
     }
+    constexpr size_t MAX_PROGRAMS = 48;  // loaded column programs per device (sparse decode unions)
+    if (!ctx->colk.count(key) && ctx->colk.size() >= MAX_PROGRAMS) {
+        auto victim = ctx->colk.begin();
+        for (auto it = ctx->colk.begin(); it != ctx->colk.end(); ++it)
+            if (it->second->last_use < victim->second->last_use) victim = it;
+        (void)hipDeviceSynchronize();  // its kernels may still run on some stream: unload when idle
+        ctx->colk.erase(victim);
+    }
     auto& slot = ctx->colk[key];
     if (!slot) {
         std::unique_ptr<ColKernel> k(new ColKernel());
         k->p = p;
         if (!all_C) k->esi.assign(esi, esi + n_esi);
-        ColIR ir;
-        std::string err;
-        const bool ok = all_C ? build_colprog_C(p, &ir, &err) : build_colprog(p, esi, n_esi, &ir, &err);
-        if (!ok) { ctx->colk.erase(key); return fail(RQ_ERR_PLAN, err); }
-        MProg mp;
-        if (!allocate_colprog(ir, alloc_options(), &mp, &err)) { ctx->colk.erase(key); return fail(RQ_ERR_PLAN, err); }
-        // distinct symbol per program so kernel traces separate encode, decode and C programs
-        const std::string kname = "rq_colprog_K" + std::to_string(p.K) + (all_C ? "_C" : "_n" + std::to_string(n_esi));
-        const std::string src = emit_colprog_asm(mp, kname);
+        const AllocOpts& ao = alloc_options();
+        std::string path;
+        if (!cache_dir().empty() && library_hash()) {
+            uint64_t h = fnv1a(key.data(), key.size(), library_hash());
+            h = fnv1a(&ao, sizeof ao, h);
+            char hex[17];
+            std::snprintf(hex, sizeof hex, "%016llx", (unsigned long long)h);
+            path = cache_dir() + "/" + hex + ".co";
+        }
+        CacheHdr ch;
+        std::string kname;
         std::vector<char> co;
-        if (!comgr_assemble(src, &co, &err)) { ctx->colk.erase(key); return fail(RQ_ERR_PLAN, err); }
+        if (path.empty() || !cache_load(path, &ch, &kname, &co)) {
+            ColIR ir;
+            std::string err;
+            const bool ok = all_C ? build_colprog_C(p, &ir, &err) : build_colprog(p, esi, n_esi, &ir, &err);
+            if (!ok) { ctx->colk.erase(key); return fail(RQ_ERR_PLAN, err); }
+            MProg mp;
+            if (!allocate_colprog(ir, ao, &mp, &err)) { ctx->colk.erase(key); return fail(RQ_ERR_PLAN, err); }
+            // distinct symbol per program so kernel traces separate encode, decode and C programs
+            kname = "rq_colprog_K" + std::to_string(p.K) + (all_C ? "_C" : "_n" + std::to_string(n_esi));
+            co.clear();
+            if (!comgr_assemble(emit_colprog_asm(mp, kname), &co, &err)) { ctx->colk.erase(key); return fail(RQ_ERR_PLAN, err); }
+            std::memset(&ch, 0, sizeof ch);
+            std::memcpy(ch.magic, "RQCO0001", 8);
+            ch.n_out = ir.n_out;
+            ch.n_slots = mp.n_slots;
+            ch.n_ins = (uint32_t)mp.ins.size();
+            const uint32_t regs = colprog_regs(mp), lds = mp.n_lds_slots * 256u;
+            uint32_t w = 4 * std::max<uint32_t>(1, 512 / regs);
+            if (lds) w = std::min<uint32_t>(w, 163840u / lds);
+            ch.waves_per_cu = std::max<uint32_t>(1, std::min<uint32_t>(w, 32));
+            ch.name_len = (uint32_t)kname.size();
+            ch.co_len = co.size();
+            ch.st = mp.st;
+            if (!path.empty()) cache_store(path, ch, kname, co);
+        }
         if (hipModuleLoadData(&k->mod, co.data()) != hipSuccess ||
             hipModuleGetFunction(&k->fn, k->mod, kname.c_str()) != hipSuccess) {
             ctx->colk.erase(key);
             return fail(RQ_ERR_DEVICE, "hipModuleLoadData/GetFunction failed for the column program");
         }
-        k->n_out = ir.n_out;
-        k->n_slots = mp.n_slots;
-        {
-            const uint32_t regs = colprog_regs(mp), lds = mp.n_lds_slots * 256u;
-            uint32_t w = 4 * std::max<uint32_t>(1, 512 / regs);
-            if (lds) w = std::min<uint32_t>(w, 163840u / lds);
-            k->waves_per_cu = std::max<uint32_t>(1, std::min<uint32_t>(w, 32));
-        }
-        k->st = mp.st;
-        k->n_ins = (uint32_t)mp.ins.size();
+        k->n_out = ch.n_out;
+        k->n_slots = ch.n_slots;
+        k->waves_per_cu = ch.waves_per_cu;
+        k->st = ch.st;
+        k->n_ins = ch.n_ins;
         slot = std::move(k);
     }
+    slot->last_use = ++ctx->tick;
     *out = slot.get();
     return RQ_OK;
 }
@@ -269,7 +388,7 @@ bool xcd_order() {
 // Run a column program over n_blocks device-resident blocks.  Caller holds ctx->mu.
 int launch_col(DevCtx* ctx, ColKernel* k, uint32_t T, uint32_t n_blocks, const void* src, uint64_t src_stride,
                void* out, uint64_t out_stride, void* stream) {
-    if (T == 0 || T % 4) return fail(RQ_ERR_BAD_ARG, "T must be a positive multiple of 4");
+    if (T < 8 || T % 4) return fail(RQ_ERR_BAD_ARG, "device-resident symbols: T must be a multiple of 4, at least 8");
     if (n_blocks == 0) return RQ_OK;
     const uint32_t Td = T / 4;
     // every buffer offset is 32-bit: split so that each launch spans < 4 GiB per buffer
@@ -354,7 +473,7 @@ std::vector<uint32_t> decode_union(uint32_t K, const std::vector<uint32_t>& rep)
 // Coefficients of every output over the source rows: the program on the identity payload.
 int ensure_mrep(DevCtx* ctx, ColKernel* k, void* stream) {
     if (k->mrep_stride) return RQ_OK;
-    const uint32_t K = k->p.K, Tid = (K + 3) & ~3u;
+    const uint32_t K = k->p.K, Tid = pad_row(K);
     std::vector<uint8_t> id((size_t)K * Tid, 0);
     for (uint32_t i = 0; i < K; ++i) id[(size_t)i * Tid + i] = 1;
     DevBuf src;
@@ -631,6 +750,16 @@ int copy_rows(void* dst, uint64_t dpitch, const void* src, uint64_t spitch, uint
     return RQ_OK;
 }
 
+// Rows of `width` bytes between pitched layouts (the host's T-byte rows and the device staging's
+// 4-byte-padded rows when T % 4 != 0): one 2D copy.
+int copy_2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t rows, hipMemcpyKind kind,
+            hipStream_t s) {
+    if (!rows || !width) return RQ_OK;
+    if (dpitch == width && spitch == width) HIP_TRY(hipMemcpyAsync(dst, src, width * rows, kind, s));
+    else HIP_TRY(hipMemcpy2DAsync(dst, dpitch, src, spitch, width, rows, kind, s));
+    return RQ_OK;
+}
+
 // One device's shard [b0, b1) of a host-memory encode: chunk c runs on stage c&1 (H2D source,
 // column program, D2H repairs); calls on one stream are ordered, so a stage's buffers are reused
 // only after its previous chunk finished.
@@ -641,28 +770,74 @@ int encode_host_shard(int dev, const rq_encode_desc& d, const Params& p, uint32_
     if (rc) return rc;
     std::lock_guard<std::mutex> lk(ctx->mu);
     if ((rc = ensure_stages(ctx))) return rc;
-    const uint64_t in_b = (uint64_t)d.K * d.T, out_b = (uint64_t)d.n_esi * d.T;
-    const uint32_t cb = chunk_blocks(ctx, d.T, b1 - b0);
+    // device rows are padded to Tp = T rounded up to 4 bytes (GF(256) work is bytewise: the pad bytes
+    // only ever reach pad bytes)
+    const uint32_t T = d.T, Tp = pad_row(T);
+    const uint64_t in_b = (uint64_t)d.K * Tp, out_b = (uint64_t)d.n_esi * Tp;
+    const uint32_t cb = chunk_blocks(ctx, Tp, b1 - b0);
     for (uint32_t c = 0, b = b0; b < b1; ++c, b += cb) {
         Stage& st = ctx->stage[c & 1];
         const uint32_t nb = std::min(cb, b1 - b);
         if ((rc = st.in.ensure(cb * in_b)) || (rc = st.out.ensure(cb * out_b))) return rc;
         const uint8_t* src = static_cast<const uint8_t*>(d.src) + b * d.src_stride;
         uint8_t* out = static_cast<uint8_t*>(d.out) + b * d.out_stride;
-        if ((rc = copy_rows(st.in.p, in_b, src, d.src_stride, in_b, nb, hipMemcpyHostToDevice, st.s)) ||
-            (rc = encode_locked(ctx, p, d.T, nb, st.in.p, in_b, d.esi, d.n_esi, st.out.p, out_b, st.s)) ||
-            (rc = copy_rows(out, d.out_stride, st.out.p, out_b, out_b, nb, hipMemcpyDeviceToHost, st.s)))
+        if (Tp == T) {
+            rc = copy_rows(st.in.p, in_b, src, d.src_stride, in_b, nb, hipMemcpyHostToDevice, st.s);
+        } else if (d.src_stride == (uint64_t)d.K * T) {
+            rc = copy_2d(st.in.p, Tp, src, T, T, (size_t)nb * d.K, hipMemcpyHostToDevice, st.s);
+        } else {
+            for (uint32_t i = 0; i < nb && !rc; ++i)
+                rc = copy_2d(st.in.as<uint8_t>() + i * in_b, Tp, src + i * d.src_stride, T, T, d.K,
+                             hipMemcpyHostToDevice, st.s);
+        }
+        if (rc || (rc = encode_locked(ctx, p, Tp, nb, st.in.p, in_b, d.esi, d.n_esi, st.out.p, out_b, st.s)))
             return rc;
+        if (Tp == T) {
+            rc = copy_rows(out, d.out_stride, st.out.p, out_b, out_b, nb, hipMemcpyDeviceToHost, st.s);
+        } else if (d.out_stride == (uint64_t)d.n_esi * T) {
+            rc = copy_2d(out, T, st.out.p, Tp, T, (size_t)nb * d.n_esi, hipMemcpyDeviceToHost, st.s);
+        } else {
+            for (uint32_t i = 0; i < nb && !rc; ++i)
+                rc = copy_2d(out + i * d.out_stride, T, st.out.as<uint8_t>() + i * out_b, Tp, T, d.n_esi,
+                             hipMemcpyDeviceToHost, st.s);
+        }
+        if (rc) return rc;
     }
     for (Stage& st : ctx->stage) HIP_TRY(hipStreamSynchronize(st.s));
+    return RQ_OK;
+}
+
+// Host-memory decode input: block b's K*T data bytes at data[b] (recovered rows written back there)
+// and its n_repair[b] received repair rows, consecutive, at rep[b].  Index arrays as in rq_decode_desc.
+struct HostDecode {
+    uint32_t T = 0, K = 0;
+    std::vector<uint8_t*> data;
+    std::vector<const uint8_t*> rep;
+    const uint32_t *n_erased = nullptr, *erased = nullptr, *n_repair = nullptr, *repair_esi = nullptr;
+    int32_t* status = nullptr;
+};
+
+// H2D of `n` blocks' regions of `bytes[i]` bytes from host pointers src[i] to consecutive device
+// memory: one copy per run of host-contiguous blocks.
+template <class P>
+int upload_runs(uint8_t* dst, const P* src, const uint64_t* bytes, uint32_t n, hipStream_t s) {
+    uint32_t i = 0;
+    while (i < n) {
+        uint64_t run = bytes[i];
+        uint32_t j = i + 1;
+        while (j < n && (const uint8_t*)src[j] == (const uint8_t*)src[i] + run) run += bytes[j++];
+        if (run) HIP_TRY(hipMemcpyAsync(dst, src[i], run, hipMemcpyHostToDevice, s));
+        dst += run;
+        i = j;
+    }
     return RQ_OK;
 }
 
 // One device's shard of a host-memory decode.  Per chunk: upload the data blocks and their received
 // repair rows (the next chunk's upload is queued on the other stage before this chunk's decode, so
 // it overlaps the kernels), decode, download only the recovered rows and scatter them into the
-// caller's buffer for the blocks that decoded.
-int decode_host_shard(int dev, const rq_decode_desc& d, const Params& p, uint32_t b0, uint32_t b1,
+// caller's buffers for the blocks that decoded.
+int decode_host_shard(int dev, const HostDecode& d, const Params& p, uint32_t b0, uint32_t b1,
                       const std::vector<uint64_t>& eoff, const std::vector<uint64_t>& roff) {
     g_device = dev;
     DevCtx* ctx;
@@ -670,8 +845,9 @@ int decode_host_shard(int dev, const rq_decode_desc& d, const Params& p, uint32_
     if (rc) return rc;
     std::lock_guard<std::mutex> lk(ctx->mu);
     if ((rc = ensure_stages(ctx))) return rc;
-    const uint64_t blk_b = (uint64_t)d.K * d.T;
-    const uint32_t cb = chunk_blocks(ctx, d.T, b1 - b0);
+    const uint32_t T = d.T, Tp = pad_row(T);  // device rows padded (see encode_host_shard)
+    const uint64_t blk_b = (uint64_t)d.K * Tp;
+    const uint32_t cb = chunk_blocks(ctx, Tp, b1 - b0);
     uint32_t max_rep = 0;
     for (uint32_t b = b0; b < b1; b += cb)
         max_rep = std::max<uint32_t>(max_rep, (uint32_t)(roff[std::min(b1, b + cb)] - roff[b]));
@@ -679,13 +855,23 @@ int decode_host_shard(int dev, const rq_decode_desc& d, const Params& p, uint32_
         Stage& st = ctx->stage[c & 1];
         const uint32_t b = b0 + c * cb, nb = std::min(cb, b1 - b);
         int r;
-        if ((r = st.in.ensure(cb * blk_b)) || (r = st.out.ensure((size_t)max_rep * d.T))) return r;
-        if ((r = copy_rows(st.in.p, blk_b, static_cast<const uint8_t*>(d.data) + b * d.data_stride, d.data_stride,
-                           blk_b, nb, hipMemcpyHostToDevice, st.s)))
-            return r;
-        const uint64_t nr = roff[b + nb] - roff[b];
-        if (nr) HIP_TRY(hipMemcpyAsync(st.out.p, static_cast<const uint8_t*>(d.repair) + roff[b] * d.T, nr * d.T,
-                                       hipMemcpyHostToDevice, st.s));
+        if ((r = st.in.ensure(cb * blk_b)) || (r = st.out.ensure(std::max<size_t>((size_t)max_rep * Tp, 4)))) return r;
+        if (Tp == T) {
+            std::vector<uint64_t> db(nb, blk_b), rb(nb);
+            for (uint32_t i = 0; i < nb; ++i) rb[i] = (uint64_t)d.n_repair[b + i] * T;
+            if ((r = upload_runs(st.in.as<uint8_t>(), d.data.data() + b, db.data(), nb, st.s)) ||
+                (r = upload_runs(st.out.as<uint8_t>(), d.rep.data() + b, rb.data(), nb, st.s)))
+                return r;
+            return RQ_OK;
+        }
+        uint8_t* rd = st.out.as<uint8_t>();
+        for (uint32_t i = 0; i < nb; ++i) {
+            if ((r = copy_2d(st.in.as<uint8_t>() + i * blk_b, Tp, d.data[b + i], T, T, d.K, hipMemcpyHostToDevice,
+                             st.s)) ||
+                (r = copy_2d(rd, Tp, d.rep[b + i], T, T, d.n_repair[b + i], hipMemcpyHostToDevice, st.s)))
+                return r;
+            rd += (size_t)d.n_repair[b + i] * Tp;
+        }
         return RQ_OK;
     };
     const uint32_t n_chunks = (b1 - b0 + cb - 1) / cb;
@@ -695,15 +881,14 @@ int decode_host_shard(int dev, const rq_decode_desc& d, const Params& p, uint32_
         Stage& st = ctx->stage[c & 1];
         const uint32_t b = b0 + c * cb, nb = std::min(cb, b1 - b);
         PackOut po;
-        if ((rc = decode_locked(ctx, p, d.T, nb, st.in.p, blk_b, d.n_erased + b, d.erased + eoff[b], d.n_repair + b,
+        if ((rc = decode_locked(ctx, p, Tp, nb, st.in.p, blk_b, d.n_erased + b, d.erased + eoff[b], d.n_repair + b,
                                 d.repair_esi + roff[b], st.out.p, d.status + b, st.s, &po)))
             return rc;
-        size_t r = 0;  // po holds the recovered rows of the blocks that decoded
+        size_t r = 0;  // po holds the recovered rows (Tp apart) of the blocks that decoded
         for (uint32_t lb : po.blocks) {
             const uint32_t gb = b + lb;
-            uint8_t* dst = static_cast<uint8_t*>(d.data) + gb * d.data_stride;
             for (uint64_t i = eoff[gb]; i < eoff[gb + 1]; ++i, ++r)
-                std::memcpy(dst + (uint64_t)d.erased[i] * d.T, po.rows.data() + r * d.T, d.T);
+                std::memcpy(d.data[gb] + (uint64_t)d.erased[i] * T, po.rows.data() + r * Tp, T);
         }
     }
     return RQ_OK;
@@ -756,6 +941,8 @@ struct rq_enc {
     Params p{};
     uint32_t T = 0, Tp = 0;
     std::vector<uint8_t> src;  // K x Tp, zero padded (GenSymbol for esi < K)
+    std::vector<uint8_t> rep;  // repairs K .. K + n_rep - 1, Tp apart (GenSymbol served from host)
+    uint32_t n_rep = 0;
     DevBuf d_src, d_C, d_esi, d_out;
 };
 
@@ -942,7 +1129,7 @@ int rq_decode_batch_async(const rq_decode_desc* d) {
 
 int rq_encode_batch_host(const rq_encode_desc* d, uint32_t device_mask) {
     if (!d || d->T == 0) return fail(RQ_ERR_SYMBOL_SIZE_ZERO, "symbol size cannot be zero");
-    if (d->T % 4 || d->K == 0 || (!d->src && d->n_blocks)) return fail(RQ_ERR_BAD_ARG, "bad encode descriptor (T % 4, K, src)");
+    if (d->K == 0 || (!d->src && d->n_blocks)) return fail(RQ_ERR_BAD_ARG, "bad encode descriptor (K, src)");
     if (d->n_blocks == 0 || d->n_esi == 0) return RQ_OK;
     if (!d->esi || !d->out) return fail(RQ_ERR_BAD_ARG, "n_esi without esi/out");
     if (d->src_stride < (uint64_t)d->K * d->T || d->out_stride < (uint64_t)d->n_esi * d->T)
@@ -957,7 +1144,7 @@ int rq_encode_batch_host(const rq_encode_desc* d, uint32_t device_mask) {
 
 int rq_decode_batch_host(const rq_decode_desc* d, uint32_t device_mask) {
     if (!d || d->T == 0) return fail(RQ_ERR_SYMBOL_SIZE_ZERO, "symbol size cannot be zero");
-    if (d->T % 4 || d->K == 0) return fail(RQ_ERR_BAD_ARG, "bad decode descriptor (T % 4, K)");
+    if (d->K == 0) return fail(RQ_ERR_BAD_ARG, "bad decode descriptor (K)");
     if (d->n_blocks == 0) return RQ_OK;
     if (!d->data || !d->n_erased || !d->n_repair || !d->status) return fail(RQ_ERR_BAD_ARG, "null decode array");
     if (d->data_stride < (uint64_t)d->K * d->T) return fail(RQ_ERR_BAD_ARG, "stride smaller than a block");
@@ -969,14 +1156,83 @@ int rq_decode_batch_host(const rq_decode_desc* d, uint32_t device_mask) {
         eoff[b + 1] = eoff[b] + d->n_erased[b];
         roff[b + 1] = roff[b] + d->n_repair[b];
     }
+    HostDecode h;
+    h.T = d->T; h.K = d->K;
+    h.n_erased = d->n_erased; h.erased = d->erased; h.n_repair = d->n_repair; h.repair_esi = d->repair_esi;
+    h.status = d->status;
+    for (uint32_t b = 0; b < d->n_blocks; ++b) {
+        h.data.push_back(static_cast<uint8_t*>(d->data) + b * d->data_stride);
+        h.rep.push_back(static_cast<const uint8_t*>(d->repair) + roff[b] * d->T);
+    }
     return run_sharded(device_mask, d->n_blocks, [&](int dev, uint32_t b0, uint32_t b1) {
-        return decode_host_shard(dev, *d, p, b0, b1, eoff, roff);
+        return decode_host_shard(dev, h, p, b0, b1, eoff, roff);
     });
+}
+
+int rq_decode_blocks_host(uint32_t K, uint32_t T, rq_block_io* blocks, uint32_t n_blocks, uint32_t device_mask) {
+    if (T == 0) return fail(RQ_ERR_SYMBOL_SIZE_ZERO, "symbol size cannot be zero");
+    if (K == 0) return fail(RQ_ERR_BAD_ARG, "bad decode arguments (K)");
+    if (n_blocks == 0) return RQ_OK;
+    if (!blocks) return fail(RQ_ERR_BAD_ARG, "null blocks");
+    Params p;
+    int rc = params_for_K(K, &p);
+    if (rc) return fail(rc, "k is too big");
+    HostDecode h;
+    h.T = T; h.K = K;
+    std::vector<uint32_t> ne(n_blocks), nr(n_blocks), er, re;
+    std::vector<int32_t> st(n_blocks, 0);
+    std::vector<uint64_t> eoff(n_blocks + 1, 0), roff(n_blocks + 1, 0);
+    for (uint32_t b = 0; b < n_blocks; ++b) {
+        const rq_block_io& x = blocks[b];
+        if (!x.data || (x.n_erased && !x.erased) || (x.n_repair && (!x.repair || !x.repair_esi)))
+            return fail(RQ_ERR_BAD_ARG, "null block buffer");
+        ne[b] = x.n_erased;
+        nr[b] = x.n_repair;
+        er.insert(er.end(), x.erased, x.erased + x.n_erased);
+        re.insert(re.end(), x.repair_esi, x.repair_esi + x.n_repair);
+        eoff[b + 1] = eoff[b] + ne[b];
+        roff[b + 1] = roff[b] + nr[b];
+        h.data.push_back(x.data);
+        h.rep.push_back(x.repair);
+    }
+    er.push_back(0);
+    re.push_back(0);
+    h.n_erased = ne.data(); h.erased = er.data(); h.n_repair = nr.data(); h.repair_esi = re.data();
+    h.status = st.data();
+    rc = run_sharded(device_mask, n_blocks, [&](int dev, uint32_t b0, uint32_t b1) {
+        return decode_host_shard(dev, h, p, b0, b1, eoff, roff);
+    });
+    for (uint32_t b = 0; b < n_blocks; ++b) blocks[b].status = st[b];
+    return rc;
+}
+
+void* rq_host_alloc(size_t bytes) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, std::max<size_t>(bytes, 1), hipHostMallocDefault) != hipSuccess) {
+        fail(RQ_ERR_DEVICE, "hipHostMalloc failed");
+        return nullptr;
+    }
+    return p;
+}
+
+void rq_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
 }
 
 // ---------------- per-object encoder (CreateEncoder / GenSymbol) ----------------
 // CreateEncoder computes the intermediate symbols C on the GPU (the column program with all L
-// outputs); GenSymbol gathers LT rows of C on the GPU (k_gather).
+// outputs, one program per K', cached on disk) and gathers the first repair symbols K..K+R_hw-1 in
+// the same stream (k_gather), so the GenSymbol calls a sender makes (0..N-1, transfer.go:180,
+// raptorq_eval main.go:216) are served from host memory without touching the GPU.  Other ESIs are
+// gathered from the device-resident C on demand.
+constexpr uint32_t high_water(uint32_t K) { return K / 4 > 32 ? K / 4 : 32; }
+
+int obj_stream(DevCtx* ctx, hipStream_t* s) {  // per-device stream of the per-object API (ctx->mu held)
+    if (!ctx->obj_stream) HIP_TRY(hipStreamCreateWithFlags(&ctx->obj_stream, hipStreamNonBlocking));
+    *s = ctx->obj_stream;
+    return RQ_OK;
+}
+
 rq_enc* rq_encoder_create(const uint8_t* data, size_t len, uint32_t T, int* err) {
     int dummy;
     if (!err) err = &dummy;
@@ -987,7 +1243,7 @@ rq_enc* rq_encoder_create(const uint8_t* data, size_t len, uint32_t T, int* err)
     std::unique_ptr<rq_enc> e(new rq_enc());
     e->p = p;
     e->T = T;
-    e->Tp = (T + 3) & ~3u;
+    e->Tp = pad_row(T);
     e->src.assign((size_t)p.K * e->Tp, 0);
     for (uint32_t i = 0; i < p.K; ++i) {
         const size_t off = (size_t)i * T;
@@ -997,19 +1253,39 @@ rq_enc* rq_encoder_create(const uint8_t* data, size_t len, uint32_t T, int* err)
     DevCtx* ctx;
     if ((rc = get_ctx(&ctx))) { *err = rc; return nullptr; }
     std::lock_guard<std::mutex> lk(ctx->mu);
-    if ((rc = ensure_tables(ctx))) { *err = rc; return nullptr; }
-    if ((rc = e->d_src.ensure(e->src.size())) || (rc = e->d_C.ensure((size_t)p.L * e->Tp))) { *err = rc; return nullptr; }
-    if (hipMemcpy(e->d_src.p, e->src.data(), e->src.size(), hipMemcpyHostToDevice) != hipSuccess) {
-        *err = fail(RQ_ERR_DEVICE, "hipMemcpy H2D failed");
+    hipStream_t st;
+    if ((rc = ensure_tables(ctx)) || (rc = obj_stream(ctx, &st))) { *err = rc; return nullptr; }
+    const uint32_t R = high_water(p.K);
+    if ((rc = e->d_src.ensure(e->src.size())) || (rc = e->d_C.ensure((size_t)p.L * e->Tp)) ||
+        (rc = e->d_esi.ensure(R * 4)) || (rc = e->d_out.ensure((size_t)R * e->Tp)) ||
+        (rc = ctx->obj_h.ensure(std::max<size_t>(e->src.size(), (size_t)R * e->Tp)))) { *err = rc; return nullptr; }
+    // source and the high-water ESI list travel in one pinned upload
+    uint8_t* h = ctx->obj_h.as<uint8_t>();
+    std::memcpy(h, e->src.data(), e->src.size());
+    std::vector<uint32_t> esi(R);
+    for (uint32_t i = 0; i < R; ++i) esi[i] = p.K + i;
+    if (hipMemcpyAsync(e->d_src.p, h, e->src.size(), hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(e->d_esi.p, esi.data(), R * 4, hipMemcpyHostToDevice, st) != hipSuccess) {
+        *err = fail(RQ_ERR_DEVICE, "hipMemcpyAsync H2D failed");
         return nullptr;
     }
     ColKernel* k;
     if ((rc = get_col_kernel(ctx, p, nullptr, 0, true, &k)) ||
-        (rc = launch_col(ctx, k, e->Tp, 1, e->d_src.p, e->src.size(), e->d_C.p, (uint64_t)p.L * e->Tp, nullptr))) {
+        (rc = launch_col(ctx, k, e->Tp, 1, e->d_src.p, e->src.size(), e->d_C.p, (uint64_t)p.L * e->Tp, st))) {
         *err = rc;
         return nullptr;
     }
-    if (hipDeviceSynchronize() != hipSuccess) { *err = fail(RQ_ERR_DEVICE, "encode failed"); return nullptr; }
+    if (launch_gather(dev_params(p), e->d_C.as<uint8_t>(), e->Tp, e->d_esi.as<uint32_t>(), R, e->d_out.as<uint8_t>(), st)) {
+        *err = fail(RQ_ERR_DEVICE, "k_gather launch failed");
+        return nullptr;
+    }
+    if (hipMemcpyAsync(h, e->d_out.p, (size_t)R * e->Tp, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess) {
+        *err = fail(RQ_ERR_DEVICE, "encode failed");
+        return nullptr;
+    }
+    e->rep.assign(h, h + (size_t)R * e->Tp);
+    e->n_rep = R;
     *err = RQ_OK;
     return e.release();
 }
@@ -1024,6 +1300,7 @@ int rq_encoder_symbols(rq_enc* e, uint32_t first, uint32_t count, uint8_t* out) 
     for (uint32_t i = 0; i < count; ++i) {
         const uint64_t esi = (uint64_t)first + i;
         if (esi < K) std::memcpy(out + (size_t)i * T, &e->src[(size_t)esi * e->Tp], T);
+        else if (esi - K < e->n_rep) std::memcpy(out + (size_t)i * T, &e->rep[(size_t)(esi - K) * e->Tp], T);
         else rep.push_back((uint32_t)esi);
     }
     if (rep.empty()) return RQ_OK;
@@ -1031,17 +1308,21 @@ int rq_encoder_symbols(rq_enc* e, uint32_t first, uint32_t count, uint8_t* out) 
     int rc = get_ctx(&ctx);
     if (rc) return rc;
     std::lock_guard<std::mutex> lk(ctx->mu);
-    if ((rc = e->d_esi.ensure(rep.size() * 4)) || (rc = e->d_out.ensure(rep.size() * e->Tp))) return rc;
-    HIP_TRY(hipMemcpy(e->d_esi.p, rep.data(), rep.size() * 4, hipMemcpyHostToDevice));
+    hipStream_t st;
+    if ((rc = obj_stream(ctx, &st)) || (rc = e->d_esi.ensure(rep.size() * 4)) ||
+        (rc = e->d_out.ensure(rep.size() * e->Tp)) || (rc = ctx->obj_h.ensure(rep.size() * e->Tp)))
+        return rc;
+    HIP_TRY(hipMemcpyAsync(e->d_esi.p, rep.data(), rep.size() * 4, hipMemcpyHostToDevice, st));
     const int le = launch_gather(dev_params(e->p), e->d_C.as<uint8_t>(), e->Tp, e->d_esi.as<uint32_t>(),
-                                 (uint32_t)rep.size(), e->d_out.as<uint8_t>(), nullptr);
+                                 (uint32_t)rep.size(), e->d_out.as<uint8_t>(), st);
     if (le) return fail(RQ_ERR_DEVICE, "k_gather launch failed");
-    std::vector<uint8_t> buf(rep.size() * e->Tp);
-    HIP_TRY(hipMemcpy(buf.data(), e->d_out.p, buf.size(), hipMemcpyDeviceToHost));
+    const uint8_t* buf = ctx->obj_h.as<uint8_t>();
+    HIP_TRY(hipMemcpyAsync(ctx->obj_h.p, e->d_out.p, rep.size() * e->Tp, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
     size_t r = 0;
     for (uint32_t i = 0; i < count; ++i) {
         const uint64_t esi = (uint64_t)first + i;
-        if (esi >= K) std::memcpy(out + (size_t)i * T, &buf[(r++) * e->Tp], T);
+        if (esi >= K && esi - K >= e->n_rep) std::memcpy(out + (size_t)i * T, &buf[(r++) * e->Tp], T);
     }
     return RQ_OK;
 }
@@ -1090,39 +1371,51 @@ int rq_decoder_add(rq_dec* d, uint32_t esi, const uint8_t* sym, size_t len, int*
     return RQ_OK;
 }
 
+// Decode: the library's fast path when every source symbol is held; otherwise the batched syndrome
+// decode on one block (subset of e + 8 received repairs first, all of them if that is
+// rank-deficient), staged through the device's pinned per-object buffer and stream.
 int rq_decoder_decode(rq_dec* d, uint8_t* out, int* ok) {
     if (!d || !ok) return fail(RQ_ERR_BAD_ARG, "null decoder/ok");
     const uint32_t K = d->p.K, T = d->T;
     *ok = 0;
     if (K > d->nfast + (uint32_t)d->slow.size()) return fail(RQ_ERR_NOT_ENOUGH, "not enough symbols to decode");
     if (d->nfast < K) {
-        const uint32_t Tp = (T + 3) & ~3u;
+        const uint32_t Tp = pad_row(T);
         std::vector<uint32_t> erased, resi;
         for (uint32_t i = 0; i < K; ++i)
             if (!d->have[i]) erased.push_back(i);
-        std::vector<uint8_t> data((size_t)K * Tp, 0), rep((size_t)d->slow.size() * Tp, 0);
-        for (uint32_t i = 0; i < K; ++i)
-            if (d->have[i]) std::memcpy(&data[(size_t)i * Tp], &d->fast[(size_t)i * T], T);
-        size_t r = 0;
-        for (auto& kv : d->slow) {
-            resi.push_back(kv.first);
-            std::memcpy(&rep[(r++) * Tp], kv.second.data(), T);
-        }
         DevCtx* ctx;
         int rc = get_ctx(&ctx);
         if (rc) return rc;
         std::lock_guard<std::mutex> lk(ctx->mu);
-        DevBuf dd, dr;
-        if ((rc = dd.ensure(data.size())) || (rc = dr.ensure(std::max<size_t>(rep.size(), 4)))) return rc;
-        HIP_TRY(hipMemcpy(dd.p, data.data(), data.size(), hipMemcpyHostToDevice));
-        if (!rep.empty()) HIP_TRY(hipMemcpy(dr.p, rep.data(), rep.size(), hipMemcpyHostToDevice));
+        hipStream_t st;
+        const size_t data_b = (size_t)K * Tp, rep_b = std::max<size_t>((size_t)d->slow.size() * Tp, 4);
+        if ((rc = obj_stream(ctx, &st)) || (rc = ctx->obj_h.ensure(data_b + rep_b)) ||
+            (rc = ctx->obj_d.ensure(data_b + rep_b)))
+            return rc;
+        uint8_t* h = ctx->obj_h.as<uint8_t>();
+        if (Tp == T) {
+            std::memcpy(h, d->fast.data(), data_b);
+        } else {
+            std::memset(h, 0, data_b);
+            for (uint32_t i = 0; i < K; ++i) std::memcpy(h + (size_t)i * Tp, &d->fast[(size_t)i * T], T);
+        }
+        size_t r = 0;
+        for (auto& kv : d->slow) {
+            resi.push_back(kv.first);
+            std::memcpy(h + data_b + (r++) * Tp, kv.second.data(), T);
+        }
+        uint8_t* dd = ctx->obj_d.as<uint8_t>();
+        HIP_TRY(hipMemcpyAsync(dd, h, data_b + r * Tp, hipMemcpyHostToDevice, st));
         const uint32_t ne = (uint32_t)erased.size(), nr = (uint32_t)resi.size();
-        int32_t st = 0;
-        rc = decode_locked(ctx, d->p, Tp, 1, dd.p, data.size(), &ne, erased.data(), &nr, resi.data(), dr.p, &st, nullptr);
+        int32_t status = 0;
+        PackOut po;
+        rc = decode_locked(ctx, d->p, Tp, 1, dd, data_b, &ne, erased.data(), &nr, resi.data(), dd + data_b, &status, st,
+                           &po);
         if (rc) return rc;
-        if (st != 1) return RQ_OK;  // rank-deficient: (false, nil, nil)
-        HIP_TRY(hipMemcpy(data.data(), dd.p, data.size(), hipMemcpyDeviceToHost));
-        for (uint32_t i : erased) std::memcpy(&d->fast[(size_t)i * T], &data[(size_t)i * Tp], T);
+        if (status != 1) return RQ_OK;  // rank-deficient: (false, nil, nil)
+        for (size_t i = 0; i < erased.size(); ++i)
+            std::memcpy(&d->fast[(size_t)erased[i] * T], po.rows.data() + i * Tp, T);
         // The library fills the missing rows into its own buffer as well (RQ/decoder.go:126-130).
         for (uint32_t i : erased) { d->have[i] = 1; d->nfast++; }
     }

@@ -40,6 +40,7 @@ EXPORTED = (
     "rq_decoder_create", "rq_decoder_k", "rq_decoder_add", "rq_decoder_decode", "rq_decoder_free",
     "rq_encode_batch", "rq_decode_batch", "rq_decode_batch_async", "rq_encode_batch_host", "rq_decode_batch_host", "rq_device_count", "rq_set_device",
     "rq_debug_colprog_eval", "rq_debug_colprog_emulate", "rq_debug_colprog_assemble", "rq_debug_decode_margin",
+    "rq_decode_blocks_host", "rq_host_alloc", "rq_host_free",
 )
 
 
@@ -64,6 +65,12 @@ class DecodeDesc(ctypes.Structure):
                 ("n_repair", ctypes.POINTER(ctypes.c_uint32)), ("repair_esi", ctypes.POINTER(ctypes.c_uint32)),
                 ("repair", ctypes.c_void_p), ("status", ctypes.POINTER(ctypes.c_int32)),
                 ("stream", ctypes.c_void_p)]
+
+
+class BlockIO(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("repair", ctypes.c_void_p), ("n_erased", ctypes.c_uint32),
+                ("erased", ctypes.POINTER(ctypes.c_uint32)), ("n_repair", ctypes.c_uint32),
+                ("repair_esi", ctypes.POINTER(ctypes.c_uint32)), ("status", ctypes.c_int32)]
 
 
 def build():
@@ -118,6 +125,10 @@ def lib():
             "rq_debug_colprog_assemble": ([ctypes.c_uint32, u32p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_size_t)],
                                           ctypes.c_int),
             "rq_debug_decode_margin": ([ctypes.c_uint32], ctypes.c_uint32),
+            "rq_decode_blocks_host": ([ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(BlockIO), ctypes.c_uint32,
+                                       ctypes.c_uint32], ctypes.c_int),
+            "rq_host_alloc": ([ctypes.c_size_t], vp),
+            "rq_host_free": ([vp], None),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -443,3 +454,27 @@ def decode_batch_host(db, data, repair, device_mask=0):
                    status=db.status.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), stream=None)
     _check(lib().rq_decode_batch_host(ctypes.byref(d), ctypes.c_uint32(device_mask)))
     return db.status
+
+
+def decode_blocks_host(K, T, blocks, device_mask=0):
+    """rq_decode_blocks_host: blocks = [(data, erased, repair_esi, repair_rows)] with data a writable
+    host uint8 buffer of K*T bytes (received source rows in place) and repair_rows [n, T] (host,
+    contiguous).  Recovered rows are written into each data buffer.  Returns the statuses."""
+    import numpy as np
+    arr = (BlockIO * max(len(blocks), 1))()
+    keep = []
+    for i, (data, erased, resi, rows) in enumerate(blocks):
+        dp, _ = _host_rows(data.reshape(1, -1) if hasattr(data, "reshape") else data)
+        er = np.asarray(erased, np.uint32)
+        re_ = np.asarray(resi, np.uint32)
+        rows = np.ascontiguousarray(rows, np.uint8) if not hasattr(rows, "data_ptr") else rows
+        rp = rows.data_ptr() if hasattr(rows, "data_ptr") else rows.ctypes.data
+        keep += [er, re_, rows]
+        arr[i].data = dp
+        arr[i].repair = rp
+        arr[i].n_erased = len(er)
+        arr[i].erased = er.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+        arr[i].n_repair = len(re_)
+        arr[i].repair_esi = re_.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+    _check(lib().rq_decode_blocks_host(K, T, arr, len(blocks), ctypes.c_uint32(device_mask)))
+    return [arr[i].status for i in range(len(blocks))]

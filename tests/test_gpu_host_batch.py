@@ -93,3 +93,57 @@ def test_host_batch_bad_device_mask(gpu, rq):
     with pytest.raises(rq.RaptorQError) as ei:
         rq.encode_batch_host(src, K, T, [K], out, device_mask=1 << 31)
     assert ei.value.code == rq.RQ_ERR_BAD_ARG
+
+
+@pytest.mark.parametrize("K,T,N", [(64, 1201, 80), (26, 1499, 32), (10, 3, 16)])
+def test_host_api_any_symbol_size(gpu, rq, oracle, K, T, N):
+    """T not a multiple of 4 through the host-memory API (rows padded in device staging): repairs
+    and recovered payloads equal the oracle's."""
+    nb = 5
+    esis = list(range(K, N))
+    rng = np.random.default_rng(T)
+    src = rng.integers(0, 256, (nb, K * T), dtype=np.uint8)
+    out = np.zeros((nb, len(esis) * T), np.uint8)
+    rq.encode_batch_host(src, K, T, esis, out)
+    for b in (0, nb - 1):
+        ref = oracle.OracleEncoder(src[b].tobytes(), T)
+        for r, e in enumerate(esis):
+            assert np.array_equal(out[b, r * T:(r + 1) * T], ref.gen_symbol(e)), (b, e)
+    er, rl, rows = [], [], []
+    for b in range(nb):
+        lost = set(rng.choice(N, 3, replace=False).tolist())
+        er.append(sorted(i for i in lost if i < K))
+        rl.append([e for e in esis if e not in lost])
+        rows += [out[b, (e - K) * T:(e - K + 1) * T] for e in rl[-1]]
+    data = src.copy()
+    for b in range(nb):
+        for i in er[b]:
+            data[b, i * T:(i + 1) * T] = 0
+    db = rq.DecodeBatch(K, T, er, rl)
+    st = rq.decode_batch_host(db, data, np.stack(rows))
+    assert (st == 1).all() and np.array_equal(data, src)
+
+
+def test_decode_blocks_host_matches_batch(gpu, rq):
+    """rq_decode_blocks_host (per-block buffers: a receiver's staging) decodes like
+    rq_decode_batch_host; blocks may sit anywhere in host memory, pinned or not."""
+    K, T, N, nb = 128, 1200, 148, 9
+    esis = list(range(K, N))
+    rng = np.random.default_rng(77)
+    src = rng.integers(0, 256, (nb, K * T), dtype=np.uint8)
+    rep = _device_encode(rq, gpu, src, K, T, esis).reshape(nb, N - K, T)
+    blocks = []
+    for b in range(nb):
+        lost = set(rng.choice(N, 7, replace=False).tolist())
+        er = sorted(i for i in lost if i < K)
+        rl = [e for e in esis if e not in lost]
+        buf = (torch.from_numpy(src[b].copy()).pin_memory() if b % 2 else src[b].copy())
+        view = buf.numpy() if hasattr(buf, "numpy") else buf
+        for i in er:
+            view[i * T:(i + 1) * T] = 0x33
+        blocks.append((buf, er, rl, np.stack([rep[b, e - K] for e in rl])))
+    st = rq.decode_blocks_host(K, T, blocks)
+    assert st == [1] * nb
+    for b, (buf, *_rest) in enumerate(blocks):
+        view = buf.numpy() if hasattr(buf, "numpy") else buf
+        assert np.array_equal(view, src[b])
