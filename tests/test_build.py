@@ -15,13 +15,15 @@ def test_clean_build_links(tmp_path):
     # copy the package sources (not its build/) and build them from nothing
     dst = tmp_path / "pkg"
     shutil.copytree(PKG / "csrc", dst / "csrc")
+    shutil.copytree(PKG / "fecquic", dst / "fecquic")
     shutil.copy(PKG / "Makefile", dst / "Makefile")
     (tmp_path / "include").mkdir()
     shutil.copy(ROOT / "include" / "rqhip.h", tmp_path / "include" / "rqhip.h")
     r = subprocess.run(["make", "-s", "-C", str(dst), "-j8", "all"], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-4000:]
     so = dst / "build" / "librqhip.so"
-    assert so.exists()
+    for f in ("librqhip.so", "librqcpu.so", "libfecquic.so", "fecquic", "raptorq_eval"):
+        assert (dst / "build" / f).exists(), f
     L = ctypes.CDLL(str(so))
     txt = re.sub(r"/\*.*?\*/", "", (ROOT / "include/rqhip.h").read_text(), flags=re.S)
     for name in sorted(set(re.findall(r"\b(rq_[a-z_]+)\s*\(", txt))):
