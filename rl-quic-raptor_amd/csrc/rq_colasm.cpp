@@ -506,7 +506,7 @@ bool divmagic(uint32_t d, uint32_t limit, uint32_t* magic, uint32_t* shift) {
 struct Policy {
     std::string src = " nt", out = " nt", scr_st = "", scr_ld = " sc1";
     Policy() {
-        if (const char* e = std::getenv("RQHIP_POLICY")) {
+        if (const char* e = knob("RQHIP_POLICY")) {
             std::string v(e), f[4];
             int i = 0;
             for (char c : v) {
@@ -523,7 +523,7 @@ struct Policy {
 // 2 drops LDS spill traffic, 4 replaces source loads by register writes, 8 drops output stores,
 // 16 loads source rows in increasing row order (wrong rows; measures the cost of the random order).
 static uint32_t diag_mask() {
-    const char* e = std::getenv("RQHIP_DIAG");
+    const char* e = knob("RQHIP_DIAG");
     return e ? (uint32_t)std::atoi(e) : 0u;
 }
 

@@ -13,11 +13,6 @@
 
 namespace rq {
 
-int g_lab = 0;  // experiment knob (lab tools only)
-std::vector<uint32_t> g_lab_force;  // lab: columns forced inactive before peeling
-std::vector<int32_t> g_lab_tag;     // lab: context tag per IR node (built when g_lab & 2)
-int32_t g_lab_ctx = -1;
-
 namespace {
 
 using Bits = std::vector<uint64_t>;
@@ -87,7 +82,6 @@ bool eliminate(const Params& p, Elim* e, std::string* err) {
     auto& cstate = e->cstate;
     cstate.assign(L, ACTIVE);
     for (uint32_t c = W; c < L; ++c) cstate[c] = INACTIVE;  // PI columns start inactive
-    for (uint32_t c : g_lab_force) if (c < W && cstate[c] == ACTIVE) cstate[c] = INACTIVE;
     std::vector<uint32_t> cnt(NR, 0);
     std::vector<uint8_t> rdone(NR, 0);
     for (uint32_t r = 0; r < NR; ++r)
@@ -98,7 +92,7 @@ bool eliminate(const Params& p, Elim* e, std::string* err) {
     std::vector<size_t> bhead(64, 0);
     for (uint32_t r = 0; r < NR; ++r) bucket[std::min<uint32_t>(cnt[r], 63)].push_back(r);
     e->ucols.clear();
-    for (uint32_t c = 0; c < L; ++c) if (cstate[c] == INACTIVE) e->ucols.push_back(c);
+    for (uint32_t c = W; c < L; ++c) e->ucols.push_back(c);
     e->col_order.assign(L, -1);
     auto drop_col = [&](uint32_t c, uint32_t except_row) {
         for (uint32_t r : col_rows[c]) {
@@ -109,19 +103,6 @@ bool eliminate(const Params& p, Elim* e, std::string* err) {
     };
     for (;;) {
         int32_t r = -1;
-        if ((g_lab & 1) && true) {
-            // lab: among degree-1 rows, the one whose active column is smallest
-            auto& bk = bucket[1];
-            uint32_t bestc = UINT32_MAX; size_t bi = 0;
-            for (size_t q = bhead[1]; q < bk.size(); ++q) {
-                const uint32_t x = bk[q];
-                if (rdone[x] || cnt[x] != 1) continue;
-                uint32_t ac = UINT32_MAX;
-                for (uint32_t c : rows[x]) if (cstate[c] == ACTIVE) { ac = c; break; }
-                if (ac < bestc) { bestc = ac; r = (int32_t)x; bi = q; }
-            }
-            if (r >= 0) { std::swap(bk[bi], bk[bhead[1]]); bhead[1]++; }
-        }
         for (uint32_t b = 1; b < 64 && r < 0; ++b) {
             auto& bk = bucket[b];
             while (bhead[b] < bk.size()) {
@@ -327,7 +308,6 @@ struct Builder {
         IrNode n;
         n.k = k; n.a = a; n.b = b; n.c = c; n.imm = imm;
         ir->nodes.push_back(n);
-        if (g_lab & 2) g_lab_tag.push_back(g_lab_ctx);
         return (uint32_t)ir->nodes.size() - 1;
     }
     // XOR of a term list (NOVAL = zero terms are skipped); NOVAL if every term is zero.
@@ -406,7 +386,6 @@ bool build(const Params& p, const std::vector<OutDesc>& outs, ColIR* ir, std::st
                 continue;
             }
             std::vector<uint32_t> t;
-            g_lab_ctx = (int32_t)e.piv_col[k];
             t.push_back(D(e.piv_row[k]));
             for (uint32_t j : e.deps[k]) t.push_back(y[j]);
             y[k] = B.xsum(t);
@@ -461,7 +440,6 @@ bool build(const Params& p, const std::vector<OutDesc>& outs, ColIR* ir, std::st
     uint32_t t = NOVAL;
     for (uint32_t j = 0; j < KS; ++j) {
         const uint32_t yj = (e.cstate[j] == 1) ? getY((uint32_t)e.col_order[j]) : NOVAL;
-        g_lab_ctx = (int32_t)j;
         t = B.xt(t, yj);
         if (j + 1 < KS && t != NOVAL) {
             part[e.ma[j]].push(B, t);
@@ -494,7 +472,6 @@ bool build(const Params& p, const std::vector<OutDesc>& outs, ColIR* ir, std::st
     ir->phase_start[2] = (uint32_t)ir->nodes.size();
     std::vector<uint32_t> CF(H, NOVAL);
     for (uint32_t f = 0; f < H; ++f) {
-        g_lab_ctx = 200000 + (int32_t)f;
         uint32_t acc = NOVAL;
         for (int bt = 7; bt >= 0; --bt) {
             std::vector<uint32_t> terms;
@@ -510,7 +487,6 @@ bool build(const Params& p, const std::vector<OutDesc>& outs, ColIR* ir, std::st
     // ---- outputs
     ir->phase_start[3] = (uint32_t)ir->nodes.size();
     for (uint32_t o = 0; o < no; ++o) {
-        g_lab_ctx = 100000 + (int32_t)o;
         uint32_t v;
         if (outs[o].source) {
             v = outs[o].row < K ? B.add(IR_LOAD, NOVAL, NOVAL, NOVAL, outs[o].row) : NOVAL;
@@ -536,7 +512,6 @@ bool build(const Params& p, const std::vector<OutDesc>& outs, ColIR* ir, std::st
                 if (x != NOVAL) live[x] = 1;
         }
         std::vector<uint32_t> remap(ir->nodes.size(), NOVAL);
-        std::vector<int32_t> ktag;
         std::vector<IrNode> kept;
         kept.reserve(ir->nodes.size());
         uint32_t ph = 0, new_ph[4] = {0, 0, 0, 0};
@@ -547,12 +522,10 @@ bool build(const Params& p, const std::vector<OutDesc>& outs, ColIR* ir, std::st
             for (uint32_t* x : {&n.a, &n.b, &n.c})
                 if (*x != NOVAL) *x = remap[*x];
             remap[i] = (uint32_t)kept.size();
-            if (g_lab & 2) ktag.push_back(g_lab_tag[i]);
             kept.push_back(n);
         }
         while (ph < 4) new_ph[ph++] = (uint32_t)kept.size();
         ir->nodes.swap(kept);
-        if (g_lab & 2) g_lab_tag.swap(ktag);
         std::memcpy(ir->phase_start, new_ph, sizeof new_ph);
     }
     auto& st = ir->st;

@@ -17,12 +17,25 @@
 // XOR of 2-3 values or a multiply by alpha (xtime) -- no general GF(256) multiply survives.
 #pragma once
 #include <cstdint>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
 #include "rq_core.hpp"
 
 namespace rq {
+
+// Experiment knobs (RQHIP_DIAG, RQHIP_ALLOC, RQHIP_POLICY, ...: tuning sweeps and diagnostic modes,
+// some of which produce wrong bytes on purpose) are read only in builds made with
+// `make EXPERIMENTS=1`; the shipped library ignores the environment.
+inline const char* knob(const char* name) {
+#ifdef RQHIP_EXPERIMENTS
+    return std::getenv(name);
+#else
+    (void)name;
+    return nullptr;
+#endif
+}
 
 enum IrKind : uint8_t {
     IR_LOAD = 0,  // imm = source row (< K)

@@ -204,7 +204,7 @@ int ensure_tables(DevCtx* ctx) {
 const AllocOpts& alloc_options() {
     static const AllocOpts o = [] {
         AllocOpts r;
-        if (const char* e = std::getenv("RQHIP_ALLOC")) {
+        if (const char* e = knob("RQHIP_ALLOC")) {
             unsigned v[6] = {0, 0, 0, 0, 0, 0};
             std::sscanf(e, "%u,%u,%u,%u,%u,%u", &v[0], &v[1], &v[2], &v[3], &v[4], &v[5]);
             if (v[5]) r.n_lds = std::min<uint32_t>(v[5] - 1, 512);
@@ -214,10 +214,10 @@ const AllocOpts& alloc_options() {
             if (v[3]) r.la_reload = v[3];
             if (v[4]) r.max_vmem = std::min<uint32_t>(v[4], 60);
         }
-        if (const char* h = std::getenv("RQHIP_LDS_HORIZON")) r.lds_horizon = (uint32_t)std::atoi(h);
-        if (const char* h = std::getenv("RQHIP_LA_DMA")) r.la_dma = (uint32_t)std::atoi(h);
-        if (const char* h = std::getenv("RQHIP_SRC_BIAS")) r.src_bias = (uint32_t)std::atoi(h);
-        if (const char* h = std::getenv("RQHIP_SRC_LDS")) r.src_lds = (uint32_t)std::atoi(h);
+        if (const char* h = knob("RQHIP_LDS_HORIZON")) r.lds_horizon = (uint32_t)std::atoi(h);
+        if (const char* h = knob("RQHIP_LA_DMA")) r.la_dma = (uint32_t)std::atoi(h);
+        if (const char* h = knob("RQHIP_SRC_BIAS")) r.src_bias = (uint32_t)std::atoi(h);
+        if (const char* h = knob("RQHIP_SRC_LDS")) r.src_lds = (uint32_t)std::atoi(h);
         return r;
     }();
     return o;
@@ -379,7 +379,7 @@ int get_col_kernel(DevCtx* ctx, const Params& p, const uint32_t* esi, uint32_t n
 // XCD-aware wave order in column programs (RQHIP_XCD=0 disables it for experiments).
 bool xcd_order() {
     static const bool on = [] {
-        const char* e = std::getenv("RQHIP_XCD");
+        const char* e = knob("RQHIP_XCD");
         return !(e && e[0] == '0');
     }();
     return on;

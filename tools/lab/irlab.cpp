@@ -1,12 +1,13 @@
-// IR live-set analysis (host-only experiment tool).
+// IR live-set analysis (host-only experiment tool): builds the column program IR for (K, R repairs)
+// and reports node counts, the live-value profile over program order, what the values live at the
+// peak are waiting for, and the forward pass's live set in pull vs push form.
+// g++ -O2 -std=c++17 -I rl-quic-raptor_amd/csrc tools/lab/irlab.cpp -o /tmp/irlab && /tmp/irlab 1024 76
 #include "../../rl-quic-raptor_amd/csrc/rq_colprog.cpp"
 #include <cstdio>
 namespace rq { const GF& gf() { static const GF g; return g; } }
 using namespace rq;
 void classify(const ColIR& ir, uint32_t at);
-namespace rq { extern int g_lab; }
 int main(int argc, char** argv) {
-    if (getenv("LAB")) rq::g_lab = atoi(getenv("LAB"));
     uint32_t K = argc > 1 ? atoi(argv[1]) : 1024, R = argc > 2 ? atoi(argv[2]) : 76;
     Params p; params_for_K(K, &p);
     std::vector<uint32_t> esi; for (uint32_t i = 0; i < R; ++i) esi.push_back(K + i);
