@@ -175,6 +175,10 @@ int rq_debug_colprog_assemble(uint32_t K, const uint32_t* esi, uint32_t n_out, s
  * and re-solve on all of them only if that subset is rank-deficient.  Sets the margin (tests force
  * the second pass with 0) and returns the previous one.  Results never depend on it. */
 uint32_t rq_debug_decode_margin(uint32_t margin);
+/* The column program's IR schedule for the three rq_debug_colprog_* entry points: -1 (default)
+ * chooses like the engine (cost model over the schedules), 0 = one demand-driven column scan,
+ * P >= 1 = peeling-order production with P Horner passes.  Returns the previous setting. */
+int rq_debug_colprog_passes(int passes);
 
 #ifdef __cplusplus
 }

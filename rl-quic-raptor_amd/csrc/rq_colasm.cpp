@@ -483,6 +483,50 @@ bool allocate_colprog(const ColIR& ir, const AllocOpts& o, MProg* mp, std::strin
     return a.run();
 }
 
+// One wave per SIMD issues one instruction per 4-cycle slot whatever its kind, so the launch time is
+// close to linear in issue slots (an xtime is 6 VALU instructions; a buffer access carries the SALU
+// that forms its soffset), plus a stall term per global-scratch spill or reload.  Least-squares fit
+// over the K=1024 schedule sweep (profiles/r02g/passes_sweep.log): 7.6e-6 ms per slot and 12 slots
+// per scratch access, within 2 % on all seven points.
+double colprog_cost(const MProg& mp) {
+    double slots = 0;
+    for (const MInst& m : mp.ins) {
+        switch (m.op) {
+            case MI_XT: case MI_XTX: slots += 6; break;
+            case MI_LDSRC: case MI_STOUT: case MI_SPST: case MI_SPLD: slots += 2; break;
+            default: slots += 1;
+        }
+    }
+    return slots + 12.0 * (double)(mp.st.spst + mp.st.spld);
+}
+
+bool compile_colprog(const Params& p, const uint32_t* esi, uint32_t n_out, const AllocOpts& o, ColIR* ir, MProg* mp,
+                     std::string* err, uint32_t* passes_out) {
+    double best = 0;
+    bool have = false;
+    std::vector<uint32_t> cand{0u, 1u, 2u, 3u, 4u, 5u, 6u};
+    if (const char* f = knob("RQHIP_PASSES")) cand = {(uint32_t)std::atoi(f)};  // experiments: fixed schedule
+    for (uint32_t P : cand) {
+        ColIR cir;
+        MProg cmp;
+        const bool ok = esi ? build_colprog(p, esi, n_out, &cir, err, P) : build_colprog_C(p, &cir, err, P);
+        if (!ok || !allocate_colprog(cir, o, &cmp, err)) {
+            if (P == 0) return false;
+            continue;
+        }
+        const double c = colprog_cost(cmp);
+        if (!have || c < best) {
+            best = c;
+            have = true;
+            *ir = std::move(cir);
+            *mp = std::move(cmp);
+            if (passes_out) *passes_out = P;
+        }
+        if (P == 0 && cmp.st.spst == 0) break;  // fits on chip: the single scan is cheapest
+    }
+    return have;
+}
+
 bool divmagic(uint32_t d, uint32_t limit, uint32_t* magic, uint32_t* shift) {
     if (d == 0) return false;
     for (uint32_t s = 0; s < 32; ++s) {

@@ -81,6 +81,17 @@ struct MProg {
 
 bool allocate_colprog(const ColIR& ir, const AllocOpts& o, MProg* mp, std::string* err);
 
+// Builds and allocates the column program for (K, outputs; esi = NULL: all L intermediate symbols),
+// choosing the IR schedule (build_colprog's `passes`) that minimises the launch-time model
+// colprog_cost: the demand-driven scan when it needs no global scratch, else the number of Horner
+// passes that best trades the extra VALU work against spill traffic.  *passes_out = the choice.
+bool compile_colprog(const Params& p, const uint32_t* esi, uint32_t n_out, const AllocOpts& o, ColIR* ir, MProg* mp,
+                     std::string* err, uint32_t* passes_out = nullptr);
+// Model of one launch's time per 64-column item (units: issue slots): every instruction of the one
+// resident wave per SIMD takes an issue slot, plus a stall term per global-scratch spill / reload;
+// fitted on the K=1024 schedule sweep of round 2 (profiles/r02g).
+double colprog_cost(const MProg& mp);
+
 // Kernel argument block of the emitted kernel (must match the prologue in emit_colprog_asm).
 struct ColKernArgs {
     uint64_t src;         // block b row i at src + b*src_stride + i*T

@@ -353,7 +353,14 @@ struct OutDesc {
     std::vector<uint32_t> cols;
 };
 
-bool build(const Params& p, const std::vector<OutDesc>& outs, ColIR* ir, std::string* err) {
+// passes = 0: demand-driven order (each y_k emitted when the single column scan first needs it).
+// passes = P >= 1: y_k in peeling order, each pushed at once into the rows that depend on it (their
+// accumulators), into the remaining-row sums and into the output sums; the HDPC Horner scan runs P
+// times, pass q over the y values produced since pass q-1 (the others count as zero: the scan is
+// linear, so the P chains' pushes and end values add up to the single scan's).  A y value then lives
+// only until its pass instead of until its column comes up in one global scan, which bounds the live
+// set by about npiv / P plus the open accumulators, at 2 ops per column per extra pass.
+bool build(const Params& p, const std::vector<OutDesc>& outs, uint32_t passes, ColIR* ir, std::string* err) {
     Elim e;
     if (!eliminate(p, &e, err)) return false;
     *ir = ColIR();
@@ -438,7 +445,48 @@ bool build(const Params& p, const std::vector<OutDesc>& outs, ColIR* ir, std::st
     std::vector<Acc> b2acc(n2), oacc(no), part(H);
     for (uint32_t i = 0; i < n2; ++i) b2acc[i].push(B, D(e.rem[i]));
     uint32_t t = NOVAL;
-    for (uint32_t j = 0; j < KS; ++j) {
+    if (passes) {  // peeling-order production, push-mode dependencies, P Horner passes
+        std::vector<std::vector<uint32_t>> dependents(npiv);
+        for (uint32_t k = 0; k < npiv; ++k)
+            for (uint32_t j : e.deps[k]) dependents[j].push_back(k);
+        std::vector<Acc> yacc(npiv);
+        std::vector<uint32_t> tends;
+        uint32_t done = 0;  // y_0 .. y_(done-1) consumed by earlier passes
+        auto pass = [&](uint32_t upto) {
+            uint32_t tp = NOVAL;
+            for (uint32_t j = 0; j < KS; ++j) {
+                uint32_t yj = NOVAL;
+                if (e.cstate[j] == 1) {
+                    const uint32_t k = (uint32_t)e.col_order[j];
+                    if (k >= done && k < upto) yj = y[k];
+                }
+                tp = B.xt(tp, yj);
+                if (j + 1 < KS && tp != NOVAL) {
+                    part[e.ma[j]].push(B, tp);
+                    part[e.mb[j]].push(B, tp);
+                }
+            }
+            if (tp != NOVAL) tends.push_back(tp);
+            done = upto;
+        };
+        uint32_t q = 1;
+        for (uint32_t k = 0; k < npiv; ++k) {
+            std::vector<uint32_t> tt{D(e.piv_row[k]), yacc[k].get(B)};
+            y[k] = B.xsum(tt);
+            ystate[k] = 2;
+            for (uint32_t d : dependents[k]) yacc[d].push(B, y[k]);
+            const uint32_t c = e.piv_col[k];
+            for (uint32_t i : col_rem[c]) b2acc[i].push(B, y[k]);
+            for (uint32_t o : col_outs[c]) oacc[o].push(B, y[k]);
+            if (k + 1 == (uint64_t)npiv * q / passes) {
+                pass(k + 1);
+                ++q;
+            }
+        }
+        if (done < npiv) pass(npiv);
+        t = B.xsum(tends);
+    }
+    for (uint32_t j = 0; j < KS && !passes; ++j) {
         const uint32_t yj = (e.cstate[j] == 1) ? getY((uint32_t)e.col_order[j]) : NOVAL;
         t = B.xt(t, yj);
         if (j + 1 < KS && t != NOVAL) {
@@ -450,7 +498,7 @@ bool build(const Params& p, const std::vector<OutDesc>& outs, ColIR* ir, std::st
             for (uint32_t o : col_outs[j]) oacc[o].push(B, yj);
         }
     }
-    for (uint32_t c = KS; c < e.L; ++c) {  // pivoted columns past the HDPC range (none in practice)
+    for (uint32_t c = KS; c < e.L && !passes; ++c) {  // pivoted columns past the HDPC range (none in practice)
         if (e.cstate[c] != 1) continue;
         const uint32_t yc = getY((uint32_t)e.col_order[c]);
         for (uint32_t i : col_rem[c]) b2acc[i].push(B, yc);
@@ -551,7 +599,7 @@ inline uint32_t xtime4(uint32_t x) {
 
 }  // namespace
 
-bool build_colprog(const Params& p, const uint32_t* esi, uint32_t n_out, ColIR* ir, std::string* err) {
+bool build_colprog(const Params& p, const uint32_t* esi, uint32_t n_out, ColIR* ir, std::string* err, uint32_t passes) {
     std::vector<OutDesc> outs(n_out);
     uint32_t cols[64];
     for (uint32_t o = 0; o < n_out; ++o) {
@@ -559,13 +607,13 @@ bool build_colprog(const Params& p, const uint32_t* esi, uint32_t n_out, ColIR* 
         const int n = lt_cols(p, esi[o] + p.Kp - p.K, cols);
         outs[o].cols.assign(cols, cols + n);
     }
-    return build(p, outs, ir, err);
+    return build(p, outs, passes, ir, err);
 }
 
-bool build_colprog_C(const Params& p, ColIR* ir, std::string* err) {
+bool build_colprog_C(const Params& p, ColIR* ir, std::string* err, uint32_t passes) {
     std::vector<OutDesc> outs(p.L);
     for (uint32_t c = 0; c < p.L; ++c) outs[c].cols = {c};
-    return build(p, outs, ir, err);
+    return build(p, outs, passes, ir, err);
 }
 
 void eval_colprog(const ColIR& ir, const uint8_t* src, uint32_t T, uint8_t* out) {

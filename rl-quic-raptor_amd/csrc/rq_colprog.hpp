@@ -67,9 +67,12 @@ struct ColIR {
 
 // Outputs are ESIs with the library's GenSymbol meaning (RQ/encoder.go:36-41): esi < K is the
 // zero-padded source row, otherwise the LT symbol of ISI esi + K' - K.  p.K is the library K.
-bool build_colprog(const Params& p, const uint32_t* esi, uint32_t n_out, ColIR* ir, std::string* err);
+// passes: 0 = one demand-driven column scan; P >= 1 = peeling-order production with P Horner passes
+// (see build() in rq_colprog.cpp).  Every choice computes the same bytes.
+bool build_colprog(const Params& p, const uint32_t* esi, uint32_t n_out, ColIR* ir, std::string* err,
+                   uint32_t passes = 0);
 // Outputs are the L intermediate symbols C[0..L-1] (per-object encoder: GenSymbol gathers).
-bool build_colprog_C(const Params& p, ColIR* ir, std::string* err);
+bool build_colprog_C(const Params& p, ColIR* ir, std::string* err, uint32_t passes = 0);
 // Host evaluation of the IR on one block (test reference for the compiler, not a product path):
 // src = K rows x T bytes, out = n_out rows x T bytes.
 void eval_colprog(const ColIR& ir, const uint8_t* src, uint32_t T, uint8_t* out);

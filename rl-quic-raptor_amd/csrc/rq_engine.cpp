@@ -241,6 +241,9 @@ const std::string& cache_dir() {
         else if (const char* x = std::getenv("XDG_CACHE_HOME")) r = std::string(x) + "/rqhip";
         else if (const char* h = std::getenv("HOME")) r = std::string(h) + "/.cache/rqhip";
         if (r == "0") r.clear();
+#ifdef RQHIP_EXPERIMENTS
+        r.clear();  // experiment knobs change the generated code without changing the cache key
+#endif
         return r;
     }();
     return d;
@@ -337,10 +340,11 @@ int get_col_kernel(DevCtx* ctx, const Params& p, const uint32_t* esi, uint32_t n
         if (path.empty() || !cache_load(path, &ch, &kname, &co)) {
             ColIR ir;
             std::string err;
-            const bool ok = all_C ? build_colprog_C(p, &ir, &err) : build_colprog(p, esi, n_esi, &ir, &err);
-            if (!ok) { ctx->colk.erase(key); return fail(RQ_ERR_PLAN, err); }
             MProg mp;
-            if (!allocate_colprog(ir, ao, &mp, &err)) { ctx->colk.erase(key); return fail(RQ_ERR_PLAN, err); }
+            if (!compile_colprog(p, all_C ? nullptr : esi, n_esi, ao, &ir, &mp, &err)) {
+                ctx->colk.erase(key);
+                return fail(RQ_ERR_PLAN, err);
+            }
             // distinct symbol per program so kernel traces separate encode, decode and C programs
             kname = "rq_colprog_K" + std::to_string(p.K) + (all_C ? "_C" : "_n" + std::to_string(n_esi));
             co.clear();
@@ -997,6 +1001,22 @@ int rq_set_device(int device) {
     return RQ_OK;
 }
 
+int g_debug_passes = -1;  // rq_debug_colprog_passes: fixed IR schedule for the debug entry points
+
+bool debug_compile(const Params& p, const uint32_t* esi, uint32_t n_out, const AllocOpts& o, ColIR* ir, MProg* mp,
+                   std::string* err) {
+    if (g_debug_passes < 0) return compile_colprog(p, esi, n_out, o, ir, mp, err);
+    const uint32_t P = (uint32_t)g_debug_passes;
+    const bool ok = esi ? build_colprog(p, esi, n_out, ir, err, P) : build_colprog_C(p, ir, err, P);
+    return ok && allocate_colprog(*ir, o, mp, err);
+}
+
+int rq_debug_colprog_passes(int passes) {
+    const int old = g_debug_passes;
+    g_debug_passes = passes;
+    return old;
+}
+
 int rq_debug_colprog_eval(uint32_t K, uint32_t T, const uint32_t* esi, uint32_t n_out, const uint8_t* src,
                           uint8_t* out, uint32_t stats[12]) {
     Params p;
@@ -1004,9 +1024,9 @@ int rq_debug_colprog_eval(uint32_t K, uint32_t T, const uint32_t* esi, uint32_t 
     if (rc) return fail(rc, "k is too big");
     if (T == 0 || T % 4) return fail(RQ_ERR_BAD_ARG, "T must be a positive multiple of 4");
     ColIR ir;
+    MProg mp;
     std::string err;
-    const bool ok = esi ? build_colprog(p, esi, n_out, &ir, &err) : build_colprog_C(p, &ir, &err);
-    if (!ok) return fail(RQ_ERR_PLAN, err);
+    if (!debug_compile(p, esi, n_out, alloc_options(), &ir, &mp, &err)) return fail(RQ_ERR_PLAN, err);
     if (src && out) eval_colprog(ir, src, T, out);
     if (stats) {
         const auto& s = ir.st;
@@ -1026,8 +1046,6 @@ int rq_debug_colprog_emulate(uint32_t K, uint32_t T, const uint32_t* esi, uint32
     if (T == 0 || T % 4) return fail(RQ_ERR_BAD_ARG, "T must be a positive multiple of 4");
     ColIR ir;
     std::string err;
-    const bool ok = esi ? build_colprog(p, esi, n_out, &ir, &err) : build_colprog_C(p, &ir, &err);
-    if (!ok) return fail(RQ_ERR_PLAN, err);
     AllocOpts o = alloc_options();
     if (opts) {
         if (opts[0]) o.n_vgpr = std::min<uint32_t>(opts[0], V_ALLOC);
@@ -1038,7 +1056,7 @@ int rq_debug_colprog_emulate(uint32_t K, uint32_t T, const uint32_t* esi, uint32
         if (opts[5]) o.n_lds = std::min<uint32_t>(opts[5] - 1, 512);
     }
     MProg mp;
-    if (!allocate_colprog(ir, o, &mp, &err)) return fail(RQ_ERR_PLAN, err);
+    if (!debug_compile(p, esi, n_out, o, &ir, &mp, &err)) return fail(RQ_ERR_PLAN, err);
     if (src && out && !emulate_colprog(mp, src, T, out, &err)) return fail(RQ_ERR_PLAN, err);
     if (stats) {
         const auto& s = mp.st;
@@ -1061,10 +1079,8 @@ int rq_debug_colprog_assemble(uint32_t K, const uint32_t* esi, uint32_t n_out, s
     if (rc) return fail(rc, "k is too big");
     ColIR ir;
     std::string err;
-    const bool ok = esi ? build_colprog(p, esi, n_out, &ir, &err) : build_colprog_C(p, &ir, &err);
-    if (!ok) return fail(RQ_ERR_PLAN, err);
     MProg mp;
-    if (!allocate_colprog(ir, alloc_options(), &mp, &err)) return fail(RQ_ERR_PLAN, err);
+    if (!debug_compile(p, esi, n_out, alloc_options(), &ir, &mp, &err)) return fail(RQ_ERR_PLAN, err);
     std::vector<char> co;
     if (!comgr_assemble(emit_colprog_asm(mp, "rq_colprog"), &co, &err)) return fail(RQ_ERR_PLAN, err);
     if (code_bytes) *code_bytes = co.size();

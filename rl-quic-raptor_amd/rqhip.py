@@ -40,7 +40,7 @@ EXPORTED = (
     "rq_decoder_create", "rq_decoder_k", "rq_decoder_add", "rq_decoder_decode", "rq_decoder_free",
     "rq_encode_batch", "rq_decode_batch", "rq_decode_batch_async", "rq_encode_batch_host", "rq_decode_batch_host", "rq_device_count", "rq_set_device",
     "rq_debug_colprog_eval", "rq_debug_colprog_emulate", "rq_debug_colprog_assemble", "rq_debug_decode_margin",
-    "rq_decode_blocks_host", "rq_host_alloc", "rq_host_free",
+    "rq_decode_blocks_host", "rq_host_alloc", "rq_host_free", "rq_debug_colprog_passes",
 )
 
 
@@ -129,6 +129,7 @@ def lib():
                                        ctypes.c_uint32], ctypes.c_int),
             "rq_host_alloc": ([ctypes.c_size_t], vp),
             "rq_host_free": ([vp], None),
+            "rq_debug_colprog_passes": ([ctypes.c_int], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)

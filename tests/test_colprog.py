@@ -114,3 +114,25 @@ def test_program_size_and_assembly(rq):
     assert rq.colprog_assemble(64, list(range(64, 80))) > 1000
     # a full-size program (>128 KiB of code: the loop back-edge must not be a 16-bit branch)
     assert rq.colprog_assemble(1024, list(range(1024, 1100))) > 131072
+
+
+@pytest.mark.parametrize("passes", [0, 1, 2, 3, 5])
+@pytest.mark.parametrize("K,T,nrep", [(64, 16, 16), (1024, 8, 76), (2048, 4, 30)])
+def test_every_ir_schedule_matches_oracle(rq, oracle, K, T, nrep, passes):
+    """Each IR schedule the engine may choose (one demand-driven scan, or peeling-order production
+    with P Horner passes, rq_colprog.cpp build()) gives the reference bytes, as IR and as the
+    allocated, emulated machine program."""
+    rng = np.random.default_rng(K + 11 * passes)
+    data = rng.integers(0, 256, K * T, dtype=np.uint8)
+    esis = _esis(K, nrep)
+    enc = oracle.OracleEncoder(data.tobytes(), T)
+    old = rq.lib().rq_debug_colprog_passes(passes)
+    try:
+        ir_out = rq.colprog_eval(K, T, esis, data)
+        mp_out, st = rq.colprog_emulate(K, T, esis, data)
+    finally:
+        rq.lib().rq_debug_colprog_passes(old)
+    for i, e in enumerate(esis):
+        ref = enc.gen_symbol(e)
+        assert np.array_equal(ir_out[i], ref), (K, passes, e)
+        assert np.array_equal(mp_out[i], ref), (K, passes, e)

@@ -2,6 +2,7 @@
 
 usage: python tools/colbench.py [K] [T] [N] [blocks] [iters]
 """
+import os
 import sys
 import time
 from pathlib import Path
@@ -13,6 +14,9 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT / "rl-quic-raptor_amd"))
 sys.path.insert(0, str(ROOT))
 import rqhip  # noqa: E402
+
+if os.environ.get("RQHIP_LIB"):  # an alternative build (e.g. tools/build_experiments.sh)
+    rqhip.LIB_PATH = Path(os.environ["RQHIP_LIB"])
 
 
 def main():
