@@ -42,6 +42,7 @@ struct Allocator {
     std::deque<std::pair<uint64_t, int>> pend_loads;  // (seq, reg)
     uint64_t lseq = 0, lretired = 0;                // LDS operations (lgkmcnt, in order, max 15)
     std::deque<std::pair<uint64_t, int>> pend_lds;
+    std::vector<size_t> vm_ins{0}, l_ins{0};        // seq -> instruction index at issue
     using HE = std::pair<uint32_t, uint32_t>;       // (next use, value)
     std::priority_queue<HE, std::vector<HE>, std::greater<HE>> reload_q;
     bool failed = false;
@@ -75,8 +76,13 @@ struct Allocator {
             pend_loads.pop_front();
         }
     }
-    void wait_seq(uint64_t s) {  // make op `s` complete
+    // Make op `s` complete.  The wait also covers the younger operations issued at least
+    // wait_age instructions ago (done by now in all likelihood), so the next uses find them retired
+    // and need no s_waitcnt of their own.
+    void wait_seq(uint64_t s) {
         if (s == 0 || s <= retired) return;
+        const size_t now = mp->ins.size();
+        while (s < seq && vm_ins[s + 1] + o.wait_age <= now) ++s;
         const uint64_t n = std::min<uint64_t>(seq - s, 63);
         emit(MI_WAIT, -1, -1, -1, -1, (uint32_t)n);
         mp->st.wait++;
@@ -89,6 +95,7 @@ struct Allocator {
             mp->st.wait++;
             retire_to(seq - n);
         }
+        vm_ins.push_back(mp->ins.size());
         return ++seq;
     }
 
@@ -103,6 +110,8 @@ struct Allocator {
     }
     void wait_lseq(uint64_t s) {
         if (s == 0 || s <= lretired) return;
+        const size_t now = mp->ins.size();
+        while (s < lseq && l_ins[s + 1] + o.lwait_age <= now) ++s;
         const uint64_t n = std::min<uint64_t>(lseq - s, 15);
         emit(MI_WAITL, -1, -1, -1, -1, (uint32_t)n);
         mp->st.waitl++;
@@ -114,6 +123,7 @@ struct Allocator {
             mp->st.waitl++;
             retire_l(lseq - 14);
         }
+        l_ins.push_back(mp->ins.size());
         return ++lseq;
     }
     bool busy(int r) const { return inflight[r] || linflight[r]; }
@@ -484,16 +494,17 @@ bool allocate_colprog(const ColIR& ir, const AllocOpts& o, MProg* mp, std::strin
 }
 
 // One wave per SIMD issues one instruction per 4-cycle slot whatever its kind, so the launch time is
-// close to linear in issue slots (an xtime is 6 VALU instructions; a buffer access carries the SALU
-// that forms its soffset), plus a stall term per global-scratch spill or reload.  Least-squares fit
+// close to linear in issue slots (an xtime is 5 VALU instructions; an output store carries the SALU that
+// forms its soffset, a source load 1/8 of an s_load + wait), plus a stall term per global-scratch spill or reload.  Least-squares fit
 // over the K=1024 schedule sweep (profiles/r02g/passes_sweep.log): 7.6e-6 ms per slot and 12 slots
 // per scratch access, within 2 % on all seven points.
 double colprog_cost(const MProg& mp) {
     double slots = 0;
     for (const MInst& m : mp.ins) {
         switch (m.op) {
-            case MI_XT: case MI_XTX: slots += 6; break;
-            case MI_LDSRC: case MI_STOUT: case MI_SPST: case MI_SPLD: slots += 2; break;
+            case MI_XT: case MI_XTX: slots += 5; break;
+            case MI_LDSRC: slots += 1.125; break;
+            case MI_STOUT: slots += 2; break;
             default: slots += 1;
         }
     }
@@ -576,6 +587,20 @@ uint32_t colprog_regs(const MProg& mp) {
     return (acc_off + std::max<uint32_t>(mp.n_agpr, 1) + 7) & ~7u;
 }
 
+// SGPR map of the emitted kernel beyond the prologue's s0..s55: s56..s63 scratch soffset bases,
+// s64..s79 / s80..s95 the two halves of the double-buffered source row-offset window.
+constexpr uint32_t SCR_BASES = 8;
+constexpr uint32_t ROW_WIN = 64;
+
+std::vector<uint32_t> colprog_src_rows(const MProg& mp) {
+    static const uint32_t diag = diag_mask();
+    std::vector<uint32_t> rows;
+    if (diag & 4) return rows;
+    for (const MInst& m : mp.ins)
+        if (m.op == MI_LDSRC) rows.push_back((diag & 16) ? (uint32_t)(rows.size() % mp.K) : m.imm);
+    return rows;
+}
+
 std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
     static const Policy pol;
     static const uint32_t diag = diag_mask();
@@ -603,7 +628,7 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
     const char* pro_once[] = {
         "s_load_dwordx8 s[4:11], s[0:1], 0x0",
         "s_load_dwordx8 s[12:19], s[0:1], 0x20",
-        "s_load_dwordx2 s[48:49], s[0:1], 0x40",
+        "s_load_dwordx4 s[48:51], s[0:1], 0x40",
         "s_waitcnt lgkmcnt(0)",
         "v_lshlrev_b32_e32 V_SCROFF, 2, v0",
         "v_add_u32_e32 V_LDS2, 0x10000, V_SCROFF",
@@ -669,11 +694,36 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
         line(l.c_str());
     };
     for (const char* p : pro_once) put(p);
+    // Scratch slot s sits at soffset 4096 * (s / 16) + offset (s % 16) * 256: soffset 0 or one of
+    // SCR_BASES SGPRs s56.. loaded once, so a spill or reload carries no SALU; slots beyond them
+    // (very large K) form their soffset with an s_mov.
+    const uint32_t n_bases = std::min<uint32_t>(SCR_BASES, mp.n_slots > 16 ? (mp.n_slots - 1) / 16 : 0);
+    for (uint32_t j = 0; j < n_bases; ++j) {
+        std::snprintf(buf, sizeof buf, "s_mov_b32 s%u, %u", 56 + j, 4096u * (j + 1));
+        line(buf);
+    }
     s += ".Lloop:\n";
     for (const char* p : pro_iter) put(p);
+    // Source row j of the program (in issue order) is read at soffset row_off[j] = row * T, a
+    // host-built table (colprog_src_rows) streamed into SGPRs 16 entries at a time by s_load_dwordx16,
+    // one group ahead: a source load carries no SALU of its own, only one s_load and one
+    // lgkmcnt(0) per 16 loads.  (LDS waits counted by the allocator only get stricter from the
+    // extra outstanding scalar load.)
+    const std::vector<uint32_t> src_rows = colprog_src_rows(mp);
+    const uint32_t n_groups = (uint32_t)((src_rows.size() + 15) / 16);
+    if (n_groups) line("s_load_dwordx16 s[64:79], s[50:51], 0x0");
+    uint32_t src_j = 0;
     int sr = 0;
-    uint32_t src_seq = 0;
     auto srot = [&]() { sr = (sr + 1) & 7; return 40 + sr; };
+    auto scr_soff = [&](uint32_t slot) -> std::string {
+        const uint32_t j = slot / 16;
+        if (j == 0) return "0";
+        if (j <= n_bases) return "s" + std::to_string(56 + j - 1);
+        const int q = srot();
+        std::snprintf(buf, sizeof buf, "s_mov_b32 s%d, %u", q, 4096u * j);
+        line(buf);
+        return "s" + std::to_string(q);
+    };
     for (const MInst& m : mp.ins) {
         switch (m.op) {
             case MI_XOR2:
@@ -682,28 +732,39 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
                 std::snprintf(buf, sizeof buf, "v_bitop3_b32 v%d, v%d, v%d, v%d bitop3:0x96", m.d, m.a, m.b, m.c); line(buf); break;
             case MI_XT:
             case MI_XTX:
+                // alpha*a (+ b) per byte in 5 VALU: m = 0xff where a byte's top bit is set (v_perm sign
+                // select over {a << 8, a}); z = (m & 0x1d..) [^ b]; result = ((a << 1) & 0xfe..) ^ z.
+                // bitop3 0x6c = (S0 & S2) ^ S1, symmetric in S0/S2 so operand order cannot flip it.
                 std::snprintf(buf, sizeof buf, "v_lshlrev_b32_e32 v%d, 8, v%d", V_T1, m.a); line(buf);
                 std::snprintf(buf, sizeof buf, "v_perm_b32 v%d, v%d, v%d, s36", V_T1, V_T1, m.a); line(buf);
-                std::snprintf(buf, sizeof buf, "v_and_b32_e32 v%d, s38, v%d", V_T1, V_T1); line(buf);
-                std::snprintf(buf, sizeof buf, "v_lshlrev_b32_e32 v%d, 1, v%d", V_T2, m.a); line(buf);
-                std::snprintf(buf, sizeof buf, "v_and_b32_e32 v%d, s37, v%d", V_T2, V_T2); line(buf);
-                if (m.op == MI_XT) std::snprintf(buf, sizeof buf, "v_xor_b32_e32 v%d, v%d, v%d", m.d, V_T1, V_T2);
-                else std::snprintf(buf, sizeof buf, "v_bitop3_b32 v%d, v%d, v%d, v%d bitop3:0x96", m.d, V_T1, V_T2, m.b);
+                if (m.op == MI_XT) std::snprintf(buf, sizeof buf, "v_and_b32_e32 v%d, s38, v%d", V_T1, V_T1);
+                else std::snprintf(buf, sizeof buf, "v_bitop3_b32 v%d, v%d, v%d, s38 bitop3:0x6c", V_T1, V_T1, m.b);
                 line(buf);
+                std::snprintf(buf, sizeof buf, "v_lshlrev_b32_e32 v%d, 1, v%d", V_T2, m.a); line(buf);
+                std::snprintf(buf, sizeof buf, "v_bitop3_b32 v%d, v%d, v%d, s37 bitop3:0x6c", m.d, V_T2, V_T1); line(buf);
                 break;
             case MI_ZERO:
                 std::snprintf(buf, sizeof buf, "v_mov_b32_e32 v%d, 0", m.d); line(buf); break;
             case MI_LDSRC: {
-                const uint32_t row = (diag & 16) ? (src_seq++ % mp.K) : m.imm;
                 if (diag & 4) {
                     std::snprintf(buf, sizeof buf, is_agpr(m.d) ? "v_accvgpr_write_b32 %s, v%d" : "v_mov_b32_e32 %s, v%d",
                                   R(m.d), V_SRCOFF);
                     line(buf);
                     break;
                 }
-                const int q = srot();
-                std::snprintf(buf, sizeof buf, "s_mul_i32 s%d, s12, %u", q, row); line(buf);
-                std::snprintf(buf, sizeof buf, "buffer_load_dword %s, v%d, s[24:27], s%d offen%s", R(m.d), V_SRCOFF, q, pol.src.c_str()); line(buf);
+                const uint32_t g = src_j / 16, i = src_j % 16, win = ROW_WIN + 16 * (g & 1);
+                if (i == 0) {
+                    line("s_waitcnt lgkmcnt(0)");
+                    if (g + 1 < n_groups) {
+                        std::snprintf(buf, sizeof buf, "s_load_dwordx16 s[%u:%u], s[50:51], 0x%x", ROW_WIN + 16 * ((g + 1) & 1),
+                                      ROW_WIN + 16 * ((g + 1) & 1) + 15, (g + 1) * 64);
+                        line(buf);
+                    }
+                }
+                ++src_j;
+                std::snprintf(buf, sizeof buf, "buffer_load_dword %s, v%d, s[24:27], s%u offen%s", R(m.d), V_SRCOFF, win + i,
+                              pol.src.c_str());
+                line(buf);
                 break;
             }
             case MI_DMA: {
@@ -725,16 +786,18 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
             }
             case MI_SPST: {
                 if (diag & 1) break;
-                const int q = srot();
-                std::snprintf(buf, sizeof buf, "s_mov_b32 s%d, %u", q, m.imm * 256u); line(buf);
-                std::snprintf(buf, sizeof buf, "buffer_store_dword %s, v%d, s[32:35], s%d offen%s", R(m.a), V_SCROFF, q, pol.scr_st.c_str()); line(buf);
+                const std::string so = scr_soff(m.imm);
+                std::snprintf(buf, sizeof buf, "buffer_store_dword %s, v%d, s[32:35], %s offen offset:%u%s", R(m.a), V_SCROFF,
+                              so.c_str(), (m.imm & 15u) * 256u, pol.scr_st.c_str());
+                line(buf);
                 break;
             }
             case MI_SPLD: {
                 if (diag & 1) break;
-                const int q = srot();
-                std::snprintf(buf, sizeof buf, "s_mov_b32 s%d, %u", q, m.imm * 256u); line(buf);
-                std::snprintf(buf, sizeof buf, "buffer_load_dword %s, v%d, s[32:35], s%d offen%s", R(m.d), V_SCROFF, q, pol.scr_ld.c_str()); line(buf);
+                const std::string so = scr_soff(m.imm);
+                std::snprintf(buf, sizeof buf, "buffer_load_dword %s, v%d, s[32:35], %s offen offset:%u%s", R(m.d), V_SCROFF,
+                              so.c_str(), (m.imm & 15u) * 256u, pol.scr_ld.c_str());
+                line(buf);
                 break;
             }
             case MI_ACCW:
@@ -777,14 +840,14 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
     s += "\t\t.amdhsa_kernarg_size 80\n\t\t.amdhsa_user_sgpr_count 2\n";
     s += "\t\t.amdhsa_user_sgpr_kernarg_segment_ptr 1\n\t\t.amdhsa_system_sgpr_workgroup_id_x 1\n";
     s += "\t\t.amdhsa_system_vgpr_workitem_id 0\n\t\t.amdhsa_next_free_vgpr " + std::to_string(n_regs) + "\n";
-    s += "\t\t.amdhsa_next_free_sgpr 56\n\t\t.amdhsa_accum_offset " + std::to_string(acc_off) +
+    s += "\t\t.amdhsa_next_free_sgpr " + std::to_string(ROW_WIN + 32) + "\n\t\t.amdhsa_accum_offset " + std::to_string(acc_off) +
          "\n\t\t.amdhsa_reserve_vcc 0\n";
     s += "\t\t.amdhsa_ieee_mode 0\n\t\t.amdhsa_dx10_clamp 0\n\t.end_amdhsa_kernel\n\t.text\n";
     s += "\t.amdgpu_metadata\n---\namdhsa.kernels:\n  - .agpr_count: " + std::to_string(n_regs - acc_off) + "\n    .args:\n";
     s += "      - .offset: 0\n        .size: 80\n        .value_kind: by_value\n";
     s += "    .group_segment_fixed_size: " + lds + "\n    .kernarg_segment_align: 8\n    .kernarg_segment_size: 80\n";
     s += "    .max_flat_workgroup_size: 64\n    .name: " + kname + "\n    .private_segment_fixed_size: 0\n";
-    s += "    .sgpr_count: 56\n    .symbol: " + kname + ".kd\n    .vgpr_count: " + std::to_string(n_regs) +
+    s += "    .sgpr_count: " + std::to_string(ROW_WIN + 32) + "\n    .symbol: " + kname + ".kd\n    .vgpr_count: " + std::to_string(n_regs) +
          "\n    .wavefront_size: 64\n";
     s += "amdhsa.target: amdgcn-amd-amdhsa--gfx950\namdhsa.version:\n  - 1\n  - 2\n...\n\t.end_amdgpu_metadata\n";
     return s;

@@ -60,6 +60,8 @@ struct AllocOpts {
     uint32_t la_dma = 0;         // look-ahead (IR nodes) for LDS-DMA source staging (0 = off)
     uint32_t src_bias = 100;     // victim choice: a source row's next use counts this % as far
     uint32_t src_lds = 1;        // evicted source rows may take LDS slots (else dropped at once)
+    uint32_t wait_age = 320;     // a vmcnt wait also covers operations issued this many instructions ago
+    uint32_t lwait_age = 48;     // the same for lgkmcnt (LDS) waits
 };
 
 struct MProg {
@@ -107,11 +109,14 @@ struct ColKernArgs {
     uint32_t pad;
     uint32_t n_items;     // 64-column items (waves' worth of work) in this launch
     uint32_t n_wg;        // persistent grid size: wave w takes items w, w + n_wg, ...
-    uint32_t pad2[2];
+    uint64_t row_off;     // uint32 table: soffset of the program's j-th source load (colprog_src_rows[j] * T)
 };
 static_assert(sizeof(ColKernArgs) == 80, "kernarg layout");
 
 std::string emit_colprog_asm(const MProg& mp, const std::string& kname);
+// Source rows of the program's buffer loads in issue order (the kernel's row_off table is these
+// times T, padded to a multiple of 16 entries).
+std::vector<uint32_t> colprog_src_rows(const MProg& mp);
 // Registers (VGPR + AGPR, allocation granule 8) per lane of the emitted kernel.
 uint32_t colprog_regs(const MProg& mp);
 

@@ -83,6 +83,8 @@ struct ColKernel {
     uint64_t last_use = 0;         // LRU clock of the per-device cache
     DevBuf mrep;                   // decode: outputs on the identity payload
     uint32_t mrep_stride = 0;
+    std::vector<uint32_t> src_rows;                 // source row of each buffer load, in issue order
+    std::map<uint32_t, std::unique_ptr<DevBuf>> row_off;  // T -> src_rows * T (the kernel's soffsets)
     ~ColKernel() { if (mod) (void)hipModuleUnload(mod); }
 };
 
@@ -218,6 +220,7 @@ const AllocOpts& alloc_options() {
         if (const char* h = knob("RQHIP_LA_DMA")) r.la_dma = (uint32_t)std::atoi(h);
         if (const char* h = knob("RQHIP_SRC_BIAS")) r.src_bias = (uint32_t)std::atoi(h);
         if (const char* h = knob("RQHIP_SRC_LDS")) r.src_lds = (uint32_t)std::atoi(h);
+        if (const char* h = knob("RQHIP_WAIT_AGE")) std::sscanf(h, "%u,%u", &r.wait_age, &r.lwait_age);
         return r;
     }();
     return o;
@@ -269,33 +272,39 @@ uint64_t library_hash() {
 
 struct CacheHdr {
     char magic[8];
-    uint32_t n_out, n_slots, n_ins, waves_per_cu, name_len, pad;
+    uint32_t n_out, n_slots, n_ins, waves_per_cu, name_len, n_rows;
     uint64_t co_len;
     MProg::Stats st;
 };
+constexpr char CACHE_MAGIC[9] = "RQCO0002";
 
-bool cache_load(const std::string& path, CacheHdr* h, std::string* name, std::vector<char>* co) {
+bool cache_load(const std::string& path, CacheHdr* h, std::string* name, std::vector<char>* co,
+                std::vector<uint32_t>* rows) {
     FILE* f = std::fopen(path.c_str(), "rb");
     if (!f) return false;
-    bool ok = std::fread(h, sizeof *h, 1, f) == 1 && std::memcmp(h->magic, "RQCO0001", 8) == 0 && h->name_len < 256 &&
-              h->co_len < (1ull << 30);
+    bool ok = std::fread(h, sizeof *h, 1, f) == 1 && std::memcmp(h->magic, CACHE_MAGIC, 8) == 0 && h->name_len < 256 &&
+              h->co_len < (1ull << 30) && h->n_rows < (1u << 24);
     if (ok) {
         name->resize(h->name_len);
         co->resize(h->co_len);
+        rows->resize(h->n_rows);
         ok = std::fread(&(*name)[0], 1, h->name_len, f) == h->name_len &&
-             std::fread(co->data(), 1, h->co_len, f) == h->co_len;
+             std::fread(co->data(), 1, h->co_len, f) == h->co_len &&
+             std::fread(rows->data(), 4, h->n_rows, f) == h->n_rows;
     }
     std::fclose(f);
     return ok;
 }
 
-void cache_store(const std::string& path, const CacheHdr& h, const std::string& name, const std::vector<char>& co) {
+void cache_store(const std::string& path, const CacheHdr& h, const std::string& name, const std::vector<char>& co,
+                 const std::vector<uint32_t>& rows) {
     ::mkdir(cache_dir().c_str(), 0755);
     const std::string tmp = path + ".tmp" + std::to_string(::getpid());
     FILE* f = std::fopen(tmp.c_str(), "wb");
     if (!f) return;
     const bool ok = std::fwrite(&h, sizeof h, 1, f) == 1 && std::fwrite(name.data(), 1, name.size(), f) == name.size() &&
-                    std::fwrite(co.data(), 1, co.size(), f) == co.size();
+                    std::fwrite(co.data(), 1, co.size(), f) == co.size() &&
+                    std::fwrite(rows.data(), 4, rows.size(), f) == rows.size();
     std::fclose(f);
     if (ok) std::rename(tmp.c_str(), path.c_str());
     else std::remove(tmp.c_str());
@@ -337,7 +346,7 @@ int get_col_kernel(DevCtx* ctx, const Params& p, const uint32_t* esi, uint32_t n
         CacheHdr ch;
         std::string kname;
         std::vector<char> co;
-        if (path.empty() || !cache_load(path, &ch, &kname, &co)) {
+        if (path.empty() || !cache_load(path, &ch, &kname, &co, &k->src_rows)) {
             ColIR ir;
             std::string err;
             MProg mp;
@@ -350,7 +359,9 @@ int get_col_kernel(DevCtx* ctx, const Params& p, const uint32_t* esi, uint32_t n
             co.clear();
             if (!comgr_assemble(emit_colprog_asm(mp, kname), &co, &err)) { ctx->colk.erase(key); return fail(RQ_ERR_PLAN, err); }
             std::memset(&ch, 0, sizeof ch);
-            std::memcpy(ch.magic, "RQCO0001", 8);
+            std::memcpy(ch.magic, CACHE_MAGIC, 8);
+            k->src_rows = colprog_src_rows(mp);
+            ch.n_rows = (uint32_t)k->src_rows.size();
             ch.n_out = ir.n_out;
             ch.n_slots = mp.n_slots;
             ch.n_ins = (uint32_t)mp.ins.size();
@@ -361,7 +372,7 @@ int get_col_kernel(DevCtx* ctx, const Params& p, const uint32_t* esi, uint32_t n
             ch.name_len = (uint32_t)kname.size();
             ch.co_len = co.size();
             ch.st = mp.st;
-            if (!path.empty()) cache_store(path, ch, kname, co);
+            if (!path.empty()) cache_store(path, ch, kname, co, k->src_rows);
         }
         if (hipModuleLoadData(&k->mod, co.data()) != hipSuccess ||
             hipModuleGetFunction(&k->fn, k->mod, kname.c_str()) != hipSuccess) {
@@ -410,6 +421,18 @@ int launch_col(DevCtx* ctx, ColKernel* k, uint32_t T, uint32_t n_blocks, const v
     int rc;
     Workspace* w = ctx->wsp(stream);
     if ((rc = w->scratch.ensure(spw * max_wg))) return rc;
+    auto& tab = k->row_off[T];
+    if (!tab) {  // once per (program, T): the source loads' soffsets, padded to whole 16-entry groups
+        std::unique_ptr<DevBuf> b(new DevBuf());
+        std::vector<uint32_t> off((k->src_rows.size() + 15) / 16 * 16 + 16, 0);
+        for (size_t j = 0; j < k->src_rows.size(); ++j) off[j] = k->src_rows[j] * T;
+        if ((rc = b->ensure(off.size() * 4))) { k->row_off.erase(T); return rc; }
+        if (hipMemcpy(b->p, off.data(), off.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+            k->row_off.erase(T);
+            return fail(RQ_ERR_DEVICE, "row-offset table upload failed");
+        }
+        tab = std::move(b);
+    }
     for (uint32_t b0 = 0; b0 < n_blocks; b0 += per) {
         const uint32_t nb = std::min(per, n_blocks - b0);
         ColKernArgs a;
@@ -422,6 +445,7 @@ int launch_col(DevCtx* ctx, ColKernel* k, uint32_t T, uint32_t n_blocks, const v
         a.T = T;
         a.n_cols = nb * Td;
         a.scr_per_wave = (uint32_t)spw;
+        a.row_off = (uint64_t)(uintptr_t)tab->p;
         if (!divmagic(Td, a.n_cols, &a.magic, &a.shift)) return fail(RQ_ERR_UNSUPPORTED, "no division magic");
         size_t sz = sizeof a;
         void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};

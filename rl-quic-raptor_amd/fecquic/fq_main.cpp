@@ -172,7 +172,12 @@ int loopback(int argc, char** argv) {
             while (::send(udp_tx, b, n, 0) < 0 && errno == ENOBUFS) std::this_thread::yield();
         }, &ts);
     } else {
-        rc = send_file(file, to, [&](const uint8_t* b, size_t n) { deliver(rx, rh, b, n); }, &ts);
+        // in-process datagrams with flow control: a full ingest ring makes the sender wait (as a
+        // blocking socket would), so the only loss is the sender's --drop
+        rc = send_file(file, to, [&](const uint8_t* b, size_t n) {
+            while (rx.ring_full()) std::this_thread::sleep_for(std::chrono::microseconds(50));
+            deliver(rx, rh, b, n);
+        }, &ts);
     }
     // wait until the file is complete (transfer.go:349-359) or the timeout
     while (rc == 0 && rx.written() < rh.file_size &&

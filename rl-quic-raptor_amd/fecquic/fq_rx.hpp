@@ -68,6 +68,7 @@ public:
     int close_and_finalize(const uint8_t sha[32], std::string* final_path);
     uint64_t written() const { return written_.load(); }
     uint64_t in_use() const { return (uint64_t)in_use_.load(); }
+    bool ring_full() const { return ring_.full(); }
     RxStats stats;
     const std::string& last_error() const { return err_; }
 
@@ -81,6 +82,10 @@ public:
         bool try_push(const Item& x);
         uint32_t try_pop_batch(Item* dst, uint32_t max);
         uint32_t capacity() const { return (uint32_t)slots.size(); }
+        bool full() const {  // the next push would fail (its slot still holds an unconsumed item)
+            const uint64_t pos = tail.load(std::memory_order_relaxed);
+            return (int64_t)slots[pos & mask].seq.load(std::memory_order_acquire) - (int64_t)pos < 0;
+        }
         struct Slot {
             std::atomic<uint64_t> seq;
             Item v;
