@@ -576,7 +576,8 @@ struct Policy {
 
 // Diagnostic builds (wrong bytes, timing only): RQHIP_DIAG bit 1 drops global scratch traffic,
 // 2 drops LDS spill traffic, 4 replaces source loads by register writes, 8 drops output stores,
-// 16 loads source rows in increasing row order (wrong rows; measures the cost of the random order).
+// 16 loads source rows in increasing row order (wrong rows; measures the cost of the random order),
+// 32 drops the XOR / xtime instructions (memory traffic and register moves only).
 static uint32_t diag_mask() {
     const char* e = knob("RQHIP_DIAG");
     return e ? (uint32_t)std::atoi(e) : 0u;
@@ -725,6 +726,7 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
         return "s" + std::to_string(q);
     };
     for (const MInst& m : mp.ins) {
+        if ((diag & 32) && m.op <= MI_ZERO) continue;  // memory-only timing: no XOR / xtime work
         switch (m.op) {
             case MI_XOR2:
                 std::snprintf(buf, sizeof buf, "v_xor_b32_e32 v%d, v%d, v%d", m.d, m.a, m.b); line(buf); break;

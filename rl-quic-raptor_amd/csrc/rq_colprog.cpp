@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <queue>
 
 namespace rq {
 
@@ -101,8 +102,28 @@ bool eliminate(const Params& p, Elim* e, std::string* err) {
             bucket[std::min<uint32_t>(cnt[r], 63)].push_back(r);
         }
     };
+    // degree-1 rows by smallest column (peel_mode 1): peeling then runs roughly in column order
+    static const int peel_mode = [] { const char* m = knob("RQHIP_PEEL"); return m ? std::atoi(m) : 0; }();
+    std::priority_queue<std::pair<uint32_t, uint32_t>, std::vector<std::pair<uint32_t, uint32_t>>,
+                        std::greater<std::pair<uint32_t, uint32_t>>> deg1;
+    auto active_col = [&](uint32_t r) -> uint32_t {
+        for (uint32_t c : rows[r]) if (cstate[c] == ACTIVE) return c;
+        return UINT32_MAX;
+    };
     for (;;) {
         int32_t r = -1;
+        if (peel_mode == 1) {
+            auto& bk = bucket[1];
+            while (bhead[1] < bk.size()) {  // move new degree-1 rows into the column-ordered heap
+                const uint32_t x = bk[bhead[1]++];
+                if (!rdone[x] && cnt[x] == 1) deg1.push({active_col(x), x});
+            }
+            while (!deg1.empty() && r < 0) {
+                const auto top = deg1.top();
+                deg1.pop();
+                if (!rdone[top.second] && cnt[top.second] == 1 && cstate[top.first] == ACTIVE) r = (int32_t)top.second;
+            }
+        }
         for (uint32_t b = 1; b < 64 && r < 0; ++b) {
             auto& bk = bucket[b];
             while (bhead[b] < bk.size()) {
@@ -360,6 +381,11 @@ struct OutDesc {
 // linear, so the P chains' pushes and end values add up to the single scan's).  A y value then lives
 // only until its pass instead of until its column comes up in one global scan, which bounds the live
 // set by about npiv / P plus the open accumulators, at 2 ops per column per extra pass.
+static bool interleave_passes() {
+    static const bool on = [] { const char* m = knob("RQHIP_WEAVE"); return m && m[0] == '1'; }();
+    return on;
+}
+
 bool build(const Params& p, const std::vector<OutDesc>& outs, uint32_t passes, ColIR* ir, std::string* err) {
     Elim e;
     if (!eliminate(p, &e, err)) return false;
@@ -451,25 +477,32 @@ bool build(const Params& p, const std::vector<OutDesc>& outs, uint32_t passes, C
             for (uint32_t j : e.deps[k]) dependents[j].push_back(k);
         std::vector<Acc> yacc(npiv);
         std::vector<uint32_t> tends;
-        uint32_t done = 0;  // y_0 .. y_(done-1) consumed by earlier passes
-        auto pass = [&](uint32_t upto) {
-            uint32_t tp = NOVAL;
-            for (uint32_t j = 0; j < KS; ++j) {
+        // Horner pass over the y values of peeling positions [lo, hi), advanced a few columns at a
+        // time: with `interleave`, pass q runs woven into the production of group q + 1 (whose
+        // source loads then overlap its VALU work) instead of after it
+        struct PassGen { uint32_t lo = 0, hi = 0, j = 0, tp = NOVAL; bool on = false; } pg;
+        auto advance = [&](uint32_t ncols) {
+            for (uint32_t c = 0; c < ncols && pg.on; ++c, ++pg.j) {
+                if (pg.j == KS) {
+                    if (pg.tp != NOVAL) tends.push_back(pg.tp);
+                    pg.on = false;
+                    break;
+                }
+                const uint32_t j = pg.j;
                 uint32_t yj = NOVAL;
                 if (e.cstate[j] == 1) {
                     const uint32_t k = (uint32_t)e.col_order[j];
-                    if (k >= done && k < upto) yj = y[k];
+                    if (k >= pg.lo && k < pg.hi) yj = y[k];
                 }
-                tp = B.xt(tp, yj);
-                if (j + 1 < KS && tp != NOVAL) {
-                    part[e.ma[j]].push(B, tp);
-                    part[e.mb[j]].push(B, tp);
+                pg.tp = B.xt(pg.tp, yj);
+                if (j + 1 < KS && pg.tp != NOVAL) {
+                    part[e.ma[j]].push(B, pg.tp);
+                    part[e.mb[j]].push(B, pg.tp);
                 }
             }
-            if (tp != NOVAL) tends.push_back(tp);
-            done = upto;
         };
-        uint32_t q = 1;
+        const bool weave = interleave_passes();
+        uint32_t q = 1, lo = 0, credit = 0;
         for (uint32_t k = 0; k < npiv; ++k) {
             std::vector<uint32_t> tt{D(e.piv_row[k]), yacc[k].get(B)};
             y[k] = B.xsum(tt);
@@ -478,12 +511,21 @@ bool build(const Params& p, const std::vector<OutDesc>& outs, uint32_t passes, C
             const uint32_t c = e.piv_col[k];
             for (uint32_t i : col_rem[c]) b2acc[i].push(B, y[k]);
             for (uint32_t o : col_outs[c]) oacc[o].push(B, y[k]);
+            if (pg.on) {  // KS columns of the running pass spread over this group's productions
+                credit += KS * passes;
+                advance(credit / npiv);
+                credit %= npiv;
+            }
             if (k + 1 == (uint64_t)npiv * q / passes) {
-                pass(k + 1);
+                advance(KS + 1);  // finish the previous pass
+                pg = PassGen{lo, k + 1, 0, NOVAL, true};
+                lo = k + 1;
+                credit = 0;
+                if (!weave) advance(KS + 1);
                 ++q;
             }
         }
-        if (done < npiv) pass(npiv);
+        advance(KS + 1);
         t = B.xsum(tends);
     }
     for (uint32_t j = 0; j < KS && !passes; ++j) {

@@ -165,9 +165,9 @@ __device__ __forceinline__ void gf_tables_copy(uint8_t* ex, uint8_t* lg) {
 // sees all rows and picks the same one), scales it by the inverse and stores its eight alpha^b
 // multiples (one byte per thread, exp/log tables), and every other row XORs in the multiples its own
 // coefficient's bits select (one v_bitop3 per bit and dword).
-template <int RPL>
-__global__ void __launch_bounds__(256) k_solve_fast(SolveArgs a) {
-    constexpr uint32_t NW = 4, NT = 64 * NW;
+template <int RPL, int NW>
+__global__ void __launch_bounds__(64 * NW) k_solve_fast(SolveArgs a) {
+    constexpr uint32_t NT = 64 * NW;
     constexpr uint32_t NROWS = 64 * RPL, WQ = 8 * RPL, SW = 32 * RPL + 4;  // quads per row, row stride
     __shared__ __attribute__((aligned(16))) uint32_t rows[NROWS * SW];
     __shared__ __attribute__((aligned(16))) uint4 mult[8][WQ];  // alpha^b * scaled pivot row
@@ -367,11 +367,25 @@ size_t solve_ws_bytes(uint32_t e) {
     return W2 + ((e + 15) & ~15u) + 4 * ((e + 7) & ~7u) + (size_t)e * W2;
 }
 
+// Waves per block of the e <= 64 solver (RQHIP_SOLVE_NW in experiments builds).
+static int solve_nw() {
+#ifdef RQHIP_EXPERIMENTS
+    static const int nw = [] {
+        const char* e = std::getenv("RQHIP_SOLVE_NW");
+        return e ? std::atoi(e) : 4;
+    }();
+    return nw;
+#else
+    return 4;
+#endif
+}
+
 int launch_solve(const SolveArgs& a, uint32_t n_blocks, bool need_general, uint32_t max_lds_e, void* stream) {
-    hipLaunchKernelGGL(k_solve_fast<1>, dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a);
+    if (solve_nw() == 1) hipLaunchKernelGGL((k_solve_fast<1, 1>), dim3(n_blocks), dim3(64), 0, (hipStream_t)stream, a);
+    else hipLaunchKernelGGL((k_solve_fast<1, 4>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !need_general) return (int)e;
-    hipLaunchKernelGGL(k_solve_fast<2>, dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL((k_solve_fast<2, 4>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a);
     if ((e = hipGetLastError()) != hipSuccess) return (int)e;
     static bool attr = false;
     if (!attr) {

@@ -21,7 +21,8 @@ from dataclasses import dataclass
 from pathlib import Path
 
 _HERE = Path(__file__).resolve().parent
-LIB_PATH = _HERE / "build" / "librqhip.so"
+# RQHIP_LIB names an alternative build of the same library (tools/build_experiments.sh) for tuning runs
+LIB_PATH = Path(os.environ["RQHIP_LIB"]).resolve() if os.environ.get("RQHIP_LIB") else _HERE / "build" / "librqhip.so"
 _lib = None
 
 RQ_OK = 0
