@@ -179,6 +179,15 @@ uint32_t rq_debug_decode_margin(uint32_t margin);
  * chooses like the engine (cost model over the schedules), 0 = one demand-driven column scan,
  * P >= 1 = peeling-order production with P Horner passes.  Returns the previous setting. */
 int rq_debug_colprog_passes(int passes);
+/* How the host-memory batch calls split n_blocks over the devices of device_mask (0 = the calling
+ * thread's device, reported as device 0 here) when n_devices exist: returns the shard count (<= cap
+ * entries written: device, first block, end block) or a negative error (a mask bit beyond n_devices:
+ * RQ_ERR_BAD_ARG).  virtual_shards > 1 splits a one-device mask over that many host threads. */
+int rq_debug_shard_plan(uint32_t device_mask, int n_devices, uint32_t n_blocks, uint32_t virtual_shards, int* dev,
+                        uint32_t* b0, uint32_t* b1, uint32_t cap);
+/* Sets the virtual shard count the host-memory batch calls use on a one-device mask (tests drive the
+ * per-device host threads on one GPU with it); returns the previous value (default 0 = off). */
+uint32_t rq_debug_virtual_shards(uint32_t n);
 
 #ifdef __cplusplus
 }

@@ -112,16 +112,18 @@ bool eliminate(const Params& p, Elim* e, std::string* err) {
     };
     for (;;) {
         int32_t r = -1;
-        if (peel_mode == 1) {
+        if (peel_mode) {
             auto& bk = bucket[1];
-            while (bhead[1] < bk.size()) {  // move new degree-1 rows into the column-ordered heap
+            while (bhead[1] < bk.size()) {  // move new degree-1 rows into the column / row ordered heap
                 const uint32_t x = bk[bhead[1]++];
-                if (!rdone[x] && cnt[x] == 1) deg1.push({active_col(x), x});
+                if (!rdone[x] && cnt[x] == 1) deg1.push({peel_mode == 1 ? active_col(x) : x, x});
             }
             while (!deg1.empty() && r < 0) {
                 const auto top = deg1.top();
                 deg1.pop();
-                if (!rdone[top.second] && cnt[top.second] == 1 && cstate[top.first] == ACTIVE) r = (int32_t)top.second;
+                if (!rdone[top.second] && cnt[top.second] == 1 &&
+                    (peel_mode != 1 || cstate[top.first] == ACTIVE))
+                    r = (int32_t)top.second;
             }
         }
         for (uint32_t b = 1; b < 64 && r < 0; ++b) {

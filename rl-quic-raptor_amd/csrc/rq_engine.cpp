@@ -923,33 +923,55 @@ int decode_host_shard(int dev, const HostDecode& d, const Params& p, uint32_t b0
 }
 
 // Split [0, n_blocks) contiguously over the devices of device_mask (0: the calling thread's
-// device) and run `shard(dev, b0, b1)` on one host thread per device.
-template <class F>
-int run_sharded(uint32_t device_mask, uint32_t n_blocks, F shard) {
+// device): shard i = devs[i], blocks [b0_i, b1_i).  `virt` > 1 (rq_debug_virtual_shards, tests) splits
+// over that many host threads on the one device of a 0 / single-bit mask.
+struct ShardPlan {
+    std::vector<int> dev;
+    std::vector<uint32_t> b0, b1;
+};
+uint32_t g_virtual_shards = 0;
+
+int plan_shards(uint32_t device_mask, int n_dev, int cur_dev, uint32_t n_blocks, uint32_t virt, ShardPlan* sp) {
     std::vector<int> devs;
     if (device_mask == 0) {
-        int dev;
-        int rc = current_device(&dev);
-        if (rc) return rc;
-        devs.push_back(dev);
+        devs.push_back(cur_dev);
     } else {
-        int n = 0;
-        if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(RQ_ERR_DEVICE, "no HIP device available");
         for (int i = 0; i < 32; ++i)
             if (device_mask >> i & 1u) {
-                if (i >= n) return fail(RQ_ERR_BAD_ARG, "device_mask names a device that does not exist");
+                if (i >= n_dev) return fail(RQ_ERR_BAD_ARG, "device_mask names a device that does not exist");
                 devs.push_back(i);
             }
     }
-    const uint32_t nd = std::min<uint32_t>((uint32_t)devs.size(), n_blocks);
-    if (nd <= 1) return shard(devs[0], 0u, n_blocks);
+    if (virt > 1 && devs.size() == 1) devs.assign(virt, devs[0]);
+    const uint32_t nd = std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)devs.size(), n_blocks));
+    *sp = ShardPlan();
+    for (uint32_t i = 0; i < nd; ++i) {
+        sp->dev.push_back(devs[i]);
+        sp->b0.push_back((uint32_t)((uint64_t)n_blocks * i / nd));
+        sp->b1.push_back((uint32_t)((uint64_t)n_blocks * (i + 1) / nd));
+    }
+    return RQ_OK;
+}
+
+// Run `shard(dev, b0, b1)` for every shard of the plan, one host thread per shard.
+template <class F>
+int run_sharded(uint32_t device_mask, uint32_t n_blocks, F shard) {
+    int n = 0, cur = 0, rc;
+    if (device_mask == 0) {
+        if ((rc = current_device(&cur))) return rc;
+    } else if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        return fail(RQ_ERR_DEVICE, "no HIP device available");
+    }
+    ShardPlan sp;
+    if ((rc = plan_shards(device_mask, n, cur, n_blocks, g_virtual_shards, &sp))) return rc;
+    const uint32_t nd = (uint32_t)sp.dev.size();
+    if (nd == 1) return shard(sp.dev[0], 0u, n_blocks);
     std::vector<int> rcs(nd, RQ_OK);
     std::vector<std::string> errs(nd);
     std::vector<std::thread> th;
     for (uint32_t i = 0; i < nd; ++i) {
-        const uint32_t b0 = (uint32_t)((uint64_t)n_blocks * i / nd), b1 = (uint32_t)((uint64_t)n_blocks * (i + 1) / nd);
-        th.emplace_back([&, i, b0, b1] {
-            rcs[i] = shard(devs[i], b0, b1);
+        th.emplace_back([&, i] {
+            rcs[i] = shard(sp.dev[i], sp.b0[i], sp.b1[i]);
             if (rcs[i]) errs[i] = g_err;
         });
     }
@@ -1109,6 +1131,25 @@ int rq_debug_colprog_assemble(uint32_t K, const uint32_t* esi, uint32_t n_out, s
     if (!comgr_assemble(emit_colprog_asm(mp, "rq_colprog"), &co, &err)) return fail(RQ_ERR_PLAN, err);
     if (code_bytes) *code_bytes = co.size();
     return RQ_OK;
+}
+
+int rq_debug_shard_plan(uint32_t device_mask, int n_devices, uint32_t n_blocks, uint32_t virtual_shards, int* dev,
+                        uint32_t* b0, uint32_t* b1, uint32_t cap) {
+    ShardPlan sp;
+    const int rc = plan_shards(device_mask, n_devices, 0, n_blocks, virtual_shards, &sp);
+    if (rc) return rc;
+    for (uint32_t i = 0; i < sp.dev.size() && i < cap; ++i) {
+        if (dev) dev[i] = sp.dev[i];
+        if (b0) b0[i] = sp.b0[i];
+        if (b1) b1[i] = sp.b1[i];
+    }
+    return (int)sp.dev.size();
+}
+
+uint32_t rq_debug_virtual_shards(uint32_t n) {
+    const uint32_t old = g_virtual_shards;
+    g_virtual_shards = n;
+    return old;
 }
 
 uint32_t rq_debug_decode_margin(uint32_t margin) {

@@ -435,7 +435,7 @@ __device__ __forceinline__ void perm_tables(uint32_t c, uint4* A, uint32_t* B) {
 // load/store instruction is one contiguous 256-B segment).  The slice's tables are built from X
 // straight into LDS (perm_tables: A = the four 8-entry halves (b128), B = the 2-bit table), for
 // MC syndromes m at a time (one chunk whenever e <= MC).
-template <int KC, int CPL>
+template <int KC, int CPL, int PD>
 __global__ void __launch_bounds__(64) k_apply(ApplyArgs a, uint32_t n_units, uint32_t np, uint32_t MC) {
     extern __shared__ __attribute__((aligned(16))) uint32_t xsh[];
     const uint32_t strips = ((a.T >> 2) + 64 * CPL - 1) / (64 * CPL);
@@ -458,8 +458,8 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a, uint32_t n_units, uin
     const uint32_t mc_max = min(MC, e);
     uint4* tA = reinterpret_cast<uint4*>(xsh);                  // [m - c0][KC]
     uint32_t* tB = xsh + (size_t)mc_max * KC * 4;                // [m - c0][KC]
-    uint32_t* offr = tB + (size_t)mc_max * KC;                   // [m - c0], m < c0 + mc + 2
-    uint32_t* off0 = offr + mc_max + 2;
+    uint32_t* offr = tB + (size_t)mc_max * KC;                   // [m - c0], m < c0 + mc + PD
+    uint32_t* off0 = offr + mc_max + PD;
     const uint8_t* xc = a.xcoef + 64ull * a.xoff[bi];
     const uint32_t xs = x_stride(e);
     uint32_t col[CPL];
@@ -475,8 +475,9 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a, uint32_t n_units, uin
     for (int k = 0; k < KC; ++k)
 #pragma unroll
         for (int j = 0; j < CPL; ++j) acc[k][j] = 0;
-    // syndromes are loaded two m ahead (received row and r0 row, XORed on arrival)
-    uint32_t ra[CPL], rb[CPL], na[CPL], nb[CPL];
+    // syndromes are loaded PD m ahead into a ring (received row and r0 row, XORed on use); MC is a
+    // multiple of PD, so ring slot d always holds syndrome m = d (mod PD) across chunks
+    uint32_t ra[PD][CPL], rb[PD][CPL];
     for (uint32_t c0 = 0; c0 < e; c0 += MC) {
         const uint32_t mc = min(MC, e - c0);
         __syncthreads();  // the previous chunk's tables are consumed
@@ -488,7 +489,7 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a, uint32_t n_units, uin
             tA[idx] = A;
             tB[idx] = B;
         }
-        for (uint32_t m = lane; m < mc + 2 && c0 + m < e; m += 64) {
+        for (uint32_t m = lane; m < mc + PD && c0 + m < e; m += 64) {
             const uint32_t j = r0b + XP[c0 + m];
             offr[m] = j * Td;
             off0[m] = a.rep_uidx[j] * Td;
@@ -496,42 +497,46 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a, uint32_t n_units, uin
         __syncthreads();
         if (c0 == 0) {
 #pragma unroll
-            for (int j = 0; j < CPL; ++j) {
-                ra[j] = recv[(size_t)offr[0] + col[j]];
-                rb[j] = r0[(size_t)off0[0] + col[j]];
-                const uint32_t m1 = e > 1 ? 1 : 0;
-                na[j] = recv[(size_t)offr[m1] + col[j]];
-                nb[j] = r0[(size_t)off0[m1] + col[j]];
-            }
-        }
-        for (uint32_t m = 0; m < mc; ++m) {
-            uint32_t s0[CPL], s1[CPL], s2[CPL];
+            for (int d = 0; d < PD; ++d)
+                if ((uint32_t)d < e) {
 #pragma unroll
-            for (int j = 0; j < CPL; ++j) {
-                const uint32_t x = ra[j] ^ rb[j];
-                s0[j] = x & 0x07070707u;
-                s1[j] = (x >> 3) & 0x07070707u;
-                s2[j] = (x >> 6) & 0x03030303u;
-                ra[j] = na[j];
-                rb[j] = nb[j];
-            }
-            if (c0 + m + 2 < e) {
-#pragma unroll
-                for (int j = 0; j < CPL; ++j) {
-                    na[j] = recv[(size_t)offr[m + 2] + col[j]];
-                    nb[j] = r0[(size_t)off0[m + 2] + col[j]];
+                    for (int j = 0; j < CPL; ++j) {
+                        ra[d][j] = recv[(size_t)offr[d] + col[j]];
+                        rb[d][j] = r0[(size_t)off0[d] + col[j]];
+                    }
                 }
-            }
+        }
+        for (uint32_t mb = 0; mb < mc; mb += PD) {
 #pragma unroll
-            for (int k = 0; k < KC; ++k) {
-                const uint4 A = tA[m * KC + k];
-                const uint32_t B = tB[m * KC + k];
+            for (int d = 0; d < PD; ++d) {
+                const uint32_t m = mb + d;
+                if (m >= mc) break;
+                uint32_t s0[CPL], s1[CPL], s2[CPL];
 #pragma unroll
                 for (int j = 0; j < CPL; ++j) {
-                    const uint32_t p0 = __builtin_amdgcn_perm(A.y, A.x, s0[j]);
-                    const uint32_t p1 = __builtin_amdgcn_perm(A.w, A.z, s1[j]);
-                    const uint32_t p2 = __builtin_amdgcn_perm(B, B, s2[j]);
-                    acc[k][j] = xor3(acc[k][j], p0, p1) ^ p2;
+                    const uint32_t x = ra[d][j] ^ rb[d][j];
+                    s0[j] = x & 0x07070707u;
+                    s1[j] = (x >> 3) & 0x07070707u;
+                    s2[j] = (x >> 6) & 0x03030303u;
+                }
+                if (c0 + m + PD < e) {
+#pragma unroll
+                    for (int j = 0; j < CPL; ++j) {
+                        ra[d][j] = recv[(size_t)offr[m + PD] + col[j]];
+                        rb[d][j] = r0[(size_t)off0[m + PD] + col[j]];
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < KC; ++k) {
+                    const uint4 A = tA[m * KC + k];
+                    const uint32_t B = tB[m * KC + k];
+#pragma unroll
+                    for (int j = 0; j < CPL; ++j) {
+                        const uint32_t p0 = __builtin_amdgcn_perm(A.y, A.x, s0[j]);
+                        const uint32_t p1 = __builtin_amdgcn_perm(A.w, A.z, s1[j]);
+                        const uint32_t p2 = __builtin_amdgcn_perm(B, B, s2[j]);
+                        acc[k][j] = xor3(acc[k][j], p0, p1) ^ p2;
+                    }
                 }
             }
         }
@@ -548,19 +553,40 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a, uint32_t n_units, uin
     }
 }
 
-template <int CPL>
+template <int CPL, int PD>
 static void launch_apply_cpl(const ApplyArgs& a, uint32_t kc, dim3 g, size_t lds, hipStream_t st, uint32_t nu,
                              uint32_t np, uint32_t mc) {
     switch (kc) {
-        case 4: hipLaunchKernelGGL((k_apply<4, CPL>), g, dim3(64), lds, st, a, nu, np, mc); break;
-        case 8: hipLaunchKernelGGL((k_apply<8, CPL>), g, dim3(64), lds, st, a, nu, np, mc); break;
-        case 12: hipLaunchKernelGGL((k_apply<12, CPL>), g, dim3(64), lds, st, a, nu, np, mc); break;
-        case 16: hipLaunchKernelGGL((k_apply<16, CPL>), g, dim3(64), lds, st, a, nu, np, mc); break;
-        case 20: hipLaunchKernelGGL((k_apply<20, CPL>), g, dim3(64), lds, st, a, nu, np, mc); break;
-        case 24: hipLaunchKernelGGL((k_apply<24, CPL>), g, dim3(64), lds, st, a, nu, np, mc); break;
-        case 28: hipLaunchKernelGGL((k_apply<28, CPL>), g, dim3(64), lds, st, a, nu, np, mc); break;
-        default: hipLaunchKernelGGL((k_apply<32, CPL>), g, dim3(64), lds, st, a, nu, np, mc); break;
+        case 4: hipLaunchKernelGGL((k_apply<4, CPL, PD>), g, dim3(64), lds, st, a, nu, np, mc); break;
+        case 8: hipLaunchKernelGGL((k_apply<8, CPL, PD>), g, dim3(64), lds, st, a, nu, np, mc); break;
+        case 12: hipLaunchKernelGGL((k_apply<12, CPL, PD>), g, dim3(64), lds, st, a, nu, np, mc); break;
+        case 16: hipLaunchKernelGGL((k_apply<16, CPL, PD>), g, dim3(64), lds, st, a, nu, np, mc); break;
+        case 20: hipLaunchKernelGGL((k_apply<20, CPL, PD>), g, dim3(64), lds, st, a, nu, np, mc); break;
+        case 24: hipLaunchKernelGGL((k_apply<24, CPL, PD>), g, dim3(64), lds, st, a, nu, np, mc); break;
+        case 28: hipLaunchKernelGGL((k_apply<28, CPL, PD>), g, dim3(64), lds, st, a, nu, np, mc); break;
+        default: hipLaunchKernelGGL((k_apply<32, CPL, PD>), g, dim3(64), lds, st, a, nu, np, mc); break;
     }
+}
+
+#ifdef RQHIP_EXPERIMENTS
+// Syndrome prefetch depth of k_apply (RQHIP_APPLY_PD = 2 / 4 / 8 in experiments builds; else 4).
+static int apply_pd() {
+    static const int pd = [] {
+        const char* e = std::getenv("RQHIP_APPLY_PD");
+        return e ? std::atoi(e) : 4;
+    }();
+    return pd;
+}
+#endif
+
+template <int CPL>
+static void launch_apply_pd(const ApplyArgs& a, uint32_t kc, dim3 g, size_t lds, hipStream_t st, uint32_t nu,
+                            uint32_t np, uint32_t mc) {
+#ifdef RQHIP_EXPERIMENTS
+    if (apply_pd() == 2) return launch_apply_cpl<CPL, 2>(a, kc, g, lds, st, nu, np, mc);
+    if (apply_pd() == 8) return launch_apply_cpl<CPL, 8>(a, kc, g, lds, st, nu, np, mc);
+#endif
+    launch_apply_cpl<CPL, 4>(a, kc, g, lds, st, nu, np, mc);
 }
 
 int launch_apply(const ApplyArgs& a, uint32_t /*n_strips*/, uint32_t n_blocks, void* stream) {
@@ -578,21 +604,14 @@ int launch_apply(const ApplyArgs& a, uint32_t /*n_strips*/, uint32_t n_blocks, v
     const uint32_t e = std::max<uint32_t>(a.max_e, 1), ec = std::min(e, MC);
     const uint32_t cap = std::max<uint32_t>(4, std::min<uint32_t>(8, (21504 / (20 * ec)) & ~3u));
     const uint32_t np = (e + cap - 1) / cap, kc = (((e + np - 1) / np) + 3) & ~3u;
-    const size_t lds = (size_t)ec * kc * 20 + (size_t)(ec + 2) * 8;
-    static bool attr = false;
-    if (!attr) {  // slices of large e need more than the default 64 KB
-        for (const void* f : {(const void*)k_apply<32, 1>, (const void*)k_apply<32, 2>, (const void*)k_apply<32, 4>,
-                              (const void*)k_apply<32, 5>, (const void*)k_apply<28, 5>, (const void*)k_apply<28, 4>})
-            (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attr = true;
-    }
+    const size_t lds = (size_t)ec * kc * 20 + (size_t)(ec + 8) * 8;  // tables + row offsets (<= 22 KB)
     const uint32_t nu = (Td + 64 * cpl - 1) / (64 * cpl) * n_blocks;
     const dim3 g((nu + 7) / 8 * 8 * np);
     switch (cpl) {
-        case 1: launch_apply_cpl<1>(a, kc, g, lds, st, nu, np, MC); break;
-        case 2: launch_apply_cpl<2>(a, kc, g, lds, st, nu, np, MC); break;
-        case 4: launch_apply_cpl<4>(a, kc, g, lds, st, nu, np, MC); break;
-        default: launch_apply_cpl<5>(a, kc, g, lds, st, nu, np, MC); break;
+        case 1: launch_apply_pd<1>(a, kc, g, lds, st, nu, np, MC); break;
+        case 2: launch_apply_pd<2>(a, kc, g, lds, st, nu, np, MC); break;
+        case 4: launch_apply_pd<4>(a, kc, g, lds, st, nu, np, MC); break;
+        default: launch_apply_pd<5>(a, kc, g, lds, st, nu, np, MC); break;
     }
     return (int)hipGetLastError();
 }

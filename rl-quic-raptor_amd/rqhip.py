@@ -42,6 +42,7 @@ EXPORTED = (
     "rq_encode_batch", "rq_decode_batch", "rq_decode_batch_async", "rq_encode_batch_host", "rq_decode_batch_host", "rq_device_count", "rq_set_device",
     "rq_debug_colprog_eval", "rq_debug_colprog_emulate", "rq_debug_colprog_assemble", "rq_debug_decode_margin",
     "rq_decode_blocks_host", "rq_host_alloc", "rq_host_free", "rq_debug_colprog_passes",
+    "rq_debug_shard_plan", "rq_debug_virtual_shards",
 )
 
 
@@ -131,6 +132,9 @@ def lib():
             "rq_host_alloc": ([ctypes.c_size_t], vp),
             "rq_host_free": ([vp], None),
             "rq_debug_colprog_passes": ([ctypes.c_int], ctypes.c_int),
+            "rq_debug_shard_plan": ([ctypes.c_uint32, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ip, u32p, u32p,
+                                     ctypes.c_uint32], ctypes.c_int),
+            "rq_debug_virtual_shards": ([ctypes.c_uint32], ctypes.c_uint32),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -225,6 +229,17 @@ def colprog_assemble(K, esis):
     _check(lib().rq_debug_colprog_assemble(K, e.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), len(e),
                                            ctypes.byref(n)))
     return n.value
+
+
+def shard_plan(device_mask, n_devices, n_blocks, virtual_shards=0):
+    """[(device, first block, end block)] of a host-memory batch call (rq_debug_shard_plan)."""
+    cap = 64
+    dev = (ctypes.c_int * cap)()
+    b0 = (ctypes.c_uint32 * cap)()
+    b1 = (ctypes.c_uint32 * cap)()
+    n = lib().rq_debug_shard_plan(device_mask, n_devices, n_blocks, virtual_shards, dev, b0, b1, cap)
+    _check(min(n, 0))
+    return [(dev[i], b0[i], b1[i]) for i in range(n)]
 
 
 def device_count():

@@ -147,3 +147,31 @@ def test_decode_blocks_host_matches_batch(gpu, rq):
     for b, (buf, *_rest) in enumerate(blocks):
         view = buf.numpy() if hasattr(buf, "numpy") else buf
         assert np.array_equal(view, src[b])
+
+
+def test_host_batch_virtual_shards(gpu, rq):
+    """The per-device host threads of the host-memory batch calls (run_sharded), driven on one GPU by
+    splitting its blocks over 3 threads: the same repairs and decoded payloads as one thread."""
+    K, T, N, nb = 64, 1200, 80, 7
+    rng = np.random.default_rng(11)
+    src = rng.integers(0, 256, (nb, K * T), dtype=np.uint8)
+    esis = list(range(K, N))
+    ref = np.zeros((nb, (N - K) * T), np.uint8)
+    rq.encode_batch_host(src, K, T, esis, ref)
+    old = rq.lib().rq_debug_virtual_shards(3)
+    try:
+        out = np.zeros_like(ref)
+        rq.encode_batch_host(src, K, T, esis, out)
+        assert np.array_equal(out, ref)
+        er = [sorted(rng.choice(K, 5, replace=False).tolist()) for _ in range(nb)]
+        rl = [esis[:12] for _ in range(nb)]
+        data = src.copy()
+        for b in range(nb):
+            for i in er[b]:
+                data[b, i * T:(i + 1) * T] = 0
+        repair = np.concatenate([ref[b].reshape(N - K, T)[:12] for b in range(nb)])  # [n_rows, T]
+        db = rq.DecodeBatch(K, T, er, rl)
+        st = rq.decode_batch_host(db, data, repair)
+        assert (st == 1).all() and np.array_equal(data, src)
+    finally:
+        rq.lib().rq_debug_virtual_shards(old)

@@ -62,3 +62,26 @@ def test_two_rank_gloo():
     assert res[1][3] == 1337 + 4096
     assert all(r[4] == 2.0 for r in res)      # max over ranks
     assert all(r[5] == 8192 for r in res)     # every block processed exactly once
+
+
+# ---- the host-memory batch calls' split over the GPUs of a device mask (rq_engine.cpp run_sharded) ----
+@pytest.mark.parametrize("mask,n_dev,n_blocks", [(0xFF, 8, 8192), (0b1011, 4, 10), (0xFF, 8, 3), (1 << 5, 8, 7),
+                                                 (0, 1, 100), (0x3, 2, 0)])
+def test_device_mask_split(rq, mask, n_dev, n_blocks):
+    plan = rq.shard_plan(mask, n_dev, n_blocks)
+    devs = [i for i in range(32) if mask >> i & 1] or [0]
+    assert len(plan) == max(1, min(len(devs), n_blocks))
+    assert [d for d, _, _ in plan] == devs[:len(plan)]
+    covered = [b for _, b0, b1 in plan for b in range(b0, b1)]
+    assert covered == list(range(n_blocks))  # contiguous, in order, no overlap
+    sizes = [b1 - b0 for _, b0, b1 in plan]
+    assert max(sizes) - min(sizes) <= 1
+
+
+def test_device_mask_errors_and_virtual_shards(rq):
+    with pytest.raises(rq.RaptorQError) as ei:
+        rq.shard_plan(1 << 8, 8, 16)  # device 8 does not exist
+    assert ei.value.code == rq.RQ_ERR_BAD_ARG
+    plan = rq.shard_plan(1 << 2, 8, 10, virtual_shards=3)  # one device, three host threads
+    assert plan == [(2, 0, 3), (2, 3, 6), (2, 6, 10)]
+    assert rq.shard_plan(0x6, 8, 10, virtual_shards=3) == [(1, 0, 5), (2, 5, 10)]  # multi-device: ignored

@@ -66,7 +66,28 @@ def main():
         a, r = rng.randrange(0, 200), rng.randrange(10, R)
         body += [f"\tv_accvgpr_write_b32 a{a}, v{r}", f"\tv_accvgpr_read_b32 v{rng.randrange(10, R)}, a{(a + 37) % 200}"]
     add("k_acc", body)
-    src += meta(names, 512)
+    # instruction kinds at one vs two waves per SIMD (the _2w kernels use 256 registers)
+    kinds = {
+        "bitop3": lambda: f"\tv_bitop3_b32 v{rng.randrange(2, 120)}, v{rng.randrange(2, 120)}, v{rng.randrange(2, 120)}, "
+                          f"v{rng.randrange(2, 120)} bitop3:0x96",
+        "perm": lambda: f"\tv_perm_b32 v{rng.randrange(2, 120)}, v{rng.randrange(2, 120)}, v{rng.randrange(2, 120)}, "
+                        f"v{rng.randrange(2, 120)}",
+        "xor": lambda: f"\tv_xor_b32_e32 v{rng.randrange(2, 120)}, v{rng.randrange(2, 120)}, v{rng.randrange(2, 120)}",
+        "fma": lambda: f"\tv_fma_f32 v{rng.randrange(2, 120)}, v{rng.randrange(2, 120)}, v{rng.randrange(2, 120)}, "
+                       f"v{rng.randrange(2, 120)}",
+        "lshl": lambda: f"\tv_lshlrev_b32_e32 v{rng.randrange(2, 120)}, 3, v{rng.randrange(2, 120)}",
+    }
+    two = []
+    for kname, gen in kinds.items():
+        body = [gen() for _ in range(N)]
+        add("k_%s_1w" % kname, body)
+        src += kernel("k_%s_2w" % kname, init(120) + consts() + body + store(120), nvgpr=256, accum=256)
+        two.append("k_%s_2w" % kname)
+    m1 = meta(names, 512)
+    m2 = meta(two, 256).replace(".agpr_count: 256", ".agpr_count: 0")
+    body2 = m2.split("amdhsa.kernels:\n", 1)[1].split("\namdhsa.target", 1)[0]
+    src += m1.replace("\namdhsa.target", "\n" + body2 + "\namdhsa.target", 1)
+    names += two
     with open(os.path.join(out, "dep.s"), "w") as f:
         f.write(src)
     clang = "/opt/rocm/llvm/bin/clang"

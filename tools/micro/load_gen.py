@@ -11,7 +11,7 @@ HDR = '\t.amdgcn_target "amdgcn-amd-amdhsa--gfx950"\n\t.amdhsa_code_object_versi
 ROWS, T, BLK = 1024, 1200, 1024 * 1200
 
 
-def kernel(name, D, valu_per_load, nvgpr=512):
+def kernel(name, D, valu_per_load, nvgpr=512, width=1):
     s = [f"\t.globl {name}", "\t.p2align 8", f"\t.type {name},@function", f"{name}:",
          "\ts_load_dwordx4 s[4:7], s[0:1], 0x0", "\ts_waitcnt lgkmcnt(0)",
          # wave w: block w / 5, column chunk (w % 5) * 256 (the last chunk of 1200 B is partial)
@@ -19,15 +19,21 @@ def kernel(name, D, valu_per_load, nvgpr=512):
          "\ts_lshl_b32 s9, s9, 8", "\ts_mul_i32 s10, s8, %d" % BLK,
          "\ts_add_u32 s20, s4, s10", "\ts_addc_u32 s21, s5, 0", "\ts_mov_b32 s22, -1", "\ts_mov_b32 s23, 0x20000",
          "\tv_lshlrev_b32_e32 v1, 2, v0", "\tv_add_u32_e32 v1, s9, v1", "\tv_mov_b32_e32 v2, 0"]
-    for i in range(ROWS):
-        row = (i * 389) % ROWS
-        r = 10 + (i % D)
+    nl = ROWS // width
+    if width > 1:  # lane l reads 4*width bytes at 4*width*l: the same bytes per wave in fewer loads
+        s.append(f"\tv_lshlrev_b32_e32 v1, {2 + (width.bit_length() - 1)}, v0")
+        s.append("\tv_add_u32_e32 v1, s9, v1")
+    for i in range(nl):
+        row = (i * 389) % nl
+        r = 10 + width * (i % D)
         if i >= D:
             s.append(f"\ts_waitcnt vmcnt({D - 1})")
             for _ in range(valu_per_load):
                 s.append(f"\tv_bitop3_b32 v2, v2, v{r}, v3 bitop3:0x96")
-        s.append(f"\ts_mov_b32 s24, {row * T}")
-        s.append(f"\tbuffer_load_dword v{r}, v1, s[20:23], s24 offen")
+        s.append(f"\ts_mov_b32 s24, {row * T * width}")
+        op = {1: "buffer_load_dword", 2: "buffer_load_dwordx2", 4: "buffer_load_dwordx4"}[width]
+        dst = f"v{r}" if width == 1 else f"v[{r}:{r + width - 1}]"
+        s.append(f"\t{op} {dst}, v1, s[20:23], s24 offen")
     s += ["\ts_waitcnt vmcnt(0)", "\tv_lshlrev_b32_e32 v0, 2, v0", "\ts_lshl_b32 s11, s2, 8",
           "\tv_add_u32_e32 v0, s11, v0", "\tglobal_store_dword v0, v2, s[6:7]", "\ts_endpgm",
           f".Lend_{name}:", f"\t.size {name}, .Lend_{name}-{name}"]
@@ -43,7 +49,7 @@ def kernel(name, D, valu_per_load, nvgpr=512):
 \t\t.amdhsa_system_vgpr_workitem_id 0
 \t\t.amdhsa_next_free_vgpr {nvgpr}
 \t\t.amdhsa_next_free_sgpr 32
-\t\t.amdhsa_accum_offset 256
+\t\t.amdhsa_accum_offset {min(nvgpr, 256)}
 \t\t.amdhsa_reserve_vcc 0
 \t\t.amdhsa_ieee_mode 0
 \t\t.amdhsa_dx10_clamp 0
@@ -56,7 +62,8 @@ def kernel(name, D, valu_per_load, nvgpr=512):
 def meta(names, nvgpr=512):
     ks = []
     for n in names:
-        ks.append(f"""  - .agpr_count: 256
+        nv = 256 if n.endswith("_2w") else nvgpr
+        ks.append(f"""  - .agpr_count: {nv - 256 if nv > 256 else 0}
     .args:
       - .offset: 0
         .size: 16
@@ -69,7 +76,7 @@ def meta(names, nvgpr=512):
     .private_segment_fixed_size: 0
     .sgpr_count: 32
     .symbol: {n}.kd
-    .vgpr_count: {nvgpr}
+    .vgpr_count: {nv}
     .wavefront_size: 64""")
     return "\t.amdgpu_metadata\n---\namdhsa.kernels:\n" + "\n".join(ks) + \
         "\namdhsa.target: amdgcn-amd-amdhsa--gfx950\namdhsa.version:\n  - 1\n  - 2\n...\n\t.end_amdgpu_metadata\n"
@@ -84,6 +91,12 @@ def main():
             n = f"k_d{D}_v{v}"
             src += kernel(n, D, v)
             names.append(n)
+    for w, v in ((2, 40), (4, 80), (4, 1)):  # same bytes and VALU per byte, fewer (wider) loads
+        n = f"k_x{w}_d16_v{v}"
+        src += kernel(n, 16, v, width=w)
+        names.append(n)
+    src += kernel("k_d32_v20_2w", 32, 20, nvgpr=256)  # two waves per SIMD
+    names.append("k_d32_v20_2w")
     src += meta(names)
     with open(os.path.join(out, "load.s"), "w") as f:
         f.write(src)
