@@ -273,6 +273,118 @@ __global__ void __launch_bounds__(64 * NW) k_solve_fast(SolveArgs a) {
     if (tid == 0) a.status[b] = 1;
 }
 
+// The five v_perm tables of a coefficient c (byte lanes): c*{0..3}, c*{4..7}, c*{0,8,16,24},
+// c*{32,40,48,56}, c*{0,64,128,192}, from the eight alpha^i multiples of c.
+__device__ __forceinline__ uint8_t xtime1(uint32_t x) { return (uint8_t)((x << 1) ^ ((x & 0x80u) ? 0x1Du : 0u)); }
+
+__device__ __forceinline__ void perm_tables(uint32_t c, uint4* A, uint32_t* B) {
+    uint32_t m[8];
+    m[0] = c;
+#pragma unroll
+    for (int i = 1; i < 8; ++i) m[i] = xtime1(m[i - 1]);
+    auto lo = [&](uint32_t x) { return ((x & 1u) ? m[0] : 0u) ^ ((x & 2u) ? m[1] : 0u) ^ ((x & 4u) ? m[2] : 0u); };
+    auto pack = [](uint32_t a, uint32_t b, uint32_t c2, uint32_t d) { return a | (b << 8) | (c2 << 16) | (d << 24); };
+    A->x = pack(0, lo(1), lo(2), lo(3));
+    A->y = pack(lo(4), lo(5), lo(6), lo(7));
+    A->z = pack(0, m[3], m[4], m[3] ^ m[4]);
+    A->w = pack(m[5], m[5] ^ m[3], m[5] ^ m[4], m[5] ^ m[4] ^ m[3]);
+    *B = pack(0, m[6], m[7], m[6] ^ m[7]);
+}
+
+// One wave per block for e <= 64 on the first <= 64 received repairs, the rows held in registers:
+// lane j owns received repair j as 32 dwords (e coefficient bytes, then the identity part at byte
+// e + j).  Each step k takes the lowest unused row with a nonzero coefficient in column k (ballot),
+// and every lane folds the pivot row (read dword by dword with v_readlane: uniform, so the v_perm
+// selectors are scalar) scaled by its own coefficient c_j = f_j / f_p into its row -- one GF(256)
+// multiply per dword as three v_perm lookups against per-lane tables of c_j (perm_tables).  The
+// pivot lane uses c = 1 ^ 1/f_p, which leaves row_p / f_p.  No barrier inside the elimination.
+__device__ __forceinline__ uint32_t perm_mul(const uint4& A, uint32_t B, uint32_t x) {
+    const uint32_t s0 = x & 0x07070707u, s1 = (x >> 3) & 0x07070707u, s2 = (x >> 6) & 0x03030303u;
+    return xor3(__builtin_amdgcn_perm(A.y, A.x, s0), __builtin_amdgcn_perm(A.w, A.z, s1),
+                __builtin_amdgcn_perm(B, B, s2));
+}
+
+__global__ void __launch_bounds__(64) k_solve_reg(SolveArgs a) {
+    __shared__ uint8_t ex[512], lg[256];
+    __shared__ uint8_t pivl[64];
+    __shared__ uint32_t rows[64 * 33];  // final rows, stride 33 dwords (no bank conflicts)
+    const uint32_t b = a.blk_map[blockIdx.x];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t e = a.erased_off[b + 1] - a.erased_off[b];
+    const uint32_t nr = a.rep_cnt[b];
+    if (e > 64) {
+        if (lane == 0) a.status[b] = ST_FALLBACK;
+        return;
+    }
+    const uint32_t nrow = min(nr, 64u);
+    const uint32_t* E = a.erased + a.erased_off[b];
+    const uint32_t* U = a.rep_uidx + a.rep_off[b];
+    gf_tables_copy(ex, lg);
+    uint32_t row[32];
+#pragma unroll
+    for (int w = 0; w < 32; ++w) row[w] = 0;
+    if (lane < nrow) {
+        const uint8_t* mr = a.mrep + (size_t)U[lane] * a.mrep_stride;
+#pragma unroll
+        for (int w = 0; w < 16; ++w)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if ((uint32_t)(4 * w + i) < e) row[w] |= (uint32_t)mr[E[4 * w + i]] << (8 * i);
+        const uint32_t pos = e + lane;
+#pragma unroll
+        for (int w = 0; w < 32; ++w)
+            if ((pos >> 2) == (uint32_t)w) row[w] |= 1u << (8 * (pos & 3));
+    }
+    bool used = lane >= nrow;
+    const uint32_t q1 = (e + nrow + 3) >> 2;  // live dwords
+    __syncthreads();                          // GF tables
+    for (uint32_t k = 0; k < e; ++k) {
+        const uint32_t W = k >> 2;
+        uint32_t rw = 0;
+#pragma unroll
+        for (int w = 0; w < 16; ++w)
+            if ((uint32_t)w == W) rw = row[w];
+        const uint32_t f = (rw >> (8 * (k & 3))) & 0xFFu;
+        const uint64_t bal = __ballot(f != 0 && !used);
+        if (bal == 0) {  // rank-deficient on these rows (uniform)
+            if (lane == 0) a.status[b] = (nr > nrow) ? ST_FALLBACK : 0;
+            return;
+        }
+        const uint32_t p = (uint32_t)__ffsll((unsigned long long)bal) - 1;
+        const bool me = lane == p;
+        used |= me;
+        const uint32_t fp = (uint32_t)__builtin_amdgcn_readlane((int)f, (int)p);
+        const uint32_t lginv = 255u - lg[fp];
+        uint32_t c = f ? ex[lg[f] + lginv] : 0u;
+        if (me) c = ex[lginv] ^ 1u;
+        uint4 A;
+        uint32_t B;
+        perm_tables(c, &A, &B);
+#pragma unroll
+        for (int w = 0; w < 32; ++w) {
+            if ((uint32_t)w >= W && (uint32_t)w < q1) {
+                const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)row[w], (int)p);
+                row[w] ^= perm_mul(A, B, x);
+            }
+        }
+        if (lane == 0) pivl[k] = (uint8_t)p;
+    }
+#pragma unroll
+    for (int w = 0; w < 32; ++w) rows[lane * 33 + w] = row[w];
+    __syncthreads();
+    // X[k][m] = identity byte (e + piv_m) of pivot row piv_k
+    uint8_t* xc = a.xcoef + 64ull * a.xoff[blockIdx.x];
+    const uint32_t xs = x_stride(e);
+    uint16_t* XP = a.xpiv + a.erased_off[b];
+    for (uint32_t m = lane; m < e; m += 64) XP[m] = pivl[m];
+    const uint8_t* rb = reinterpret_cast<const uint8_t*>(rows);
+    for (uint32_t idx = lane; idx < e * e; idx += 64) {
+        const uint32_t m = idx / e, k = idx - m * e;
+        xc[m * xs + k] = rb[pivl[k] * 132 + e + pivl[m]];
+    }
+    if (lane == 0) a.status[b] = 1;
+}
+
 // General solver for the blocks the fast solvers deferred: any e, every received repair.  The
 // received rows are taken in order and reduced against a Gauss-Jordan basis of the rows kept so far
 // (basis row i: pivot column pc[i], coefficients zero on every other pivot column, then the
@@ -367,7 +479,9 @@ size_t solve_ws_bytes(uint32_t e) {
     return W2 + ((e + 15) & ~15u) + 4 * ((e + 7) & ~7u) + (size_t)e * W2;
 }
 
-// Waves per block of the e <= 64 solver (RQHIP_SOLVE_NW in experiments builds).
+// The e <= 64 solver: k_solve_fast<1> with four waves per block; experiments builds select one wave
+// (RQHIP_SOLVE_NW=1) or the register-resident k_solve_reg (RQHIP_SOLVE_NW=0; measured 111 us against
+// 94 us for the four-wave solver at 1 024 blocks, e = 55: profiles/r02r).
 static int solve_nw() {
 #ifdef RQHIP_EXPERIMENTS
     static const int nw = [] {
@@ -381,8 +495,11 @@ static int solve_nw() {
 }
 
 int launch_solve(const SolveArgs& a, uint32_t n_blocks, bool need_general, uint32_t max_lds_e, void* stream) {
-    if (solve_nw() == 1) hipLaunchKernelGGL((k_solve_fast<1, 1>), dim3(n_blocks), dim3(64), 0, (hipStream_t)stream, a);
-    else hipLaunchKernelGGL((k_solve_fast<1, 4>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a);
+    switch (solve_nw()) {
+        case 1: hipLaunchKernelGGL((k_solve_fast<1, 1>), dim3(n_blocks), dim3(64), 0, (hipStream_t)stream, a); break;
+        case 4: hipLaunchKernelGGL((k_solve_fast<1, 4>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a); break;
+        default: hipLaunchKernelGGL(k_solve_reg, dim3(n_blocks), dim3(64), 0, (hipStream_t)stream, a); break;
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !need_general) return (int)e;
     hipLaunchKernelGGL((k_solve_fast<2, 4>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a);
@@ -409,24 +526,6 @@ uint32_t solve_lds_e_max() {
 // v_perm (selectors x & 7, (x >> 3) & 7, x >> 6 per byte) against per-coefficient tables and two
 // XORs per dword: 5 VALU per mul-add instead of 8 bit-selects (replaces asmSSSE3MulAdd's nibble
 // pshufb, RQ/discmath/optimizations.s:36-78, with CDNA4's byte permute).
-
-// The five v_perm tables of a coefficient c (byte lanes): c*{0..3}, c*{4..7}, c*{0,8,16,24},
-// c*{32,40,48,56}, c*{0,64,128,192}, from the eight alpha^i multiples of c.
-__device__ __forceinline__ uint8_t xtime1(uint32_t x) { return (uint8_t)((x << 1) ^ ((x & 0x80u) ? 0x1Du : 0u)); }
-
-__device__ __forceinline__ void perm_tables(uint32_t c, uint4* A, uint32_t* B) {
-    uint32_t m[8];
-    m[0] = c;
-#pragma unroll
-    for (int i = 1; i < 8; ++i) m[i] = xtime1(m[i - 1]);
-    auto lo = [&](uint32_t x) { return ((x & 1u) ? m[0] : 0u) ^ ((x & 2u) ? m[1] : 0u) ^ ((x & 4u) ? m[2] : 0u); };
-    auto pack = [](uint32_t a, uint32_t b, uint32_t c2, uint32_t d) { return a | (b << 8) | (c2 << 16) | (d << 24); };
-    A->x = pack(0, lo(1), lo(2), lo(3));
-    A->y = pack(lo(4), lo(5), lo(6), lo(7));
-    A->z = pack(0, m[3], m[4], m[3] ^ m[4]);
-    A->w = pack(m[5], m[5] ^ m[3], m[5] ^ m[4], m[5] ^ m[4] ^ m[3]);
-    *B = pack(0, m[6], m[7], m[6] ^ m[7]);
-}
 
 // One wave per (unit = solved block x strip, output slice of KC).  Workgroup w maps to slice
 // (w / 8) % np of unit (w / 8np) * 8 + w % 8: the slices of one unit share an XCD (workgroups are
