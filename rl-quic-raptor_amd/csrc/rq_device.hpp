@@ -37,6 +37,17 @@ struct ZeroArgs {
     uint8_t* pack;              // k_pack_rows: row i of the list -> pack + i*T
 };
 
+// Zero the erased source rows of the blocks of a decode pass: workgroup bi takes block blk_map[bi]
+// (four waves, one erased row each in turn), so no per-row list crosses PCIe.
+struct ZeroBlocksArgs {
+    const uint32_t* blk_map;
+    const uint32_t* erased_off;
+    const uint32_t* erased;
+    uint8_t* data;
+    uint64_t data_stride;
+    uint32_t T, nw;
+};
+
 // Per solved block bi (block b = blk_map[bi], e erased rows): X (e x xs bytes, xs = x_stride(e))
 // at xcoef + 64 * xoff[bi], X[k][m] at row m, byte k; the e received repairs it combines (indices
 // within the block) at xpiv + erased_off[b].
@@ -85,6 +96,7 @@ struct ApplyArgs {
 
 // Launchers (rq_kernels.hip).  Return hipError_t as int.
 int launch_zero_rows(const ZeroArgs& a, void* stream);
+int launch_zero_blocks(const ZeroBlocksArgs& a, void* stream);
 // Host-memory decode: copy the recovered rows (the same (blk, row) list) into a dense buffer so only
 // e*T bytes per block travel back over PCIe.
 int launch_pack_rows(const ZeroArgs& a, void* stream);

@@ -114,11 +114,11 @@ struct Workspace {
     HostBuf h_status, h_pack;
     // decode descriptors, double-buffered so that rq_decode_batch_async can return before its upload
     // ran: call n uses set n % 2; the host refills a set's pinned staging only after that set's
-    // previous upload completed (`up`), and reallocates its device copy only once the kernels that
-    // read it are done (`used`)
+    // previous upload completed (`up`); the device copy is rewritten in stream order, and grown
+    // only after a stream synchronisation
     DevBuf idx[2];
     HostBuf h_idx[2];
-    hipEvent_t up[2] = {nullptr, nullptr}, used[2] = {nullptr, nullptr};
+    hipEvent_t up[2] = {nullptr, nullptr};
     uint32_t flip = 0;
 };
 
@@ -565,9 +565,10 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     // union index of every candidate repair: direct for a dense union, binary search otherwise
     const bool dense_uni = uni.back() - uni.front() + 1 == uni.size();
     const size_t n_er = eoff[n_blocks], n_rep = roff[n_blocks];
-    // index workspace: blk_map | eoff | roff | cnt | erased | rep_uidx | status | zero (blk, row) | xoff | goff
+    // index workspace: blk_map | eoff | roff | cnt | erased | rep_uidx | status | xoff | goff
+    // [| pack list (blk, row): host-memory decodes only]
     std::vector<uint32_t> idx;
-    idx.reserve(nw * 3 + 3 * (n_blocks + 1) + n_er * 3 + n_rep + n_blocks);
+    idx.reserve(nw * 3 + 3 * (n_blocks + 1) + n_er * (po ? 3 : 1) + n_rep + n_blocks);
     const size_t o_map = 0;
     idx.insert(idx.end(), blk_map.begin(), blk_map.end());
     const size_t o_eoff = idx.size();
@@ -593,17 +594,19 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
         }
     const size_t o_st = idx.size();  // device status: host-decided values, ST_PENDING for the rest
     for (uint32_t b = 0; b < n_blocks; ++b) idx.push_back((uint32_t)status[b]);
-    const size_t o_zb = idx.size();
-    uint32_t nz = 0;
-    for (uint32_t b : blk_map)
-        for (uint32_t i = eoff[b]; i < eoff[b + 1]; ++i, ++nz) idx.push_back(b);
-    const size_t o_zr = idx.size();
-    for (uint32_t b : blk_map)
-        for (uint32_t i = eoff[b]; i < eoff[b + 1]; ++i) idx.push_back(erased[i]);
     const size_t o_xo = idx.size();
     idx.insert(idx.end(), xoff.begin(), xoff.end());
     const size_t o_go = idx.size();
     idx.insert(idx.end(), goff.begin(), goff.end());
+    const size_t o_zb = idx.size();
+    uint32_t nz = 0;
+    if (po) {  // recovered rows packed densely for the download, in blk_map order
+        for (uint32_t b : blk_map)
+            for (uint32_t i = eoff[b]; i < eoff[b + 1]; ++i, ++nz) idx.push_back(b);
+        for (uint32_t b : blk_map)
+            for (uint32_t i = eoff[b]; i < eoff[b + 1]; ++i) idx.push_back(erased[i]);
+    }
+    const size_t o_zr = o_zb + nz;
     // descriptor upload through pinned staging, queued behind the caller's work on the stream (e.g.
     // the encode that produced `repair`) without blocking this thread.  (A separate copy stream
     // overlapping the upload with that work measured slower with rq_decode_batch_async.)
@@ -612,12 +615,11 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     if (!w->up[0]) {
         for (int i = 0; i < 2; ++i) {
             HIP_TRY(hipEventCreateWithFlags(&w->up[i], hipEventDisableTiming));
-            HIP_TRY(hipEventCreateWithFlags(&w->used[i], hipEventDisableTiming));
         }
     }
     HIP_TRY(hipEventSynchronize(w->up[set]));  // the staging's previous upload has been read
     if ((rc = w->h_idx[set].ensure(idx.size() * 4)) || (rc = w->h_status.ensure((size_t)n_blocks * 4))) return rc;
-    if (w->idx[set].cap < idx.size() * 4) HIP_TRY(hipEventSynchronize(w->used[set]));  // realloc: set idle
+    if (w->idx[set].cap < idx.size() * 4) HIP_TRY(hipStreamSynchronize((hipStream_t)stream));  // realloc: idle
     if ((rc = w->idx[set].ensure(idx.size() * 4))) return rc;
     std::memcpy(w->h_idx[set].p, idx.data(), idx.size() * 4);
     HIP_TRY(hipMemcpyAsync(w->idx[set].p, w->h_idx[set].p, idx.size() * 4, hipMemcpyHostToDevice, (hipStream_t)stream));
@@ -629,10 +631,13 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     if (go && (rc = w->gws.ensure((size_t)go * 64))) return rc;
 
     // 1) erased rows := 0, then r0 = the column program on every block (syndromes s = r ^ r0)
+    ZeroBlocksArgs zb;
+    zb.blk_map = di + o_map; zb.erased_off = di + o_eoff; zb.erased = di + o_er;
+    zb.data = static_cast<uint8_t*>(data); zb.data_stride = data_stride; zb.T = T; zb.nw = nw;
+    if (launch_zero_blocks(zb, stream)) return fail(RQ_ERR_DEVICE, "k_zero_blocks launch failed");
     ZeroArgs z;
     z.blk = di + o_zb; z.row = di + o_zr; z.data = static_cast<uint8_t*>(data); z.data_stride = data_stride;
     z.T = T; z.n = nz; z.pack = nullptr;
-    if (launch_zero_rows(z, stream)) return fail(RQ_ERR_DEVICE, "k_zero_rows launch failed");
     if ((rc = launch_col(ctx, k, T, n_blocks, data, data_stride, w->r0.p, (uint64_t)uni.size() * T, stream)))
         return rc;
     // 2) per-block solve
@@ -682,13 +687,11 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     if (async) {  // statuses land in the caller's pinned array when the stream gets here
         HIP_TRY(hipMemcpyAsync(status, w->idx[set].as<uint32_t>() + o_st, n_blocks * 4, hipMemcpyDeviceToHost,
                                (hipStream_t)stream));
-        HIP_TRY(hipEventRecord(w->used[set], (hipStream_t)stream));
         return RQ_OK;
     }
     int32_t* st = static_cast<int32_t*>(w->h_status.p);
     HIP_TRY(hipMemcpyAsync(st, w->idx[set].as<uint32_t>() + o_st, n_blocks * 4, hipMemcpyDeviceToHost,
                            (hipStream_t)stream));
-    HIP_TRY(hipEventRecord(w->used[set], (hipStream_t)stream));
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
     for (uint32_t b : blk_map) status[b] = st[b];
     if (po) {

@@ -109,6 +109,27 @@ int launch_zero_rows(const ZeroArgs& a, void* stream) {
     return (int)hipGetLastError();
 }
 
+__global__ void __launch_bounds__(256) k_zero_blocks(ZeroBlocksArgs a) {
+    const uint32_t b = a.blk_map[blockIdx.x], wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t e0 = a.erased_off[b], e1 = a.erased_off[b + 1];
+    uint8_t* blk = a.data + (size_t)b * a.data_stride;
+    for (uint32_t i = e0 + wave; i < e1; i += 4) {
+        uint4* r16 = reinterpret_cast<uint4*>(blk + (size_t)a.erased[i] * a.T);
+        uint32_t* r4 = reinterpret_cast<uint32_t*>(r16);
+        if ((a.T & 15) == 0 && ((uintptr_t)r16 & 15) == 0) {
+            for (uint32_t c = lane; c < a.T / 16; c += 64) r16[c] = make_uint4(0, 0, 0, 0);
+        } else {
+            for (uint32_t c = lane; c < a.T / 4; c += 64) r4[c] = 0;
+        }
+    }
+}
+
+int launch_zero_blocks(const ZeroBlocksArgs& a, void* stream) {
+    if (a.nw == 0) return 0;
+    hipLaunchKernelGGL(k_zero_blocks, dim3(a.nw), dim3(256), 0, (hipStream_t)stream, a);
+    return (int)hipGetLastError();
+}
+
 // Recovered row i of the same list -> pack + i*T (dense D2H staging), one wave per row.
 __global__ void __launch_bounds__(256) k_pack_rows(ZeroArgs a) {
     const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
