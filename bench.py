@@ -343,7 +343,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     dt = rqshard.max_over_ranks(time.perf_counter() - t0, dist, coll_dev)
-    assert np.array_equal(st_async, st), "async decode statuses differ"
+    if not args.no_verify:
+        assert np.array_equal(st_async, st), "async decode statuses differ"
     enc_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1, _ in ev]))
     dec_ms = float(np.mean([e1.elapsed_time(e2) for _, e1, e2 in ev]))
     total_blocks = rqshard.sum_over_ranks(B, dist, coll_dev)

@@ -25,27 +25,17 @@ struct DevParams {
 // Decode, per block b: erased source rows E = erased[erased_off[b] .. erased_off[b+1]) and
 // received repair symbols j = rep_off[b] .. rep_off[b+1] (rows of `recv`, T bytes each) whose
 // ESIs sit at index rep_uidx[j] of the column program's output list ("union").
-//   r0   : column program outputs on the data with erased rows zeroed, n_union rows per block
+//   r0   : column program outputs on the data as received (erased rows hold whatever bytes g_E),
+//          n_union rows per block; s = recv ^ r0 = M (x_E ^ g_E)
 //   mrep : column program outputs on the identity payload: mrep[u*mrep_stride + i] = coefficient
 //          of source row i in output u (the repair rows of G*A^-1 restricted to source columns)
-struct ZeroArgs {
-    const uint32_t* blk;        // [n] block index of each erased row
-    const uint32_t* row;        // [n] erased source row
+struct PackArgs {
+    const uint32_t* blk;        // [n] block index of each recovered row
+    const uint32_t* row;        // [n] recovered source row
     uint8_t* data;
     uint64_t data_stride;
     uint32_t T, n;
     uint8_t* pack;              // k_pack_rows: row i of the list -> pack + i*T
-};
-
-// Zero the erased source rows of the blocks of a decode pass: workgroup bi takes block blk_map[bi]
-// (four waves, one erased row each in turn), so no per-row list crosses PCIe.
-struct ZeroBlocksArgs {
-    const uint32_t* blk_map;
-    const uint32_t* erased_off;
-    const uint32_t* erased;
-    uint8_t* data;
-    uint64_t data_stride;
-    uint32_t T, nw;
 };
 
 // Per solved block bi (block b = blk_map[bi], e erased rows): X (e x xs bytes, xs = x_stride(e))
@@ -95,11 +85,9 @@ struct ApplyArgs {
 };
 
 // Launchers (rq_kernels.hip).  Return hipError_t as int.
-int launch_zero_rows(const ZeroArgs& a, void* stream);
-int launch_zero_blocks(const ZeroBlocksArgs& a, void* stream);
 // Host-memory decode: copy the recovered rows (the same (blk, row) list) into a dense buffer so only
 // e*T bytes per block travel back over PCIe.
-int launch_pack_rows(const ZeroArgs& a, void* stream);
+int launch_pack_rows(const PackArgs& a, void* stream);
 // Fast solves (e <= 64 on the first 64 received repairs, e <= 128 on the first 128), then the
 // general solver (any e, every received repair) for the blocks they deferred.
 int launch_solve(const SolveArgs& a, uint32_t n_blocks, bool need_general, uint32_t max_lds_e, void* stream);

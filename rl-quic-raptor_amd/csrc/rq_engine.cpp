@@ -631,12 +631,9 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     if ((rc = w->xp.ensure(std::max<size_t>(n_er, 1) * 2))) return rc;
     if (go && (rc = w->gws.ensure((size_t)go * 64))) return rc;
 
-    // 1) erased rows := 0, then r0 = the column program on every block (syndromes s = r ^ r0)
-    ZeroBlocksArgs zb;
-    zb.blk_map = di + o_map; zb.erased_off = di + o_eoff; zb.erased = di + o_er;
-    zb.data = static_cast<uint8_t*>(data); zb.data_stride = data_stride; zb.T = T; zb.nw = nw;
-    if (launch_zero_blocks(zb, stream)) return fail(RQ_ERR_DEVICE, "k_zero_blocks launch failed");
-    ZeroArgs z;
+    // 1) r0 = the column program on every block, erased rows as they are (whatever bytes g_E they
+    //    hold): the syndromes s = r ^ r0 = M (x_E ^ g_E), and k_apply starts each output from g_E
+    PackArgs z;
     z.blk = di + o_zb; z.row = di + o_zr; z.data = static_cast<uint8_t*>(data); z.data_stride = data_stride;
     z.T = T; z.n = nz; z.pack = nullptr;
     if ((rc = launch_col(ctx, k, T, n_blocks, data, data_stride, w->r0.p, (uint64_t)uni.size() * T, stream)))

@@ -89,49 +89,9 @@ __device__ __forceinline__ void d_for_cols(const DevParams& p, uint32_t X, F&& f
     }
 }
 
-// ------------------------------ decode: zero the erased source rows --------------------------
-// One wave per erased row, four rows per workgroup: the syndrome pass reads erased rows as zero.
-__global__ void __launch_bounds__(256) k_zero_rows(ZeroArgs a) {
-    const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (i >= a.n) return;
-    uint4* r16 = reinterpret_cast<uint4*>(a.data + (size_t)a.blk[i] * a.data_stride + (size_t)a.row[i] * a.T);
-    uint32_t* r4 = reinterpret_cast<uint32_t*>(r16);
-    if ((a.T & 15) == 0 && ((uintptr_t)r16 & 15) == 0) {
-        for (uint32_t c = lane; c < a.T / 16; c += 64) r16[c] = make_uint4(0, 0, 0, 0);
-    } else {
-        for (uint32_t c = lane; c < a.T / 4; c += 64) r4[c] = 0;
-    }
-}
-
-int launch_zero_rows(const ZeroArgs& a, void* stream) {
-    if (a.n == 0) return 0;
-    hipLaunchKernelGGL(k_zero_rows, dim3((a.n + 3) / 4), dim3(256), 0, (hipStream_t)stream, a);
-    return (int)hipGetLastError();
-}
-
-__global__ void __launch_bounds__(256) k_zero_blocks(ZeroBlocksArgs a) {
-    const uint32_t b = a.blk_map[blockIdx.x], wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t e0 = a.erased_off[b], e1 = a.erased_off[b + 1];
-    uint8_t* blk = a.data + (size_t)b * a.data_stride;
-    for (uint32_t i = e0 + wave; i < e1; i += 4) {
-        uint4* r16 = reinterpret_cast<uint4*>(blk + (size_t)a.erased[i] * a.T);
-        uint32_t* r4 = reinterpret_cast<uint32_t*>(r16);
-        if ((a.T & 15) == 0 && ((uintptr_t)r16 & 15) == 0) {
-            for (uint32_t c = lane; c < a.T / 16; c += 64) r16[c] = make_uint4(0, 0, 0, 0);
-        } else {
-            for (uint32_t c = lane; c < a.T / 4; c += 64) r4[c] = 0;
-        }
-    }
-}
-
-int launch_zero_blocks(const ZeroBlocksArgs& a, void* stream) {
-    if (a.nw == 0) return 0;
-    hipLaunchKernelGGL(k_zero_blocks, dim3(a.nw), dim3(256), 0, (hipStream_t)stream, a);
-    return (int)hipGetLastError();
-}
-
+// ------------------------------ decode: pack the recovered rows ---------------------------
 // Recovered row i of the same list -> pack + i*T (dense D2H staging), one wave per row.
-__global__ void __launch_bounds__(256) k_pack_rows(ZeroArgs a) {
+__global__ void __launch_bounds__(256) k_pack_rows(PackArgs a) {
     const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (i >= a.n) return;
     const uint32_t* r4 = reinterpret_cast<const uint32_t*>(a.data + (size_t)a.blk[i] * a.data_stride + (size_t)a.row[i] * a.T);
@@ -139,7 +99,7 @@ __global__ void __launch_bounds__(256) k_pack_rows(ZeroArgs a) {
     for (uint32_t c = lane; c < a.T / 4; c += 64) p4[c] = r4[c];
 }
 
-int launch_pack_rows(const ZeroArgs& a, void* stream) {
+int launch_pack_rows(const PackArgs& a, void* stream) {
     if (a.n == 0) return 0;
     hipLaunchKernelGGL(k_pack_rows, dim3((a.n + 3) / 4), dim3(256), 0, (hipStream_t)stream, a);
     return (int)hipGetLastError();
@@ -590,11 +550,16 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a, uint32_t n_units, uin
         live[j] = c < Td;
         col[j] = live[j] ? c : 0;
     }
+    // The erased rows were not cleared before the syndrome program, so s = M (x_E ^ g_E) with g_E their
+    // current bytes: start every output from g_E and X s completes it to x_E.
+    const uint32_t kn = min((uint32_t)KC, e - k0);
     uint32_t acc[KC][CPL];
 #pragma unroll
-    for (int k = 0; k < KC; ++k)
+    for (int k = 0; k < KC; ++k) {
+        const uint32_t* grow = reinterpret_cast<const uint32_t*>(blk + (size_t)E[k0 + min((uint32_t)k, kn - 1)] * a.T);
 #pragma unroll
-        for (int j = 0; j < CPL; ++j) acc[k][j] = 0;
+        for (int j = 0; j < CPL; ++j) acc[k][j] = ((uint32_t)k < kn && live[j]) ? grow[col[j]] : 0u;
+    }
     // syndromes are loaded PD m ahead into a ring (received row and r0 row, XORed on use); MC is a
     // multiple of PD, so ring slot d always holds syndrome m = d (mod PD) across chunks
     uint32_t ra[PD][CPL], rb[PD][CPL];
@@ -661,7 +626,6 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a, uint32_t n_units, uin
             }
         }
     }
-    const uint32_t kn = min((uint32_t)KC, e - k0);
 #pragma unroll
     for (int k = 0; k < KC; ++k) {
         if ((uint32_t)k < kn) {
