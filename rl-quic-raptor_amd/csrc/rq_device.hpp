@@ -90,7 +90,10 @@ struct ApplyArgs {
 int launch_pack_rows(const PackArgs& a, void* stream);
 // Fast solves (e <= 64 on the first 64 received repairs, e <= 128 on the first 128), then the
 // general solver (any e, every received repair) for the blocks they deferred.
-int launch_solve(const SolveArgs& a, uint32_t n_blocks, bool need_general, uint32_t max_lds_e, void* stream);
+// need_general: some block may end in the general solver (e or candidate repairs > 64); wide: some
+// block has 64 < e <= 128 (the two-row-per-lane fast solver runs first).
+int launch_solve(const SolveArgs& a, uint32_t n_blocks, bool need_general, bool wide, uint32_t max_lds_e,
+                 void* stream);
 int launch_apply(const ApplyArgs& a, uint32_t n_strips, uint32_t n_blocks, void* stream);
 int launch_gather(const DevParams& p, const uint8_t* C, uint32_t T, const uint32_t* esi, uint32_t n, uint8_t* out,
                   void* stream);

@@ -544,6 +544,7 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     const uint32_t nw = (uint32_t)blk_map.size();
     uint32_t max_e = 0, max_lds_e = 0;
     bool need_general = false;  // some block may reach the general solver (e or candidates > 64)
+    bool wide = false;          // some block has 64 < e <= 128
     std::vector<uint32_t> cand;
     std::vector<uint32_t> xoff(nw), goff(nw);
     uint64_t xo = 0, go = 0;
@@ -552,6 +553,7 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
         max_e = std::max(max_e, e);
         if (e <= lds_e_max()) max_lds_e = std::max(max_lds_e, e);
         need_general |= (e > 64 || cnt[b] > 64);
+        wide |= (e > 64 && e <= 128);
         cand.insert(cand.end(), repair_esi + roff[b], repair_esi + roff[b] + cnt[b]);
         xoff[bi] = (uint32_t)xo;
         xo += ((uint64_t)e * x_stride(e) + 63) / 64;
@@ -655,7 +657,7 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     s.gws = w->gws.as<uint8_t>();
     s.goff = di + o_go;
     s.lds_e = lds_e_max();
-    if (launch_solve(s, nw, need_general, max_lds_e, stream)) return fail(RQ_ERR_DEVICE, "k_solve launch failed");
+    if (launch_solve(s, nw, need_general, wide, max_lds_e, stream)) return fail(RQ_ERR_DEVICE, "k_solve launch failed");
     // 3) apply: x_E = X * s
     ApplyArgs ap;
     ap.blk_map = di + o_map;
