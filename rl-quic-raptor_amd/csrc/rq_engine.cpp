@@ -119,6 +119,7 @@ struct Workspace {
     DevBuf idx[2];
     HostBuf h_idx[2];
     hipEvent_t up[2] = {nullptr, nullptr};
+    DevBuf dstatus;                 // zero-copy descriptors: the solver/apply statuses stay on the device
 
     uint32_t flip = 0;
 };
@@ -610,9 +611,8 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
             for (uint32_t i = eoff[b]; i < eoff[b + 1]; ++i) idx.push_back(erased[i]);
     }
     const size_t o_zr = o_zb + nz;
-    // descriptor upload through pinned staging, queued behind the caller's work on the stream (e.g.
-    // the encode that produced `repair`) without blocking this thread.  (A separate copy stream
-    // joined by events measured 0.25 ms slower per rq_decode_batch_async call, profiles/r02u.)
+    // descriptors through pinned staging, without blocking this thread.  (An upload on a copy stream
+    // of its own, joined by events, measured 0.25 ms slower per rq_decode_batch_async call, r02u.)
     Workspace* w = ctx->wsp(stream);
     const uint32_t set = w->flip++ & 1u;
     if (!w->up[0]) {
@@ -620,14 +620,33 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
             HIP_TRY(hipEventCreateWithFlags(&w->up[i], hipEventDisableTiming));
         }
     }
-    HIP_TRY(hipEventSynchronize(w->up[set]));  // the staging's previous upload has been read
+    // The kernels read the descriptors straight from the pinned staging over PCIe (zero copy): no
+    // H2D copy of ~0.5 MB sits in the stream between the caller's previous work and the solve (the
+    // statuses alone go to the device); `up` then marks the end of the call's kernels.  Measured
+    // 1-2 % faster per step than the in-stream copy (profiles/r02aa; RQHIP_DEC_ZC=0 restores it in
+    // experiments builds).
+    static const bool zero_copy = [] { const char* e = knob("RQHIP_DEC_ZC"); return !(e && e[0] == '0'); }();
+    HIP_TRY(hipEventSynchronize(w->up[set]));  // the staging's previous contents have been read
     if ((rc = w->h_idx[set].ensure(idx.size() * 4)) || (rc = w->h_status.ensure((size_t)n_blocks * 4))) return rc;
-    if (w->idx[set].cap < idx.size() * 4) HIP_TRY(hipStreamSynchronize((hipStream_t)stream));  // realloc: idle
+    if (w->idx[set].cap < idx.size() * 4 || w->dstatus.cap < (size_t)n_blocks * 4)
+        HIP_TRY(hipStreamSynchronize((hipStream_t)stream));  // realloc: idle
     if ((rc = w->idx[set].ensure(idx.size() * 4))) return rc;
     std::memcpy(w->h_idx[set].p, idx.data(), idx.size() * 4);
-    HIP_TRY(hipMemcpyAsync(w->idx[set].p, w->h_idx[set].p, idx.size() * 4, hipMemcpyHostToDevice, (hipStream_t)stream));
-    HIP_TRY(hipEventRecord(w->up[set], (hipStream_t)stream));
-    const uint32_t* di = w->idx[set].as<uint32_t>();
+    const uint32_t* di;
+    int32_t* dst_status;
+    if (zero_copy) {
+        if ((rc = w->dstatus.ensure((size_t)n_blocks * 4))) return rc;
+        di = static_cast<const uint32_t*>(w->h_idx[set].p);
+        dst_status = w->dstatus.as<int32_t>();
+        HIP_TRY(hipMemcpyAsync(dst_status, static_cast<uint32_t*>(w->h_idx[set].p) + o_st, n_blocks * 4, hipMemcpyHostToDevice,
+                               (hipStream_t)stream));
+    } else {
+        HIP_TRY(hipMemcpyAsync(w->idx[set].p, w->h_idx[set].p, idx.size() * 4, hipMemcpyHostToDevice,
+                               (hipStream_t)stream));
+        HIP_TRY(hipEventRecord(w->up[set], (hipStream_t)stream));
+        di = w->idx[set].as<uint32_t>();
+        dst_status = reinterpret_cast<int32_t*>(w->idx[set].as<uint32_t>() + o_st);
+    }
     if ((rc = w->r0.ensure((size_t)n_blocks * uni.size() * T))) return rc;
     if ((rc = w->xb.ensure((size_t)xo * 64))) return rc;
     if ((rc = w->xp.ensure(std::max<size_t>(n_er, 1) * 2))) return rc;
@@ -653,7 +672,7 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     s.xcoef = w->xb.as<uint8_t>();
     s.xoff = di + o_xo;
     s.xpiv = w->xp.as<uint16_t>();
-    s.status = reinterpret_cast<int32_t*>(w->idx[set].as<uint32_t>() + o_st);
+    s.status = dst_status;
     s.gws = w->gws.as<uint8_t>();
     s.goff = di + o_go;
     s.lds_e = lds_e_max();
@@ -685,13 +704,13 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
         HIP_TRY(hipMemcpyAsync(w->h_pack.p, w->pk.p, pack_bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
     }
     if (async) {  // statuses land in the caller's pinned array when the stream gets here
-        HIP_TRY(hipMemcpyAsync(status, w->idx[set].as<uint32_t>() + o_st, n_blocks * 4, hipMemcpyDeviceToHost,
-                               (hipStream_t)stream));
+        HIP_TRY(hipMemcpyAsync(status, dst_status, n_blocks * 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
+        if (zero_copy) HIP_TRY(hipEventRecord(w->up[set], (hipStream_t)stream));
         return RQ_OK;
     }
     int32_t* st = static_cast<int32_t*>(w->h_status.p);
-    HIP_TRY(hipMemcpyAsync(st, w->idx[set].as<uint32_t>() + o_st, n_blocks * 4, hipMemcpyDeviceToHost,
-                           (hipStream_t)stream));
+    HIP_TRY(hipMemcpyAsync(st, dst_status, n_blocks * 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
+    if (zero_copy) HIP_TRY(hipEventRecord(w->up[set], (hipStream_t)stream));
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
     for (uint32_t b : blk_map) status[b] = st[b];
     if (po) {
