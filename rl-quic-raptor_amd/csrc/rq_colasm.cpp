@@ -512,7 +512,7 @@ double colprog_cost(const MProg& mp) {
 }
 
 bool compile_colprog(const Params& p, const uint32_t* esi, uint32_t n_out, const AllocOpts& o, ColIR* ir, MProg* mp,
-                     std::string* err, uint32_t* passes_out) {
+                     std::string* err, uint32_t* passes_out, bool search_waves) {
     double best = 0;
     bool have = false;
     std::vector<uint32_t> cand{0u, 1u, 2u, 3u, 4u, 5u, 6u};
@@ -534,6 +534,27 @@ bool compile_colprog(const Params& p, const uint32_t* esi, uint32_t n_out, const
             if (passes_out) *passes_out = P;
         }
         if (P == 0 && cmp.st.spst == 0) break;  // fits on chip: the single scan is cheapest
+    }
+    if (!have || !search_waves || mp->st.spst) return have;
+    // A program that fits on chip at one wave per SIMD may fit at 2, 4 or 8: another wave on the SIMD
+    // then issues while one waits on memory.  Take the highest residency whose program still needs no
+    // global scratch and at most 1.5x the instructions (measured: K=128 4 waves -24 %, K=256 2 waves
+    // -13 %, K=512 spills at 2 waves and loses, profiles/r02ab).
+    const size_t ins1 = mp->ins.size();
+    static const uint32_t cap[3][3] = {{122, 128, 78}, {58, 64, 39}, {26, 32, 19}};  // VGPR, AGPR, LDS slots
+    for (const auto& c : cap) {
+        AllocOpts w = o;
+        w.n_vgpr = std::min(o.n_vgpr, c[0]);
+        w.n_agpr = std::min(o.n_agpr, c[1]);
+        w.n_lds = std::min(o.n_lds, c[2]);
+        ColIR cir;
+        MProg cmp;
+        std::string e2;
+        const bool ok = esi ? build_colprog(p, esi, n_out, &cir, &e2, 0) : build_colprog_C(p, &cir, &e2, 0);
+        if (!ok || !allocate_colprog(cir, w, &cmp, &e2) || cmp.st.spst || cmp.ins.size() * 2 > ins1 * 3) break;
+        *ir = std::move(cir);
+        *mp = std::move(cmp);
+        if (passes_out) *passes_out = 0;
     }
     return have;
 }

@@ -87,8 +87,11 @@ bool allocate_colprog(const ColIR& ir, const AllocOpts& o, MProg* mp, std::strin
 // choosing the IR schedule (build_colprog's `passes`) that minimises the launch-time model
 // colprog_cost: the demand-driven scan when it needs no global scratch, else the number of Horner
 // passes that best trades the extra VALU work against spill traffic.  *passes_out = the choice.
+// search_waves: a program that fits on chip is re-allocated for 2 / 4 / 8 waves per SIMD while it
+// still needs no global scratch and at most 1.5x the instructions (the engine's choice; the debug
+// entry points keep the caller's register budget).
 bool compile_colprog(const Params& p, const uint32_t* esi, uint32_t n_out, const AllocOpts& o, ColIR* ir, MProg* mp,
-                     std::string* err, uint32_t* passes_out = nullptr);
+                     std::string* err, uint32_t* passes_out = nullptr, bool search_waves = false);
 // Model of one launch's time per 64-column item (units: issue slots): every instruction of the one
 // resident wave per SIMD takes an issue slot, plus a stall term per global-scratch spill / reload;
 // fitted on the K=1024 schedule sweep of round 2 (profiles/r02g).

@@ -352,7 +352,8 @@ int get_col_kernel(DevCtx* ctx, const Params& p, const uint32_t* esi, uint32_t n
             ColIR ir;
             std::string err;
             MProg mp;
-            if (!compile_colprog(p, all_C ? nullptr : esi, n_esi, ao, &ir, &mp, &err)) {
+            const bool search_waves = !knob("RQHIP_ALLOC");  // experiments: the given budget as is
+            if (!compile_colprog(p, all_C ? nullptr : esi, n_esi, ao, &ir, &mp, &err, nullptr, search_waves)) {
                 ctx->colk.erase(key);
                 return fail(RQ_ERR_PLAN, err);
             }
