@@ -205,7 +205,8 @@ def run_config2(args):
                        "verified_blocks_vs_cpu_port": 0 if args.no_verify else 8},
             "roofline": {"bound": "hbm", "kernel": "rq_colprog_K%d_n%d" % (K, R), "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": None, "launch_ms": round(enc_ms, 4)}}), flush=True)
+                         "traffic": None, "launch_ms": round(enc_ms, 4),
+                         "achieved_read_write": round(B * (K + R) * T / (enc_ms * 1e-3) / 1e9, 2)}}), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 
@@ -364,7 +365,9 @@ def main():
             "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "traffic_source": traffic_src, "algorithmic_bytes_per_launch": B * K * T,
-                         "launch_ms": round(enc_ms, 4)},
+                         "launch_ms": round(enc_ms, 4),
+                         # total read + write rate of the launch, (K + R) * T per block
+                         "achieved_read_write": round(B * (K + R) * T / (enc_ms * 1e-3) / 1e9, 2)},
         }
         if args.cpu_sample > 0 and world == 1:
             line["cpu_baseline"] = cpu_baseline(K, T, N, n_erase, args.cpu_sample)

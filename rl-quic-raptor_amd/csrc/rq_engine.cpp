@@ -11,9 +11,11 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -53,7 +55,9 @@ inline uint32_t pad_row(uint32_t T) { return T <= 8 ? 8u : (T + 3) & ~3u; }
         if (e_ != hipSuccess) return fail(RQ_ERR_DEVICE, std::string(#expr ": ") + hipGetErrorString(e_)); \
     } while (0)
 
-// Growable device buffer (allocation happens outside any timed region after warmup).
+// Growable device buffer (allocation happens outside any timed region after warmup).  Growth is
+// geometric: a reallocation frees the old buffer, and hipFree waits for the whole device, so a
+// stream of varying sizes (chunks, shapes) should settle after a few calls.
 struct DevBuf {
     void* p = nullptr;
     size_t cap = 0;
@@ -61,8 +65,8 @@ struct DevBuf {
         if (n <= cap) return RQ_OK;
         if (p) (void)hipFree(p);
         p = nullptr;
+        const size_t want = std::max<size_t>({n, cap + cap / 2, 4096});
         cap = 0;
-        const size_t want = std::max<size_t>(n, 4096);
         if (hipMalloc(&p, want) != hipSuccess) return fail(RQ_ERR_DEVICE, "hipMalloc failed");
         cap = want;
         return RQ_OK;
@@ -96,8 +100,8 @@ struct HostBuf {
         if (n <= cap) return RQ_OK;
         if (p) (void)hipHostFree(p);
         p = nullptr;
+        const size_t want = std::max<size_t>({n, cap + cap / 2, 1 << 16});  // geometric, as DevBuf
         cap = 0;
-        const size_t want = std::max<size_t>(n, 1 << 16);
         if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) return fail(RQ_ERR_DEVICE, "hipHostMalloc failed");
         cap = want;
         return RQ_OK;
@@ -138,7 +142,13 @@ struct DevCtx {
     std::map<std::string, std::unique_ptr<ColKernel>> colk;  // keyed by (K', K, outputs); LRU-bounded
     uint64_t tick = 0;
     std::map<void*, std::unique_ptr<Workspace>> ws;
-    Stage stage[2];
+    static constexpr uint32_t NST = 3;  // host-memory pipeline stages: uploads run two chunks ahead
+    Stage stage[NST];
+    hipEvent_t kdone[NST] = {};  // host-memory paths: a stage's kernels were queued up to here
+    // ... and its upload: the next chunk's upload waits for it, so the uploads run one after another
+    // at the link's full rate instead of sharing it (all chunks' uploads finished together, and the
+    // first chunk's kernels waited for the last upload: profiles/r02ae)
+    hipEvent_t updone[NST] = {};
     hipStream_t obj_stream = nullptr;  // per-object API: its own stream, pinned staging, device buffer
     HostBuf obj_h;
     DevBuf obj_d;
@@ -536,13 +546,44 @@ uint32_t lds_e_max() {
     return v;
 }
 
+// How a decode pass ends: Sync waits and reads the statuses (and packed rows) back; Async leaves the
+// statuses to land in the caller's pinned array; Deferred queues their download into the workspace
+// and returns -- the caller syncs the stream and calls decode_collect.
+enum class Fin { Sync, Async, Deferred };
+
+// Statuses and packed recovered rows of a finished Sync / Deferred pass over blk_map (workspace w).
+// With `sink`, each decoded block's rows go to sink(b, rows) straight from the pinned download
+// instead of being copied into po.
+using RowSink = std::function<void(uint32_t, const uint8_t*)>;
+void decode_collect(const Workspace* w, const std::vector<uint32_t>& blk_map, const std::vector<uint32_t>& eoff,
+                    uint32_t T, int32_t* status, PackOut* po, const RowSink* sink = nullptr) {
+    const int32_t* st = static_cast<const int32_t*>(w->h_status.p);
+    for (uint32_t b : blk_map) status[b] = st[b];
+    if (!po && !sink) return;
+    const uint8_t* rows = static_cast<const uint8_t*>(w->h_pack.p);
+    size_t r = 0;
+    for (uint32_t b : blk_map) {
+        const size_t nb = (size_t)(eoff[b + 1] - eoff[b]) * T;
+        if (status[b] == 1) {
+            if (sink) {
+                (*sink)(b, rows + r);
+            } else {
+                po->blocks.push_back(b);
+                po->rows.insert(po->rows.end(), rows + r, rows + r + nb);
+            }
+        }
+        r += nb;
+    }
+}
+
 // One solve pass over the blocks of `blocks` (each pending; cnt[b] = candidate repairs offered).
 // Caller holds ctx->mu.  Host arrays as in rq_decode_desc.
 int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, void* data, uint64_t data_stride,
                 const std::vector<uint32_t>& eoff, const uint32_t* erased, const std::vector<uint32_t>& roff,
                 const uint32_t* repair_esi, const std::vector<uint32_t>& cnt, const std::vector<uint32_t>& blk_map,
-                const void* repair, int32_t* status, void* stream, PackOut* po, bool async) {
+                const void* repair, int32_t* status, void* stream, PackOut* po, Fin fin) {
     int rc;
+    const bool async = fin == Fin::Async;
     const uint32_t nw = (uint32_t)blk_map.size();
     uint32_t max_e = 0, max_lds_e = 0;
     bool need_general = false;  // some block may reach the general solver (e or candidates > 64)
@@ -709,76 +750,131 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
         if (zero_copy) HIP_TRY(hipEventRecord(w->up[set], (hipStream_t)stream));
         return RQ_OK;
     }
-    int32_t* st = static_cast<int32_t*>(w->h_status.p);
-    HIP_TRY(hipMemcpyAsync(st, dst_status, n_blocks * 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
+    HIP_TRY(hipMemcpyAsync(w->h_status.p, dst_status, n_blocks * 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
     if (zero_copy) HIP_TRY(hipEventRecord(w->up[set], (hipStream_t)stream));
+    if (fin == Fin::Deferred) return RQ_OK;  // decode_collect after the caller's stream sync
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
-    for (uint32_t b : blk_map) status[b] = st[b];
-    if (po) {
-        const uint8_t* rows = static_cast<const uint8_t*>(w->h_pack.p);
-        size_t r = 0;
-        for (uint32_t b : blk_map) {
-            const size_t nb = (size_t)(eoff[b + 1] - eoff[b]) * T;
-            if (status[b] == 1) {
-                po->blocks.push_back(b);
-                po->rows.insert(po->rows.end(), rows + r, rows + r + nb);
-            }
-            r += nb;
-        }
-    }
+    decode_collect(w, blk_map, eoff, T, status, po);
     return RQ_OK;
 }
 
 // Batched syndrome decode.  Caller holds ctx->mu.  Host arrays as in rq_decode_desc.  Sync calls run
 // the subset pass and, for blocks whose subset was rank-deficient, the all-repairs pass (see
 // g_subset_margin); async calls offer every received repair in one pass (no host decision between
-// passes).
-int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, void* data, uint64_t data_stride,
-                  const uint32_t* n_erased, const uint32_t* erased, const uint32_t* n_repair,
-                  const uint32_t* repair_esi, const void* repair, int32_t* status, void* stream,
-                  PackOut* po = nullptr, bool async = false) {
-    std::vector<uint32_t> eoff(n_blocks + 1, 0), roff(n_blocks + 1, 0);
+// passes).  A deferred decode (the host-memory pipeline) is decode_begin now, decode_finish after
+// its stream was synchronised: the subset pass, then the all-repairs pass like a sync call.
+struct DecodeJob {
+    Params p;
+    uint32_t T = 0, n_blocks = 0;
+    void* data = nullptr;
+    uint64_t data_stride = 0;
+    const uint32_t *erased = nullptr, *n_repair = nullptr, *repair_esi = nullptr;
+    const void* repair = nullptr;
+    int32_t* status = nullptr;
+    void* stream = nullptr;
+    std::vector<uint32_t> eoff, roff, blk_map, cnt;
+};
+
+int decode_begin(DevCtx* ctx, DecodeJob* j, const uint32_t* n_erased, PackOut* po, Fin fin) {
+    const uint32_t n_blocks = j->n_blocks;
+    j->eoff.assign(n_blocks + 1, 0);
+    j->roff.assign(n_blocks + 1, 0);
     for (uint32_t b = 0; b < n_blocks; ++b) {
-        eoff[b + 1] = eoff[b] + n_erased[b];
-        roff[b + 1] = roff[b] + n_repair[b];
+        j->eoff[b + 1] = j->eoff[b] + n_erased[b];
+        j->roff[b + 1] = j->roff[b] + j->n_repair[b];
     }
-    std::vector<uint32_t> blk_map, cnt(n_blocks, 0);
+    j->blk_map.clear();
+    j->cnt.assign(n_blocks, 0);
     for (uint32_t b = 0; b < n_blocks; ++b) {
-        const uint32_t e = n_erased[b], nr = n_repair[b];
-        for (uint32_t i = eoff[b]; i < eoff[b + 1]; ++i)
-            if (erased[i] >= p.K) return fail(RQ_ERR_BAD_ARG, "erased ESI >= K");
-        for (uint32_t i = roff[b]; i < roff[b + 1]; ++i)
-            if (repair_esi[i] < p.K) return fail(RQ_ERR_BAD_ARG, "repair ESI < K");
-        if (e > nr) { status[b] = RQ_ERR_NOT_ENOUGH; continue; }  // (K - e) + nr < K held symbols
-        if (e == 0) { status[b] = 1; continue; }
-        status[b] = ST_PENDING;
-        cnt[b] = async ? nr : std::min(nr, e + g_subset_margin);
-        blk_map.push_back(b);
+        const uint32_t e = n_erased[b], nr = j->n_repair[b];
+        for (uint32_t i = j->eoff[b]; i < j->eoff[b + 1]; ++i)
+            if (j->erased[i] >= j->p.K) return fail(RQ_ERR_BAD_ARG, "erased ESI >= K");
+        for (uint32_t i = j->roff[b]; i < j->roff[b + 1]; ++i)
+            if (j->repair_esi[i] < j->p.K) return fail(RQ_ERR_BAD_ARG, "repair ESI < K");
+        if (e > nr) { j->status[b] = RQ_ERR_NOT_ENOUGH; continue; }  // (K - e) + nr < K held symbols
+        if (e == 0) { j->status[b] = 1; continue; }
+        j->status[b] = ST_PENDING;
+        j->cnt[b] = fin == Fin::Async ? nr : std::min(nr, e + g_subset_margin);
+        j->blk_map.push_back(b);
     }
-    if (blk_map.empty()) return RQ_OK;
-    int rc = decode_pass(ctx, p, T, n_blocks, data, data_stride, eoff, erased, roff, repair_esi, cnt, blk_map, repair,
-                         status, stream, po, async);
-    if (rc || async) return rc;
+    if (j->blk_map.empty()) return RQ_OK;
+    return decode_pass(ctx, j->p, j->T, n_blocks, j->data, j->data_stride, j->eoff, j->erased, j->roff, j->repair_esi,
+                       j->cnt, j->blk_map, j->repair, j->status, j->stream, po, fin);
+}
+
+// After a Sync pass (or a Deferred one and a sync of its stream): the all-repairs pass for the
+// blocks whose subset was rank-deficient.
+int decode_finish(DevCtx* ctx, DecodeJob* j, PackOut* po, bool collect, const RowSink* sink = nullptr) {
+    if (j->blk_map.empty()) return RQ_OK;
+    if (collect) decode_collect(ctx->wsp(j->stream), j->blk_map, j->eoff, j->T, j->status, po, sink);
     std::vector<uint32_t> again;
-    for (uint32_t b : blk_map)
-        if (status[b] == 0 && cnt[b] < n_repair[b]) {
-            cnt[b] = n_repair[b];
-            status[b] = ST_PENDING;
+    for (uint32_t b : j->blk_map)
+        if (j->status[b] == 0 && j->cnt[b] < j->n_repair[b]) {
+            j->cnt[b] = j->n_repair[b];
+            j->status[b] = ST_PENDING;
             again.push_back(b);
         }
     if (again.empty()) return RQ_OK;
-    return decode_pass(ctx, p, T, n_blocks, data, data_stride, eoff, erased, roff, repair_esi, cnt, again, repair,
-                       status, stream, po, false);
+    return decode_pass(ctx, j->p, j->T, j->n_blocks, j->data, j->data_stride, j->eoff, j->erased, j->roff,
+                       j->repair_esi, j->cnt, again, j->repair, j->status, j->stream, po, Fin::Sync);
+}
+
+int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, void* data, uint64_t data_stride,
+                  const uint32_t* n_erased, const uint32_t* erased, const uint32_t* n_repair,
+                  const uint32_t* repair_esi, const void* repair, int32_t* status, void* stream,
+                  PackOut* po = nullptr, Fin fin = Fin::Sync) {
+    DecodeJob j;
+    j.p = p; j.T = T; j.n_blocks = n_blocks; j.data = data; j.data_stride = data_stride; j.erased = erased;
+    j.n_repair = n_repair; j.repair_esi = repair_esi; j.repair = repair; j.status = status; j.stream = stream;
+    int rc = decode_begin(ctx, &j, n_erased, po, fin);
+    if (rc || fin == Fin::Async) return rc;
+    return decode_finish(ctx, &j, po, false);
 }
 
 // ---------------- host-memory batches (rq_encode_batch_host / rq_decode_batch_host) ----------------
-// Blocks per pipeline chunk: enough 64-column items to fill every resident wave slot about twice
-// (a chunk is one persistent launch), and at least a quarter of the shard so the H2D of one chunk
-// overlaps the kernels of the other.
-uint32_t chunk_blocks(const DevCtx* ctx, uint32_t T, uint32_t n_blocks) {
-    const uint32_t items_per_block = (T / 4 + 63) / 64;
-    const uint32_t fill = (2 * 4 * ctx->n_cu + items_per_block - 1) / items_per_block;
-    return std::max<uint32_t>(1, std::min(n_blocks, std::max(fill, (n_blocks + 3) / 4)));
+// Blocks per pipeline chunk of the host-memory paths, which are PCIe-bound: about eight chunks, so
+// that every chunk's kernels, download and host scatter hide behind the next chunks' uploads, but
+// each at least twice as long to upload (at ~50 GB/s) as its launches' fixed latency `launch_us`
+// (one round of column-program items, the solver's pivot chain), and at least 16 MiB
+// (profiles/r02ae: one 128 MiB chunk at K=512 T=256 left copies and kernels serial; 16 MiB chunks at
+// K=2048 paid the 0.23 ms solve of e ~ 113 eight times).
+uint64_t g_chunk_min_mib = 32, g_chunks = 4;
+uint32_t chunk_blocks(uint64_t block_bytes, uint32_t n_blocks, double launch_us) {
+#ifdef RQHIP_EXPERIMENTS
+    static const bool once = [] {
+        if (const char* e = knob("RQHIP_CHUNK_MIB")) g_chunk_min_mib = std::strtoull(e, nullptr, 10);
+        if (const char* e = knob("RQHIP_CHUNKS")) g_chunks = std::strtoull(e, nullptr, 10);
+        return true;
+    }();
+    (void)once;
+#endif
+    const uint64_t min_bytes = std::max<uint64_t>(g_chunk_min_mib << 20, (uint64_t)(launch_us * 1e5));
+    const uint64_t min_b = (min_bytes + block_bytes - 1) / std::max<uint64_t>(block_bytes, 1);
+    const uint64_t cb = std::max<uint64_t>((n_blocks + g_chunks - 1) / g_chunks, min_b);
+    return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_blocks, cb));
+}
+
+// Fixed latency of one launch sequence (us), fitted on the K=512 / 2048 traces of profiles/r02ae:
+// a round of column-program items ~0.075 us per source symbol; the decode solve ~2 us per pivot.
+double encode_launch_us(uint32_t K) { return 0.075 * K + 20; }
+double decode_launch_us(uint32_t K, uint32_t max_e) { return 0.075 * K + 2.0 * max_e + 50; }
+
+int ensure_kdone(DevCtx* ctx) {
+    for (hipEvent_t& e : ctx->kdone)
+        if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (hipEvent_t& e : ctx->updone)
+        if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return RQ_OK;
+}
+
+// Orders chunk c's upload on stage stream `s` after chunk c-1's (begin) and marks its end (end).
+int upload_begin(DevCtx* ctx, uint32_t c, hipStream_t s) {
+    if (c > 0) HIP_TRY(hipStreamWaitEvent(s, ctx->updone[(c - 1) % DevCtx::NST], 0));
+    return RQ_OK;
+}
+int upload_end(DevCtx* ctx, uint32_t c, hipStream_t s) {
+    HIP_TRY(hipEventRecord(ctx->updone[c % DevCtx::NST], s));
+    return RQ_OK;
 }
 
 int ensure_stages(DevCtx* ctx) {
@@ -811,27 +907,28 @@ int copy_2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t wid
     return RQ_OK;
 }
 
-// One device's shard [b0, b1) of a host-memory encode: chunk c runs on stage c&1 (H2D source,
+// One device's shard [b0, b1) of a host-memory encode: chunk c runs on stage c % NST (H2D source,
 // column program, D2H repairs); calls on one stream are ordered, so a stage's buffers are reused
-// only after its previous chunk finished.
+// only after its previous chunk finished, and `kdone` keeps the stages' kernels in chunk order.
 int encode_host_shard(int dev, const rq_encode_desc& d, const Params& p, uint32_t b0, uint32_t b1) {
     g_device = dev;
     DevCtx* ctx;
     int rc = get_ctx(&ctx);
     if (rc) return rc;
     std::lock_guard<std::mutex> lk(ctx->mu);
-    if ((rc = ensure_stages(ctx))) return rc;
+    if ((rc = ensure_stages(ctx)) || (rc = ensure_kdone(ctx))) return rc;
     // device rows are padded to Tp = T rounded up to 4 bytes (GF(256) work is bytewise: the pad bytes
     // only ever reach pad bytes)
     const uint32_t T = d.T, Tp = pad_row(T);
     const uint64_t in_b = (uint64_t)d.K * Tp, out_b = (uint64_t)d.n_esi * Tp;
-    const uint32_t cb = chunk_blocks(ctx, Tp, b1 - b0);
+    const uint32_t cb = chunk_blocks(in_b, b1 - b0, encode_launch_us(d.K));
     for (uint32_t c = 0, b = b0; b < b1; ++c, b += cb) {
-        Stage& st = ctx->stage[c & 1];
+        Stage& st = ctx->stage[c % DevCtx::NST];
         const uint32_t nb = std::min(cb, b1 - b);
         if ((rc = st.in.ensure(cb * in_b)) || (rc = st.out.ensure(cb * out_b))) return rc;
         const uint8_t* src = static_cast<const uint8_t*>(d.src) + b * d.src_stride;
         uint8_t* out = static_cast<uint8_t*>(d.out) + b * d.out_stride;
+        if ((rc = upload_begin(ctx, c, st.s))) return rc;
         if (Tp == T) {
             rc = copy_rows(st.in.p, in_b, src, d.src_stride, in_b, nb, hipMemcpyHostToDevice, st.s);
         } else if (d.src_stride == (uint64_t)d.K * T) {
@@ -841,8 +938,12 @@ int encode_host_shard(int dev, const rq_encode_desc& d, const Params& p, uint32_
                 rc = copy_2d(st.in.as<uint8_t>() + i * in_b, Tp, src + i * d.src_stride, T, T, d.K,
                              hipMemcpyHostToDevice, st.s);
         }
+        if (!rc) rc = upload_end(ctx, c, st.s);
+        if (!rc && c > 0) rc = hipStreamWaitEvent(st.s, ctx->kdone[(c - 1) % DevCtx::NST], 0) == hipSuccess ? RQ_OK
+                                  : fail(RQ_ERR_DEVICE, "hipStreamWaitEvent failed");
         if (rc || (rc = encode_locked(ctx, p, Tp, nb, st.in.p, in_b, d.esi, d.n_esi, st.out.p, out_b, st.s)))
             return rc;
+        HIP_TRY(hipEventRecord(ctx->kdone[c % DevCtx::NST], st.s));  // the stages' kernels run in chunk order
         if (Tp == T) {
             rc = copy_rows(out, d.out_stride, st.out.p, out_b, out_b, nb, hipMemcpyDeviceToHost, st.s);
         } else if (d.out_stride == (uint64_t)d.n_esi * T) {
@@ -885,9 +986,9 @@ int upload_runs(uint8_t* dst, const P* src, const uint64_t* bytes, uint32_t n, h
 }
 
 // One device's shard of a host-memory decode.  Per chunk: upload the data blocks and their received
-// repair rows (the next chunk's upload is queued on the other stage before this chunk's decode, so
-// it overlaps the kernels), decode, download only the recovered rows and scatter them into the
-// caller's buffers for the blocks that decoded.
+// repair rows, decode, download only the recovered rows and scatter them into the caller's buffers
+// for the blocks that decoded.  The uploads and kernels of the next NST - 1 chunks are queued on the
+// other stages before a chunk is collected, so the link stays busy while the host scatters.
 int decode_host_shard(int dev, const HostDecode& d, const Params& p, uint32_t b0, uint32_t b1,
                       const std::vector<uint64_t>& eoff, const std::vector<uint64_t>& roff) {
     g_device = dev;
@@ -898,22 +999,39 @@ int decode_host_shard(int dev, const HostDecode& d, const Params& p, uint32_t b0
     if ((rc = ensure_stages(ctx))) return rc;
     const uint32_t T = d.T, Tp = pad_row(T);  // device rows padded (see encode_host_shard)
     const uint64_t blk_b = (uint64_t)d.K * Tp;
-    const uint32_t cb = chunk_blocks(ctx, Tp, b1 - b0);
+    uint32_t max_e = 0;
+    for (uint32_t b = b0; b < b1; ++b) max_e = std::max<uint32_t>(max_e, d.n_erased[b]);
+    const uint32_t cb = chunk_blocks(blk_b, b1 - b0, decode_launch_us(d.K, max_e));
     uint32_t max_rep = 0;
     for (uint32_t b = b0; b < b1; b += cb)
         max_rep = std::max<uint32_t>(max_rep, (uint32_t)(roff[std::min(b1, b + cb)] - roff[b]));
+    // phase timing on stderr (experiments builds, RQHIP_HOST_PROF)
+#ifdef RQHIP_EXPERIMENTS
+    static const bool hprof = knob("RQHIP_HOST_PROF") != nullptr;
+#else
+    constexpr bool hprof = false;
+#endif
+    const auto t_start = std::chrono::steady_clock::now();
+    auto hp = [&](const char* what, uint32_t c) {
+        if (hprof)
+            std::fprintf(stderr, "[hprof]   %s %u %.3f\n", what, c,
+                         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count());
+    };
     auto upload = [&](uint32_t c) -> int {
-        Stage& st = ctx->stage[c & 1];
+        Stage& st = ctx->stage[c % DevCtx::NST];
         const uint32_t b = b0 + c * cb, nb = std::min(cb, b1 - b);
         int r;
         if ((r = st.in.ensure(cb * blk_b)) || (r = st.out.ensure(std::max<size_t>((size_t)max_rep * Tp, 4)))) return r;
+        hp("ensured", c);
+        if ((r = upload_begin(ctx, c, st.s))) return r;
         if (Tp == T) {
             std::vector<uint64_t> db(nb, blk_b), rb(nb);
             for (uint32_t i = 0; i < nb; ++i) rb[i] = (uint64_t)d.n_repair[b + i] * T;
-            if ((r = upload_runs(st.in.as<uint8_t>(), d.data.data() + b, db.data(), nb, st.s)) ||
-                (r = upload_runs(st.out.as<uint8_t>(), d.rep.data() + b, rb.data(), nb, st.s)))
-                return r;
-            return RQ_OK;
+            if ((r = upload_runs(st.in.as<uint8_t>(), d.data.data() + b, db.data(), nb, st.s))) return r;
+            hp("data queued", c);
+            if ((r = upload_runs(st.out.as<uint8_t>(), d.rep.data() + b, rb.data(), nb, st.s))) return r;
+            hp("repairs queued", c);
+            return upload_end(ctx, c, st.s);
         }
         uint8_t* rd = st.out.as<uint8_t>();
         for (uint32_t i = 0; i < nb; ++i) {
@@ -923,24 +1041,74 @@ int decode_host_shard(int dev, const HostDecode& d, const Params& p, uint32_t b0
                 return r;
             rd += (size_t)d.n_repair[b + i] * Tp;
         }
-        return RQ_OK;
+        return upload_end(ctx, c, st.s);
     };
     const uint32_t n_chunks = (b1 - b0 + cb - 1) / cb;
-    if ((rc = upload(0))) return rc;
-    for (uint32_t c = 0; c < n_chunks; ++c) {
-        if (c + 1 < n_chunks && (rc = upload(c + 1))) return rc;
-        Stage& st = ctx->stage[c & 1];
+    // chunk c+1 is uploaded and its kernels queued before chunk c's statuses and rows are collected
+    // and scattered on the host (kernels of the two stages run in order: `kdone`), so the download,
+    // the scatter and the next chunk's descriptor work overlap the device instead of idling it
+    DecodeJob job[DevCtx::NST];
+    PackOut po[DevCtx::NST];
+    auto issue = [&](uint32_t c) -> int {
+        Stage& st = ctx->stage[c % DevCtx::NST];
         const uint32_t b = b0 + c * cb, nb = std::min(cb, b1 - b);
-        PackOut po;
-        if ((rc = decode_locked(ctx, p, Tp, nb, st.in.p, blk_b, d.n_erased + b, d.erased + eoff[b], d.n_repair + b,
-                                d.repair_esi + roff[b], st.out.p, d.status + b, st.s, &po)))
-            return rc;
-        size_t r = 0;  // po holds the recovered rows (Tp apart) of the blocks that decoded
-        for (uint32_t lb : po.blocks) {
+        if (c > 0) HIP_TRY(hipStreamWaitEvent(st.s, ctx->kdone[(c - 1) % DevCtx::NST], 0));
+        DecodeJob& j = job[c % DevCtx::NST];
+        j = DecodeJob();
+        j.p = p; j.T = Tp; j.n_blocks = nb; j.data = st.in.p; j.data_stride = blk_b; j.erased = d.erased + eoff[b];
+        j.n_repair = d.n_repair + b; j.repair_esi = d.repair_esi + roff[b]; j.repair = st.out.p;
+        j.status = d.status + b; j.stream = st.s;
+        po[c % DevCtx::NST] = PackOut();
+        int r = decode_begin(ctx, &j, d.n_erased + b, &po[c % DevCtx::NST], Fin::Deferred);
+        if (!r) HIP_TRY(hipEventRecord(ctx->kdone[c % DevCtx::NST], st.s));
+        return r;
+    };
+    auto finish = [&](uint32_t c) -> int {
+        Stage& st = ctx->stage[c % DevCtx::NST];
+        const uint32_t b = b0 + c * cb;
+        HIP_TRY(hipStreamSynchronize(st.s));
+        // the first pass's rows are scattered from the pinned download; a rank-deficient retry's
+        // (rare) arrive in po
+        const RowSink sink = [&](uint32_t lb, const uint8_t* rows) {
             const uint32_t gb = b + lb;
-            for (uint64_t i = eoff[gb]; i < eoff[gb + 1]; ++i, ++r)
-                std::memcpy(d.data[gb] + (uint64_t)d.erased[i] * T, po.rows.data() + r * Tp, T);
+            for (uint64_t i = eoff[gb]; i < eoff[gb + 1]; ++i, rows += Tp)
+                std::memcpy(d.data[gb] + (uint64_t)d.erased[i] * T, rows, T);
+        };
+        int r = decode_finish(ctx, &job[c % DevCtx::NST], &po[c % DevCtx::NST], true, &sink);
+        if (r) return r;
+        size_t k = 0;  // po holds the retry's recovered rows (Tp apart) of the blocks that decoded
+        const PackOut& o = po[c % DevCtx::NST];
+        for (uint32_t lb : o.blocks) {
+            const uint32_t gb = b + lb;
+            for (uint64_t i = eoff[gb]; i < eoff[gb + 1]; ++i, ++k)
+                std::memcpy(d.data[gb] + (uint64_t)d.erased[i] * T, o.rows.data() + k * Tp, T);
         }
+        return RQ_OK;
+    };
+    constexpr uint32_t AHEAD = DevCtx::NST - 1;  // chunks queued beyond the one being collected
+    auto timed = [&](const char* what, uint32_t c, auto&& fn) {
+        if (!hprof) return fn(c);
+        auto ms = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count(); };
+        const double t0 = ms();
+        const int r = fn(c);
+        std::fprintf(stderr, "[hprof] %s %u %.3f-%.3f\n", what, c, t0, ms());
+        return r;
+    };
+    auto run_upload = [&](uint32_t c) { return timed("upload", c, upload); };
+    auto run_issue = [&](uint32_t c) { return timed("issue", c, issue); };
+    auto run_finish = [&](uint32_t c) { return timed("finish", c, finish); };
+    if ((rc = ensure_kdone(ctx))) return rc;
+    for (uint32_t c = 0; c < std::min(AHEAD, n_chunks); ++c)
+        if ((rc = run_upload(c)) || (rc = run_issue(c))) {
+            for (Stage& st : ctx->stage) (void)hipStreamSynchronize(st.s);  // no queued work behind the error
+            return rc;
+        }
+    for (uint32_t c = 0; c < n_chunks; ++c) {
+        if (c + AHEAD < n_chunks && ((rc = run_upload(c + AHEAD)) || (rc = run_issue(c + AHEAD)))) {
+            for (Stage& st : ctx->stage) (void)hipStreamSynchronize(st.s);
+            return rc;
+        }
+        if ((rc = run_finish(c))) return rc;
     }
     return RQ_OK;
 }
@@ -1228,7 +1396,7 @@ int rq_decode_batch_async(const rq_decode_desc* d) {
     if ((rc = get_ctx(&ctx))) return rc;
     std::lock_guard<std::mutex> lk(ctx->mu);
     return decode_locked(ctx, p, d->T, d->n_blocks, d->data, d->data_stride, d->n_erased, d->erased, d->n_repair,
-                         d->repair_esi, d->repair, d->status, d->stream, nullptr, true);
+                         d->repair_esi, d->repair, d->status, d->stream, nullptr, Fin::Async);
 }
 
 int rq_encode_batch_host(const rq_encode_desc* d, uint32_t device_mask) {
