@@ -21,6 +21,7 @@ collectives are the timing barrier and the max-over-ranks reduction (rqshard.max
 """
 import argparse
 import json
+import re
 import os
 import sys
 import time
@@ -74,7 +75,10 @@ def erasure_pattern(K, N, n_blocks, n_erase, seed):
 def pmc_traffic(kernel, K, T, N, B):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary of this exact
     workload (profiles/rNN_traffic.json, written by tools/gpu_profile.sh); (None, None) if absent."""
-    for path in sorted((ROOT / "profiles").glob("r*_traffic.json"), reverse=True):
+    def tag_order(path):  # r02y < r02z < r02aa < r02af: round, then the length and letters of the tag
+        m = re.match(r"r(\d+)([a-z]*)_traffic\.json$", path.name)
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
+    for path in sorted((ROOT / "profiles").glob("r*_traffic.json"), key=tag_order, reverse=True):
         t = json.loads(path.read_text())
         if t.get("kernel") == kernel and t.get("workload") == {"K": K, "T": T, "N": N, "blocks": B}:
             return t["traffic_bytes"], path.name
