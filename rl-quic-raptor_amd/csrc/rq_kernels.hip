@@ -272,6 +272,133 @@ __device__ __forceinline__ void perm_tables(uint32_t c, uint4* A, uint32_t* B) {
     *B = pack(0, m[6], m[7], m[6] ^ m[7]);
 }
 
+// c * x on four bytes with c's perm_tables: three v_perm lookups (3 + 3 + 2 bits of each byte).
+__device__ __forceinline__ uint32_t perm_mul(const uint4& A, uint32_t B, uint32_t x) {
+    const uint32_t s0 = x & 0x07070707u, s1 = (x >> 3) & 0x07070707u, s2 = (x >> 6) & 0x03030303u;
+    return xor3(__builtin_amdgcn_perm(A.y, A.x, s0), __builtin_amdgcn_perm(A.w, A.z, s1),
+                __builtin_amdgcn_perm(B, B, s2));
+}
+
+// k_solve_fast's layout (four waves, RPL rows per lane as LDS rows, wave g on the quads g, g+4, ...)
+// with the elimination done by GF(256) multiplication instead of alpha-multiple tables: each lane
+// turns its coefficient c_j = f_j / f_p into v_perm tables (perm_tables) and folds c_j times the
+// pivot row into its row, the pivot row's dwords read once per quad (one broadcast b128) and made
+// scalar, so the lookups' selectors are SGPRs.  The pivot lane uses c = 1 ^ 1/f_p, which leaves
+// row_p / f_p (each wave reads the pivot quad before its pivot lane rewrites it).  One barrier per
+// step (the alpha-multiple tables, their byte stores and the second barrier are gone) and an eighth
+// of the LDS reads.
+template <int RPL, int NW>
+__global__ void __launch_bounds__(64 * NW) k_solve_pm(SolveArgs a) {
+    constexpr uint32_t NT = 64 * NW;
+    constexpr uint32_t NROWS = 64 * RPL, SW = 32 * RPL + 4;  // rows, row stride (dwords)
+    __shared__ __attribute__((aligned(16))) uint32_t rows[NROWS * SW];
+    __shared__ uint8_t ex[512], lg[256];
+    __shared__ uint8_t pivl[NROWS];
+    __shared__ uint32_t Es[NROWS];
+    const uint32_t b = a.blk_map[blockIdx.x];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
+    if (RPL > 1 && a.status[b] != ST_FALLBACK) return;  // the wide pass takes deferred blocks only
+    const uint32_t e = a.erased_off[b + 1] - a.erased_off[b];
+    const uint32_t nr = a.rep_cnt[b];
+    if (e > NROWS) {
+        if (tid == 0) a.status[b] = ST_FALLBACK;
+        return;
+    }
+    const uint32_t nrow = min(nr, NROWS);
+    const uint32_t* E = a.erased + a.erased_off[b];
+    const uint32_t* U = a.rep_uidx + a.rep_off[b];
+    for (uint32_t i = tid; i < e; i += NT) Es[i] = E[i];
+    gf_tables_copy(ex, lg);
+    for (uint32_t i = tid; i < NROWS * SW; i += NT) rows[i] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < RPL; ++q) {
+        const uint32_t row = lane + 64 * q;
+        if (row < nrow) {  // row gather: wave g takes columns g, g+4, ...
+            uint8_t* myb = reinterpret_cast<uint8_t*>(rows + row * SW);
+            const uint8_t* mr = a.mrep + (size_t)U[row] * a.mrep_stride;
+            for (uint32_t k = g; k < e; k += NW) myb[k] = mr[Es[k]];
+            if (g == 0) myb[e + row] = 1;
+        }
+    }
+    __syncthreads();
+    const uint32_t q1 = (e + nrow + 15) >> 4;  // quads holding live columns
+    bool used[RPL];
+#pragma unroll
+    for (int q = 0; q < RPL; ++q) used[q] = lane + 64 * q >= nrow;
+    const uint8_t* rb = reinterpret_cast<const uint8_t*>(rows);
+    for (uint32_t k = 0; k < e; ++k) {
+        uint32_t f[RPL];
+        uint32_t p = 0xFFFFFFFFu;
+#pragma unroll
+        for (int q = RPL - 1; q >= 0; --q) {
+            f[q] = (rows[(lane + 64 * q) * SW + (k >> 2)] >> ((k & 3) * 8)) & 0xFFu;
+            const uint64_t bal = __ballot(f[q] != 0 && !used[q]);
+            if (bal) p = 64 * q + (uint32_t)__ffsll((unsigned long long)bal) - 1;
+        }
+        if (p == 0xFFFFFFFFu) {  // uniform over the block: every wave saw the same rows
+            if (tid == 0) a.status[b] = (nr > nrow) ? ST_FALLBACK : 0;
+            return;
+        }
+#pragma unroll
+        for (int q = 0; q < RPL; ++q)
+            if (lane + 64 * q == p) used[q] = true;
+        if (tid == 0) pivl[k] = (uint8_t)p;
+        // f_p from the pivot lane's register (no LDS round trip); lg[f] issued beside lg[f_p]
+        uint32_t fp = 0;
+#pragma unroll
+        for (int q = 0; q < RPL; ++q)
+            if ((p >> 6) == (uint32_t)q) fp = __builtin_amdgcn_readlane(f[q], p & 63);
+        const uint32_t lgp = lg[fp];
+        const uint32_t inv = ex[255u - lgp];
+        uint4 A[RPL];
+        uint32_t B[RPL];
+        bool act[RPL];
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+            uint32_t c = 0;
+            if (lane + 64 * q == p) {
+                c = 1u ^ inv;
+            } else if (f[q]) {
+                uint32_t t = lg[f[q]] + 255u - lgp;
+                t = t >= 255u ? t - 255u : t;
+                c = ex[t];
+            }
+            act[q] = c != 0;
+            perm_tables(c, &A[q], &B[q]);
+        }
+        // columns < k are zero in the pivot row (all are earlier pivot columns): start at quad k/16
+        const uint4* prow = reinterpret_cast<const uint4*>(rows + p * SW);
+        for (uint32_t w = (k >> 4) + g; w < q1; w += NW) {
+            const uint4 P = prow[w];
+            const uint32_t px = __builtin_amdgcn_readfirstlane(P.x), py = __builtin_amdgcn_readfirstlane(P.y);
+            const uint32_t pz = __builtin_amdgcn_readfirstlane(P.z), pw = __builtin_amdgcn_readfirstlane(P.w);
+#pragma unroll
+            for (int q = 0; q < RPL; ++q) {
+                if (!act[q]) continue;
+                uint4* my4 = reinterpret_cast<uint4*>(rows + (lane + 64 * q) * SW);
+                uint4 r = my4[w];
+                r.x ^= perm_mul(A[q], B[q], px);
+                r.y ^= perm_mul(A[q], B[q], py);
+                r.z ^= perm_mul(A[q], B[q], pz);
+                r.w ^= perm_mul(A[q], B[q], pw);
+                my4[w] = r;
+            }
+        }
+        __syncthreads();
+    }
+    // X[k][m] = identity byte (e + piv_m) of pivot row piv_k
+    uint8_t* xc = a.xcoef + 64ull * a.xoff[blockIdx.x];
+    const uint32_t xs = x_stride(e);
+    uint16_t* XP = a.xpiv + a.erased_off[b];
+    for (uint32_t m = tid; m < e; m += NT) XP[m] = pivl[m];
+    for (uint32_t idx = tid; idx < e * e; idx += NT) {
+        const uint32_t m = idx / e, k = idx - m * e;
+        xc[m * xs + k] = rb[pivl[k] * SW * 4 + e + pivl[m]];
+    }
+    if (tid == 0) a.status[b] = 1;
+}
+
 // One wave per block for e <= 64 on the first <= 64 received repairs, the rows held in registers:
 // lane j owns received repair j as 32 dwords (e coefficient bytes, then the identity part at byte
 // e + j).  Each step k takes the lowest unused row with a nonzero coefficient in column k (ballot),
@@ -279,12 +406,6 @@ __device__ __forceinline__ void perm_tables(uint32_t c, uint4* A, uint32_t* B) {
 // selectors are scalar) scaled by its own coefficient c_j = f_j / f_p into its row -- one GF(256)
 // multiply per dword as three v_perm lookups against per-lane tables of c_j (perm_tables).  The
 // pivot lane uses c = 1 ^ 1/f_p, which leaves row_p / f_p.  No barrier inside the elimination.
-__device__ __forceinline__ uint32_t perm_mul(const uint4& A, uint32_t B, uint32_t x) {
-    const uint32_t s0 = x & 0x07070707u, s1 = (x >> 3) & 0x07070707u, s2 = (x >> 6) & 0x03030303u;
-    return xor3(__builtin_amdgcn_perm(A.y, A.x, s0), __builtin_amdgcn_perm(A.w, A.z, s1),
-                __builtin_amdgcn_perm(B, B, s2));
-}
-
 __global__ void __launch_bounds__(64) k_solve_reg(SolveArgs a) {
     __shared__ uint8_t ex[512], lg[256];
     __shared__ uint8_t pivl[64];
@@ -463,6 +584,19 @@ size_t solve_ws_bytes(uint32_t e) {
 // The e <= 64 solver: k_solve_fast<1> with four waves per block; experiments builds select one wave
 // (RQHIP_SOLVE_NW=1) or the register-resident k_solve_reg (RQHIP_SOLVE_NW=0; measured 111 us against
 // 94 us for the four-wave solver at 1 024 blocks, e = 55: profiles/r02r).
+// Elimination by GF(256) multiplication (k_solve_pm, the default) or by alpha-multiple tables
+// (k_solve_fast: RQHIP_SOLVE_PM=0 in experiments builds).  Measured at 1 024 blocks K=1024, e ~ 52:
+// decode 0.810 against 0.820 ms per step; the e ~ 113 wide pass at K=2048: 192 against 237 us
+// (profiles/r02ag).
+static bool solve_pm() {
+#ifdef RQHIP_EXPERIMENTS
+    static const bool on = [] { const char* e = std::getenv("RQHIP_SOLVE_PM"); return !(e && e[0] == '0'); }();
+    return on;
+#else
+    return true;
+#endif
+}
+
 static int solve_nw() {
 #ifdef RQHIP_EXPERIMENTS
     static const int nw = [] {
@@ -479,13 +613,17 @@ int launch_solve(const SolveArgs& a, uint32_t n_blocks, bool need_general, bool 
                  void* stream) {
     switch (solve_nw()) {
         case 1: hipLaunchKernelGGL((k_solve_fast<1, 1>), dim3(n_blocks), dim3(64), 0, (hipStream_t)stream, a); break;
-        case 4: hipLaunchKernelGGL((k_solve_fast<1, 4>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a); break;
+        case 4:
+            if (solve_pm()) hipLaunchKernelGGL((k_solve_pm<1, 4>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a);
+            else hipLaunchKernelGGL((k_solve_fast<1, 4>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a);
+            break;
         default: hipLaunchKernelGGL(k_solve_reg, dim3(n_blocks), dim3(64), 0, (hipStream_t)stream, a); break;
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !need_general) return (int)e;
     if (wide) {  // blocks with 64 < e <= 128; the rare rank-deficient-on-64-rows block goes to k_solve
-        hipLaunchKernelGGL((k_solve_fast<2, 4>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a);
+        if (solve_pm()) hipLaunchKernelGGL((k_solve_pm<2, 4>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a);
+        else hipLaunchKernelGGL((k_solve_fast<2, 4>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a);
         if ((e = hipGetLastError()) != hipSuccess) return (int)e;
     }
     static bool attr = false;
