@@ -175,3 +175,37 @@ def test_host_batch_virtual_shards(gpu, rq):
         assert (st == 1).all() and np.array_equal(data, src)
     finally:
         rq.lib().rq_debug_virtual_shards(old)
+
+
+def test_host_decode_forced_retry_multi_chunk(gpu, rq):
+    """Host-memory decode over several pipeline chunks (1 000 blocks of 76.8 KB) with the subset
+    margin forced to 0: each block's first pass solves on exactly e repairs, so some are rank-
+    deficient and take the all-repairs pass inside the chunk's collect step (after the first pass's
+    rows were scattered).  Every block decodes to its source, with the device batch's statuses."""
+    K, T, N, nb, n_erase = 64, 1200, 80, 1000, 8
+    esis = list(range(K, N))
+    rng = np.random.default_rng(31)
+    src = rng.integers(0, 256, (nb, K * T), dtype=np.uint8)
+    rep_all = _device_encode(rq, gpu, src, K, T, esis).reshape(nb, N - K, T)
+    er, rl = [], []
+    for b in range(nb):
+        lost = set(rng.choice(N, n_erase, replace=False).tolist())
+        er.append(sorted(i for i in lost if i < K))
+        rl.append([e for e in esis if e not in lost])
+    repair = torch.from_numpy(np.stack([rep_all[b, e - K] for b in range(nb) for e in rl[b]])).pin_memory()
+    data = torch.from_numpy(src.copy()).pin_memory()
+    d3 = data.numpy().reshape(nb, K, T)
+    for b in range(nb):
+        d3[b, er[b]] = 0x3C
+    before = data.numpy().copy()
+    old = rq.lib().rq_debug_decode_margin(0)
+    try:
+        st = rq.decode_batch_host(rq.DecodeBatch(K, T, er, rl), data, repair).copy()
+        dd = torch.from_numpy(before).to(gpu)
+        st2 = rq.DecodeBatch(K, T, er, rl).run(dd, repair.to(gpu))
+        torch.cuda.synchronize()
+    finally:
+        rq.lib().rq_debug_decode_margin(old)
+    assert (st == 1).all() and np.array_equal(st, st2)
+    assert np.array_equal(data.numpy(), src)
+    assert np.array_equal(dd.cpu().numpy(), src)
