@@ -59,6 +59,10 @@ struct SolveArgs {
     uint8_t* gws;               // general solver: basis of block bi at gws + 64 * goff[bi] when e > lds_e
     const uint32_t* goff;
     uint32_t lds_e;             // largest e whose basis the general solver keeps in LDS
+    // host-decided statuses of all n_all blocks (ST_PENDING for the solver's blocks), read by the
+    // first solver launch in place of an upload (nullptr: status already holds them)
+    const int32_t* status_init;
+    uint32_t n_all;
 };
 constexpr int32_t ST_PENDING = -100;   // queued for the solver
 constexpr int32_t ST_FALLBACK = -101;  // beyond the fast solvers: the general solver decides

@@ -658,8 +658,9 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     Workspace* w = ctx->wsp(stream);
     const uint32_t set = w->flip++ & 1u;
     if (!w->up[0]) {
-        for (int i = 0; i < 2; ++i) {
-            HIP_TRY(hipEventCreateWithFlags(&w->up[i], hipEventDisableTiming));
+        for (int i = 0; i < 2; ++i) {  // only says the device finished reading the pinned staging:
+            // no system-scope release (cache writeback) needed
+            HIP_TRY(hipEventCreateWithFlags(&w->up[i], hipEventDisableTiming | hipEventDisableSystemFence));
         }
     }
     // The kernels read the descriptors straight from the pinned staging over PCIe (zero copy): no
@@ -679,9 +680,7 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     if (zero_copy) {
         if ((rc = w->dstatus.ensure((size_t)n_blocks * 4))) return rc;
         di = static_cast<const uint32_t*>(w->h_idx[set].p);
-        dst_status = w->dstatus.as<int32_t>();
-        HIP_TRY(hipMemcpyAsync(dst_status, static_cast<uint32_t*>(w->h_idx[set].p) + o_st, n_blocks * 4, hipMemcpyHostToDevice,
-                               (hipStream_t)stream));
+        dst_status = w->dstatus.as<int32_t>();  // the host-decided statuses: copied by the first solver
     } else {
         HIP_TRY(hipMemcpyAsync(w->idx[set].p, w->h_idx[set].p, idx.size() * 4, hipMemcpyHostToDevice,
                                (hipStream_t)stream));
@@ -718,6 +717,8 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     s.gws = w->gws.as<uint8_t>();
     s.goff = di + o_go;
     s.lds_e = lds_e_max();
+    s.status_init = zero_copy ? reinterpret_cast<const int32_t*>(di + o_st) : nullptr;
+    s.n_all = n_blocks;
     if (launch_solve(s, nw, need_general, wide, max_lds_e, stream)) return fail(RQ_ERR_DEVICE, "k_solve launch failed");
     // 3) apply: x_E = X * s
     ApplyArgs ap;
@@ -743,15 +744,16 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
         if ((rc = w->pk.ensure(pack_bytes)) || (rc = w->h_pack.ensure(pack_bytes))) return rc;
         z.pack = w->pk.as<uint8_t>();
         if (launch_pack_rows(z, stream)) return fail(RQ_ERR_DEVICE, "k_pack_rows launch failed");
-        HIP_TRY(hipMemcpyAsync(w->h_pack.p, w->pk.p, pack_bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
     }
+    // the last kernel that reads the staging is queued: `up` (no fence) before the downloads, so the
+    // stream's last command stays a copy whose completion makes its bytes visible to the host
+    if (zero_copy) HIP_TRY(hipEventRecord(w->up[set], (hipStream_t)stream));
+    if (po) HIP_TRY(hipMemcpyAsync(w->h_pack.p, w->pk.p, pack_bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
     if (async) {  // statuses land in the caller's pinned array when the stream gets here
         HIP_TRY(hipMemcpyAsync(status, dst_status, n_blocks * 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
-        if (zero_copy) HIP_TRY(hipEventRecord(w->up[set], (hipStream_t)stream));
         return RQ_OK;
     }
     HIP_TRY(hipMemcpyAsync(w->h_status.p, dst_status, n_blocks * 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
-    if (zero_copy) HIP_TRY(hipEventRecord(w->up[set], (hipStream_t)stream));
     if (fin == Fin::Deferred) return RQ_OK;  // decode_collect after the caller's stream sync
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
     decode_collect(w, blk_map, eoff, T, status, po);

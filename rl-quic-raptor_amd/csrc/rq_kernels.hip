@@ -297,6 +297,9 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pm(SolveArgs a) {
     __shared__ uint32_t Es[NROWS];
     const uint32_t b = a.blk_map[blockIdx.x];
     const uint32_t tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
+    if (a.status_init)  // the host-decided statuses (disjoint from the solver's blocks, ST_PENDING)
+        for (uint32_t i = blockIdx.x * NT + tid; i < a.n_all; i += gridDim.x * NT)
+            if (a.status_init[i] != ST_PENDING) a.status[i] = a.status_init[i];
     if (RPL > 1 && a.status[b] != ST_FALLBACK) return;  // the wide pass takes deferred blocks only
     const uint32_t e = a.erased_off[b + 1] - a.erased_off[b];
     const uint32_t nr = a.rep_cnt[b];
@@ -609,12 +612,20 @@ static int solve_nw() {
 #endif
 }
 
-int launch_solve(const SolveArgs& a, uint32_t n_blocks, bool need_general, bool wide, uint32_t max_lds_e,
+int launch_solve(const SolveArgs& a_in, uint32_t n_blocks, bool need_general, bool wide, uint32_t max_lds_e,
                  void* stream) {
+    // the first k_solve_pm launch copies the host-decided statuses (a_in.status_init); the other
+    // solvers get them uploaded first, and later launches never copy
+    SolveArgs a = a_in;
+    a.status_init = nullptr;
+    if (a_in.status_init && !(solve_pm() && solve_nw() == 4) &&
+        hipMemcpyAsync(a.status, a_in.status_init, (size_t)a_in.n_all * 4, hipMemcpyHostToDevice,
+                       (hipStream_t)stream) != hipSuccess)
+        return (int)hipGetLastError();
     switch (solve_nw()) {
         case 1: hipLaunchKernelGGL((k_solve_fast<1, 1>), dim3(n_blocks), dim3(64), 0, (hipStream_t)stream, a); break;
         case 4:
-            if (solve_pm()) hipLaunchKernelGGL((k_solve_pm<1, 4>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a);
+            if (solve_pm()) hipLaunchKernelGGL((k_solve_pm<1, 4>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a_in);
             else hipLaunchKernelGGL((k_solve_fast<1, 4>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a);
             break;
         default: hipLaunchKernelGGL(k_solve_reg, dim3(n_blocks), dim3(64), 0, (hipStream_t)stream, a); break;
