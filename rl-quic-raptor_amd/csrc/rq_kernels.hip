@@ -287,7 +287,7 @@ __device__ __forceinline__ uint32_t perm_mul(const uint4& A, uint32_t B, uint32_
 // row_p / f_p (each wave reads the pivot quad before its pivot lane rewrites it).  One barrier per
 // step (the alpha-multiple tables, their byte stores and the second barrier are gone) and an eighth
 // of the LDS reads.
-template <int RPL, int NW>
+template <int RPL, int NW, bool LUT>
 __global__ void __launch_bounds__(64 * NW) k_solve_pm(SolveArgs a) {
     constexpr uint32_t NT = 64 * NW;
     constexpr uint32_t NROWS = 64 * RPL, SW = 32 * RPL + 4;  // rows, row stride (dwords)
@@ -295,6 +295,9 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pm(SolveArgs a) {
     __shared__ uint8_t ex[512], lg[256];
     __shared__ uint8_t pivl[NROWS];
     __shared__ uint32_t Es[NROWS];
+    // LUT: the v_perm tables of every nonzero coefficient, indexed by its log (built once per block)
+    __shared__ __attribute__((aligned(16))) uint4 tlA[LUT ? 255 : 1];
+    __shared__ uint32_t tlB[LUT ? 255 : 1];
     const uint32_t b = a.blk_map[blockIdx.x];
     const uint32_t tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
     if (a.status_init)  // the host-decided statuses (disjoint from the solver's blocks, ST_PENDING)
@@ -312,6 +315,8 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pm(SolveArgs a) {
     const uint32_t* U = a.rep_uidx + a.rep_off[b];
     for (uint32_t i = tid; i < e; i += NT) Es[i] = E[i];
     gf_tables_copy(ex, lg);
+    if (LUT)
+        for (uint32_t l = tid; l < 255; l += NT) perm_tables(kGf.ex[l], &tlA[l], &tlB[l]);
     for (uint32_t i = tid; i < NROWS * SW; i += NT) rows[i] = 0;
     __syncthreads();
 #pragma unroll
@@ -357,18 +362,37 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pm(SolveArgs a) {
         uint4 A[RPL];
         uint32_t B[RPL];
         bool act[RPL];
+        if (LUT) {
+            const uint32_t cp = 1u ^ inv;                      // the pivot lane's coefficient
+            const uint32_t lcp = cp ? (uint32_t)lg[cp] : 0u;
 #pragma unroll
-        for (int q = 0; q < RPL; ++q) {
-            uint32_t c = 0;
-            if (lane + 64 * q == p) {
-                c = 1u ^ inv;
-            } else if (f[q]) {
-                uint32_t t = lg[f[q]] + 255u - lgp;
-                t = t >= 255u ? t - 255u : t;
-                c = ex[t];
+            for (int q = 0; q < RPL; ++q) {
+                uint32_t l = 0;
+                if (lane + 64 * q == p) {
+                    act[q] = cp != 0;
+                    l = lcp;
+                } else {
+                    act[q] = f[q] != 0;
+                    l = lg[f[q]] + 255u - lgp;
+                    l = l >= 255u ? l - 255u : l;
+                }
+                A[q] = tlA[act[q] ? l : 0];
+                B[q] = tlB[act[q] ? l : 0];
             }
-            act[q] = c != 0;
-            perm_tables(c, &A[q], &B[q]);
+        } else {
+#pragma unroll
+            for (int q = 0; q < RPL; ++q) {
+                uint32_t c = 0;
+                if (lane + 64 * q == p) {
+                    c = 1u ^ inv;
+                } else if (f[q]) {
+                    uint32_t t = lg[f[q]] + 255u - lgp;
+                    t = t >= 255u ? t - 255u : t;
+                    c = ex[t];
+                }
+                act[q] = c != 0;
+                perm_tables(c, &A[q], &B[q]);
+            }
         }
         // columns < k are zero in the pivot row (all are earlier pivot columns): start at quad k/16
         const uint4* prow = reinterpret_cast<const uint4*>(rows + p * SW);
@@ -600,6 +624,19 @@ static bool solve_pm() {
 #endif
 }
 
+// k_solve_pm's coefficient tables from a per-block log-indexed LUT (the default; RQHIP_SOLVE_LUT=0 in
+// experiments builds builds them per step): the solve is VALU-bound at four blocks per CU, and the
+// per-step perm_tables were ~40 VALU per lane.  Decode 0.806 -> 0.790 ms, wide pass 194 -> 182 us
+// (profiles/r02ag/lut).
+static bool solve_lut() {
+#ifdef RQHIP_EXPERIMENTS
+    static const bool on = [] { const char* e = std::getenv("RQHIP_SOLVE_LUT"); return !(e && e[0] == '0'); }();
+    return on;
+#else
+    return true;
+#endif
+}
+
 static int solve_nw() {
 #ifdef RQHIP_EXPERIMENTS
     static const int nw = [] {
@@ -625,7 +662,10 @@ int launch_solve(const SolveArgs& a_in, uint32_t n_blocks, bool need_general, bo
     switch (solve_nw()) {
         case 1: hipLaunchKernelGGL((k_solve_fast<1, 1>), dim3(n_blocks), dim3(64), 0, (hipStream_t)stream, a); break;
         case 4:
-            if (solve_pm()) hipLaunchKernelGGL((k_solve_pm<1, 4>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a_in);
+            if (solve_pm() && solve_lut())
+                hipLaunchKernelGGL((k_solve_pm<1, 4, true>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a_in);
+            else if (solve_pm())
+                hipLaunchKernelGGL((k_solve_pm<1, 4, false>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a_in);
             else hipLaunchKernelGGL((k_solve_fast<1, 4>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a);
             break;
         default: hipLaunchKernelGGL(k_solve_reg, dim3(n_blocks), dim3(64), 0, (hipStream_t)stream, a); break;
@@ -633,7 +673,10 @@ int launch_solve(const SolveArgs& a_in, uint32_t n_blocks, bool need_general, bo
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !need_general) return (int)e;
     if (wide) {  // blocks with 64 < e <= 128; the rare rank-deficient-on-64-rows block goes to k_solve
-        if (solve_pm()) hipLaunchKernelGGL((k_solve_pm<2, 4>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a);
+        if (solve_pm() && solve_lut())
+            hipLaunchKernelGGL((k_solve_pm<2, 4, true>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a);
+        else if (solve_pm())
+            hipLaunchKernelGGL((k_solve_pm<2, 4, false>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a);
         else hipLaunchKernelGGL((k_solve_fast<2, 4>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a);
         if ((e = hipGetLastError()) != hipSuccess) return (int)e;
     }
