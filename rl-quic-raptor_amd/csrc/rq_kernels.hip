@@ -117,7 +117,7 @@ __device__ __forceinline__ uint8_t gmul_t(const uint8_t* lg, const uint8_t* ex, 
 
 // GF(256) exp/log tables (poly 0x11D, alpha = 2), constant-initialised in device memory and copied
 // into LDS by the blocks that need them.
-struct GfTabs {
+struct alignas(16) GfTabs {
     uint8_t ex[512];
     uint8_t lg[256];
 };
@@ -134,8 +134,33 @@ constexpr GfTabs make_gf_tabs() {
 __device__ const GfTabs kGf = make_gf_tabs();
 
 __device__ __forceinline__ void gf_tables_copy(uint8_t* ex, uint8_t* lg) {
-    for (uint32_t i = threadIdx.x; i < 512; i += blockDim.x) ex[i] = kGf.ex[i];
-    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) lg[i] = kGf.lg[i];
+    // as 192 dwords, one load per thread (no serialised byte-load loop)
+    const uint32_t* se = reinterpret_cast<const uint32_t*>(kGf.ex);
+    const uint32_t* sl = reinterpret_cast<const uint32_t*>(kGf.lg);
+    for (uint32_t i = threadIdx.x; i < 192; i += blockDim.x) {
+        if (i < 128) reinterpret_cast<uint32_t*>(ex)[i] = se[i];
+        else reinterpret_cast<uint32_t*>(lg)[i - 128] = sl[i - 128];
+    }
+}
+
+// Row gather of the solvers: wave g copies coefficient bytes k = g, g + NW, ... of one received
+// repair (mr[Es[k]], a byte gather from the program's identity-payload outputs) into its LDS row,
+// sixteen loads in flight per lane instead of one load-then-store round trip per byte.
+template <int NW>
+__device__ __forceinline__ void gather_row(uint8_t* myb, const uint8_t* mr, const uint32_t* Es, uint32_t e, uint32_t g) {
+    for (uint32_t k0 = g; k0 < e; k0 += 16 * NW) {
+        uint8_t v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const uint32_t k = k0 + NW * u;
+            v[u] = k < e ? mr[Es[k]] : (uint8_t)0;
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const uint32_t k = k0 + NW * u;
+            if (k < e) myb[k] = v[u];
+        }
+    }
 }
 
 // Four waves per block, RPL rows per lane: lane j of every wave holds received repairs j + 64q
@@ -152,7 +177,7 @@ __global__ void __launch_bounds__(64 * NW) k_solve_fast(SolveArgs a) {
     constexpr uint32_t NROWS = 64 * RPL, WQ = 8 * RPL, SW = 32 * RPL + 4;  // quads per row, row stride
     __shared__ __attribute__((aligned(16))) uint32_t rows[NROWS * SW];
     __shared__ __attribute__((aligned(16))) uint4 mult[8][WQ];  // alpha^b * scaled pivot row
-    __shared__ uint8_t ex[512], lg[256];
+    __shared__ __attribute__((aligned(4))) uint8_t ex[512], lg[256];
     __shared__ uint8_t pivl[NROWS];
     __shared__ uint32_t Es[NROWS];
     const uint32_t b = a.blk_map[blockIdx.x];
@@ -177,7 +202,7 @@ __global__ void __launch_bounds__(64 * NW) k_solve_fast(SolveArgs a) {
         if (row < nrow) {  // row gather: wave g takes columns g, g+4, ...
             uint8_t* myb = reinterpret_cast<uint8_t*>(rows + row * SW);
             const uint8_t* mr = a.mrep + (size_t)U[row] * a.mrep_stride;
-            for (uint32_t k = g; k < e; k += NW) myb[k] = mr[Es[k]];
+            gather_row<NW>(myb, mr, Es, e, g);
             if (g == 0) myb[e + row] = 1;
         }
     }
@@ -292,12 +317,15 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pm(SolveArgs a) {
     constexpr uint32_t NT = 64 * NW;
     constexpr uint32_t NROWS = 64 * RPL, SW = 32 * RPL + 4;  // rows, row stride (dwords)
     __shared__ __attribute__((aligned(16))) uint32_t rows[NROWS * SW];
-    __shared__ uint8_t ex[512], lg[256];
+    __shared__ __attribute__((aligned(4))) uint8_t ex[512], lg[256];
     __shared__ uint8_t pivl[NROWS];
     __shared__ uint32_t Es[NROWS];
     // LUT: the v_perm tables of every nonzero coefficient, indexed by its log (built once per block)
     __shared__ __attribute__((aligned(16))) uint4 tlA[LUT ? 255 : 1];
     __shared__ uint32_t tlB[LUT ? 255 : 1];
+    // LUT: per pivot value f (!= 0), log f | log(1 ^ 1/f) << 8 | (1 ^ 1/f != 0) << 16: one lookup per
+    // step instead of three dependent ones (lg[f_p], ex[255 - lg f_p], lg[c_p])
+    __shared__ uint32_t pinfo[LUT ? 256 : 1];
     const uint32_t b = a.blk_map[blockIdx.x];
     const uint32_t tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
     if (a.status_init)  // the host-decided statuses (disjoint from the solver's blocks, ST_PENDING)
@@ -325,10 +353,15 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pm(SolveArgs a) {
         if (row < nrow) {  // row gather: wave g takes columns g, g+4, ...
             uint8_t* myb = reinterpret_cast<uint8_t*>(rows + row * SW);
             const uint8_t* mr = a.mrep + (size_t)U[row] * a.mrep_stride;
-            for (uint32_t k = g; k < e; k += NW) myb[k] = mr[Es[k]];
+            gather_row<NW>(myb, mr, Es, e, g);
             if (g == 0) myb[e + row] = 1;
         }
     }
+    if (LUT)
+        for (uint32_t x = 1 + tid; x < 256; x += NT) {
+            const uint32_t lx = lg[x], cp = 1u ^ ex[255u - lx];
+            pinfo[x] = lx | (cp ? (uint32_t)lg[cp] << 8 | 1u << 16 : 0u);
+        }
     __syncthreads();
     const uint32_t q1 = (e + nrow + 15) >> 4;  // quads holding live columns
     bool used[RPL];
@@ -357,19 +390,17 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pm(SolveArgs a) {
 #pragma unroll
         for (int q = 0; q < RPL; ++q)
             if ((p >> 6) == (uint32_t)q) fp = __builtin_amdgcn_readlane(f[q], p & 63);
-        const uint32_t lgp = lg[fp];
-        const uint32_t inv = ex[255u - lgp];
         uint4 A[RPL];
         uint32_t B[RPL];
         bool act[RPL];
         if (LUT) {
-            const uint32_t cp = 1u ^ inv;                      // the pivot lane's coefficient
-            const uint32_t lcp = cp ? (uint32_t)lg[cp] : 0u;
+            const uint32_t pi = pinfo[fp];
+            const uint32_t lgp = pi & 0xFFu, lcp = (pi >> 8) & 0xFFu;  // the pivot lane's coefficient 1 ^ 1/f_p
 #pragma unroll
             for (int q = 0; q < RPL; ++q) {
                 uint32_t l = 0;
                 if (lane + 64 * q == p) {
-                    act[q] = cp != 0;
+                    act[q] = (pi >> 16) != 0;
                     l = lcp;
                 } else {
                     act[q] = f[q] != 0;
@@ -380,6 +411,8 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pm(SolveArgs a) {
                 B[q] = tlB[act[q] ? l : 0];
             }
         } else {
+            const uint32_t lgp = lg[fp];
+            const uint32_t inv = ex[255u - lgp];
 #pragma unroll
             for (int q = 0; q < RPL; ++q) {
                 uint32_t c = 0;
@@ -434,7 +467,7 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pm(SolveArgs a) {
 // multiply per dword as three v_perm lookups against per-lane tables of c_j (perm_tables).  The
 // pivot lane uses c = 1 ^ 1/f_p, which leaves row_p / f_p.  No barrier inside the elimination.
 __global__ void __launch_bounds__(64) k_solve_reg(SolveArgs a) {
-    __shared__ uint8_t ex[512], lg[256];
+    __shared__ __attribute__((aligned(4))) uint8_t ex[512], lg[256];
     __shared__ uint8_t pivl[64];
     __shared__ uint32_t rows[64 * 33];  // final rows, stride 33 dwords (no bank conflicts)
     const uint32_t b = a.blk_map[blockIdx.x];
@@ -525,7 +558,7 @@ __global__ void __launch_bounds__(64) k_solve_reg(SolveArgs a) {
 // (RQ/discmath/gauss.go:7-45) on the e erased columns.
 __global__ void __launch_bounds__(256) k_solve(SolveArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
-    __shared__ uint8_t ex[512], lg[256];
+    __shared__ __attribute__((aligned(4))) uint8_t ex[512], lg[256];
     __shared__ int piv;
     const uint32_t bi = blockIdx.x, b = a.blk_map[bi];
     if (a.status[b] != ST_FALLBACK) return;
@@ -761,13 +794,25 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a, uint32_t n_units, uin
     for (uint32_t c0 = 0; c0 < e; c0 += MC) {
         const uint32_t mc = min(MC, e - c0);
         __syncthreads();  // the previous chunk's tables are consumed
-        for (uint32_t idx = lane; idx < mc * KC; idx += 64) {
-            const uint32_t m = idx / KC, k = idx - m * KC;
-            uint4 A = make_uint4(0, 0, 0, 0);
-            uint32_t B = 0;
-            if (k0 + k < e) perm_tables(xc[(size_t)(c0 + m) * xs + k0 + k], &A, &B);
-            tA[idx] = A;
-            tB[idx] = B;
+        // coefficient bytes loaded eight per lane at a time before their tables are built (one
+        // dependent load round trip per eight instead of per coefficient)
+        for (uint32_t i0 = lane; i0 < mc * KC; i0 += 64 * 8) {
+            uint32_t cv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const uint32_t idx = i0 + 64 * u, m = idx / KC, k = idx - m * KC;
+                cv[u] = (idx < mc * KC && k0 + k < e) ? xc[(size_t)(c0 + m) * xs + k0 + k] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const uint32_t idx = i0 + 64 * u;
+                if (idx >= mc * KC) break;
+                uint4 A = make_uint4(0, 0, 0, 0);
+                uint32_t B = 0;
+                perm_tables(cv[u], &A, &B);  // c = 0 gives all-zero tables
+                tA[idx] = A;
+                tB[idx] = B;
+            }
         }
         for (uint32_t m = lane; m < mc + PD && c0 + m < e; m += 64) {
             const uint32_t j = r0b + XP[c0 + m];
