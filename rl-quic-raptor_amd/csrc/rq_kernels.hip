@@ -760,23 +760,30 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a, uint32_t n_units, uin
     const uint32_t* E = a.erased + a.erased_off[b];
     const uint16_t* XP = a.xpiv + a.erased_off[b];
     const uint32_t r0b = a.rep_off[b];
-    const uint32_t* recv = reinterpret_cast<const uint32_t*>(a.recv);
-    const uint32_t* r0 = reinterpret_cast<const uint32_t*>(a.r0) + (size_t)b * a.n_union * Td;
+    // the block's received repair rows and its r0 rows as buffer resources: a syndrome row's offset
+    // is one SGPR (soffset) and a lane's column one VGPR, so the loads carry no address arithmetic
+    const __amdgpu_buffer_rsrc_t rsR =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(a.recv + (size_t)r0b * a.T), (short)0, 0x7FFFFFFF, 0x20000);
+    const __amdgpu_buffer_rsrc_t rs0 =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(a.r0 + (size_t)b * a.n_union * a.T), (short)0, 0x7FFFFFFF, 0x20000);
     uint8_t* blk = a.data + (size_t)b * a.data_stride;
-    const uint32_t mc_max = min(MC, e);
+    // a chunk's syndromes are processed in whole groups of PD: the padding m's get zero tables and
+    // a valid row offset, so the ring needs no branch (and the compiler no register copies)
+    const uint32_t mc_max = (min(MC, e) + PD - 1) / PD * PD;
     uint4* tA = reinterpret_cast<uint4*>(xsh);                  // [m - c0][KC]
     uint32_t* tB = xsh + (size_t)mc_max * KC * 4;                // [m - c0][KC]
-    uint32_t* offr = tB + (size_t)mc_max * KC;                   // [m - c0], m < c0 + mc + PD
+    uint32_t* offr = tB + (size_t)mc_max * KC;                   // [m - c0], m < mcp + PD
     uint32_t* off0 = offr + mc_max + PD;
     const uint8_t* xc = a.xcoef + 64ull * a.xoff[bi];
     const uint32_t xs = x_stride(e);
-    uint32_t col[CPL];
+    uint32_t col[CPL], vo[CPL];
     bool live[CPL];
 #pragma unroll
     for (int j = 0; j < CPL; ++j) {
         const uint32_t c = strip * 64 * CPL + j * 64 + lane;
         live[j] = c < Td;
         col[j] = live[j] ? c : 0;
+        vo[j] = col[j] * 4;
     }
     // The erased rows were not cleared before the syndrome program, so s = M (x_E ^ g_E) with g_E their
     // current bytes: start every output from g_E and X s completes it to x_E.
@@ -792,11 +799,11 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a, uint32_t n_units, uin
     // multiple of PD, so ring slot d always holds syndrome m = d (mod PD) across chunks
     uint32_t ra[PD][CPL], rb[PD][CPL];
     for (uint32_t c0 = 0; c0 < e; c0 += MC) {
-        const uint32_t mc = min(MC, e - c0);
+        const uint32_t mc = min(MC, e - c0), mcp = (mc + PD - 1) / PD * PD;
         __syncthreads();  // the previous chunk's tables are consumed
         // coefficient bytes loaded eight per lane at a time before their tables are built (one
         // dependent load round trip per eight instead of per coefficient)
-        for (uint32_t i0 = lane; i0 < mc * KC; i0 += 64 * 8) {
+        for (uint32_t i0 = lane; i0 < mcp * KC; i0 += 64 * 8) {
             uint32_t cv[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
@@ -806,7 +813,7 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a, uint32_t n_units, uin
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 const uint32_t idx = i0 + 64 * u;
-                if (idx >= mc * KC) break;
+                if (idx >= mcp * KC) break;
                 uint4 A = make_uint4(0, 0, 0, 0);
                 uint32_t B = 0;
                 perm_tables(cv[u], &A, &B);  // c = 0 gives all-zero tables
@@ -814,30 +821,29 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a, uint32_t n_units, uin
                 tB[idx] = B;
             }
         }
-        for (uint32_t m = lane; m < mc + PD && c0 + m < e; m += 64) {
-            const uint32_t j = r0b + XP[c0 + m];
-            offr[m] = j * Td;
-            off0[m] = a.rep_uidx[j] * Td;
+        for (uint32_t m = lane; m < mcp + PD; m += 64) {  // byte offsets in the block (row 0 past e)
+            const uint32_t j = c0 + m < e ? XP[c0 + m] : 0u;
+            offr[m] = j * a.T;
+            off0[m] = c0 + m < e ? a.rep_uidx[r0b + j] * a.T : 0u;
         }
         __syncthreads();
         if (c0 == 0) {
 #pragma unroll
-            for (int d = 0; d < PD; ++d)
-                if ((uint32_t)d < e) {
+            for (int d = 0; d < PD; ++d) {
+                const int sr = (int)__builtin_amdgcn_readfirstlane(offr[d]), s0o = (int)__builtin_amdgcn_readfirstlane(off0[d]);
 #pragma unroll
-                    for (int j = 0; j < CPL; ++j) {
-                        ra[d][j] = recv[(size_t)offr[d] + col[j]];
-                        rb[d][j] = r0[(size_t)off0[d] + col[j]];
-                    }
+                for (int j = 0; j < CPL; ++j) {
+                    ra[d][j] = __builtin_amdgcn_raw_buffer_load_b32(rsR, (int)vo[j], sr, 0);
+                    rb[d][j] = __builtin_amdgcn_raw_buffer_load_b32(rs0, (int)vo[j], s0o, 0);
                 }
+            }
         }
         // (taking the syndromes in pairs, six lookups folded by three XOR3, measured 3 % slower:
         // profiles/r02w)
-        for (uint32_t mb = 0; mb < mc; mb += PD) {
+        for (uint32_t mb = 0; mb < mcp; mb += PD) {
 #pragma unroll
             for (int d = 0; d < PD; ++d) {
                 const uint32_t m = mb + d;
-                if (m >= mc) break;
                 uint32_t s0[CPL], s1[CPL], s2[CPL];
 #pragma unroll
                 for (int j = 0; j < CPL; ++j) {
@@ -846,11 +852,13 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a, uint32_t n_units, uin
                     s1[j] = (x >> 3) & 0x07070707u;
                     s2[j] = (x >> 6) & 0x03030303u;
                 }
-                if (c0 + m + PD < e) {
+                {  // past e the ring reads row 0 (zero tables consume it)
+                    const int sr = (int)__builtin_amdgcn_readfirstlane(offr[m + PD]);
+                    const int s0o = (int)__builtin_amdgcn_readfirstlane(off0[m + PD]);
 #pragma unroll
                     for (int j = 0; j < CPL; ++j) {
-                        ra[d][j] = recv[(size_t)offr[m + PD] + col[j]];
-                        rb[d][j] = r0[(size_t)off0[m + PD] + col[j]];
+                        ra[d][j] = __builtin_amdgcn_raw_buffer_load_b32(rsR, (int)vo[j], sr, 0);
+                        rb[d][j] = __builtin_amdgcn_raw_buffer_load_b32(rs0, (int)vo[j], s0o, 0);
                     }
                 }
 #pragma unroll
@@ -930,7 +938,8 @@ int launch_apply(const ApplyArgs& a, uint32_t /*n_strips*/, uint32_t n_blocks, v
     const uint32_t e = std::max<uint32_t>(a.max_e, 1), ec = std::min(e, MC);
     const uint32_t cap = std::max<uint32_t>(4, std::min<uint32_t>(8, (21504 / (20 * ec)) & ~3u));
     const uint32_t np = (e + cap - 1) / cap, kc = (((e + np - 1) / np) + 3) & ~3u;
-    const size_t lds = (size_t)ec * kc * 20 + (size_t)(ec + 8) * 8;  // tables + row offsets (<= 22 KB)
+    const size_t ecp = (ec + 7) / 8 * 8;  // the kernel pads a chunk to whole groups of PD (<= 8) syndromes
+    const size_t lds = ecp * kc * 20 + (ecp + 8) * 8;  // tables + row offsets (<= 23 KB)
     const uint32_t nu = (Td + 64 * cpl - 1) / (64 * cpl) * n_blocks;
     const dim3 g((nu + 7) / 8 * 8 * np);
     switch (cpl) {
