@@ -486,8 +486,10 @@ int encode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, c
 }
 
 // Decode output set: every candidate repair ESI the batch holds.  A dense range [K, K+R) (R a
-// multiple of 16) when the received ESIs are not too sparse -- one compiled program then serves
-// every erasure pattern of that range -- otherwise the exact sorted set.
+// multiple of 4) when the received ESIs are not too sparse -- one compiled program then serves
+// every erasure pattern of that range, and when the highest ESI received is the sender's last
+// (N - 1, N - K a multiple of 4) it is the sender's own encode program -- otherwise the exact
+// sorted set.
 std::vector<uint32_t> decode_union(uint32_t K, const std::vector<uint32_t>& rep) {
     std::vector<uint32_t> u;
     if (rep.empty()) return u;
@@ -502,7 +504,7 @@ std::vector<uint32_t> decode_union(uint32_t K, const std::vector<uint32_t>& rep)
         std::sort(u.begin(), u.end());
         u.erase(std::unique(u.begin(), u.end()), u.end());
     }
-    const uint64_t span = ((uint64_t)u.back() - K + 16) & ~(uint64_t)15;
+    const uint64_t span = ((uint64_t)u.back() - K + 4) & ~(uint64_t)3;
     if (span <= 4 * u.size() + 64) {
         std::vector<uint32_t> r((size_t)span);
         for (uint32_t i = 0; i < span; ++i) r[i] = K + i;
