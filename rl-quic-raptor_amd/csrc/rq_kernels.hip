@@ -761,11 +761,13 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a, uint32_t n_units, uin
     const uint16_t* XP = a.xpiv + a.erased_off[b];
     const uint32_t r0b = a.rep_off[b];
     // the block's received repair rows and its r0 rows as buffer resources: a syndrome row's offset
-    // is one SGPR (soffset) and a lane's column one VGPR, so the loads carry no address arithmetic
+    // is one SGPR (soffset) and a lane's column one VGPR, so the loads carry no address arithmetic.
+    // Offsets are 32-bit within one block (its received repairs and r0 rows span < 4 GiB, as every
+    // launch's buffers do, rq_engine.cpp launch_col); the record count is unlimited.
     const __amdgpu_buffer_rsrc_t rsR =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(a.recv + (size_t)r0b * a.T), (short)0, 0x7FFFFFFF, 0x20000);
+        __builtin_amdgcn_make_buffer_rsrc((void*)(a.recv + (size_t)r0b * a.T), (short)0, -1, 0x20000);
     const __amdgpu_buffer_rsrc_t rs0 =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(a.r0 + (size_t)b * a.n_union * a.T), (short)0, 0x7FFFFFFF, 0x20000);
+        __builtin_amdgcn_make_buffer_rsrc((void*)(a.r0 + (size_t)b * a.n_union * a.T), (short)0, -1, 0x20000);
     uint8_t* blk = a.data + (size_t)b * a.data_stride;
     // a chunk's syndromes are processed in whole groups of PD: the padding m's get zero tables and
     // a valid row offset, so the ring needs no branch (and the compiler no register copies)
