@@ -427,8 +427,10 @@ int launch_col(DevCtx* ctx, ColKernel* k, uint32_t T, uint32_t n_blocks, const v
         return fail(RQ_ERR_UNSUPPORTED, "block stride beyond the 4 GiB buffer-offset range");
     if ((uint64_t)per * Td > 0x7FFFFFFFull) return fail(RQ_ERR_UNSUPPORTED, "batch too large");
     const uint32_t max_items = (uint32_t)(((uint64_t)per * Td + 63) / 64);
-    // persistent grid: at most the resident wave count (scratch is per grid wave)
-    const uint32_t resident = ctx->n_cu * k->waves_per_cu;
+    // persistent grid: at most the resident wave count (scratch is per grid wave; RQHIP_WAVES caps it
+    // in experiments builds)
+    static const uint32_t cap = [] { const char* e = knob("RQHIP_WAVES"); return e ? (uint32_t)std::atoi(e) : 0u; }();
+    const uint32_t resident = cap ? std::min(cap, ctx->n_cu * k->waves_per_cu) : ctx->n_cu * k->waves_per_cu;
     const uint32_t max_wg = std::min(max_items, resident);
     const size_t spw = (size_t)std::max<uint32_t>(k->n_slots, 1) * 256;
     int rc;
@@ -463,7 +465,12 @@ int launch_col(DevCtx* ctx, ColKernel* k, uint32_t T, uint32_t n_blocks, const v
         size_t sz = sizeof a;
         void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
         const uint32_t items = (a.n_cols + 63) / 64;
-        const uint32_t waves = std::min(items, resident);
+        // Balanced rounds: as many waves as spread the items evenly over the rounds the resident set
+        // needs (a multiple of 8 for the XCD remap), not the whole resident set with a partial last
+        // round -- 1024 blocks K=1024 = 4 800 items: 960 waves x 5 instead of 704 x 5 + 320 x 4, the
+        // busy waves then share HBM with fewer others (0.49 -> 0.47 ms, profiles/r02at).
+        const uint32_t rounds = (items + resident - 1) / resident;
+        const uint32_t waves = std::min(resident, ((items + rounds - 1) / rounds + 7) / 8 * 8);
         a.n_items = items;
         a.n_wg = waves;
         if (xcd_order() && waves % 8 == 0) {  // the remap needs the stride to keep w % 8 fixed
