@@ -938,7 +938,10 @@ int launch_apply(const ApplyArgs& a, uint32_t /*n_strips*/, uint32_t n_blocks, v
     // the slice's tables (20 B per coefficient) for MC syndromes within ~20 KB of LDS
     constexpr uint32_t MC = 256;
     const uint32_t e = std::max<uint32_t>(a.max_e, 1), ec = std::min(e, MC);
-    const uint32_t cap = std::max<uint32_t>(4, std::min<uint32_t>(8, (21504 / (20 * ec)) & ~3u));
+    uint32_t cap = std::max<uint32_t>(4, std::min<uint32_t>(8, (21504 / (20 * ec)) & ~3u));
+#ifdef RQHIP_EXPERIMENTS
+    if (const char* v = std::getenv("RQHIP_APPLY_KC")) cap = std::max(4, std::min(32, std::atoi(v))) & ~3u;
+#endif
     const uint32_t np = (e + cap - 1) / cap, kc = (((e + np - 1) / np) + 3) & ~3u;
     const size_t ecp = (ec + 7) / 8 * 8;  // the kernel pads a chunk to whole groups of PD (<= 8) syndromes
     const size_t lds = ecp * kc * 20 + (ecp + 8) * 8;  // tables + row offsets (<= 23 KB)
