@@ -944,7 +944,10 @@ int launch_apply(const ApplyArgs& a, uint32_t /*n_strips*/, uint32_t n_blocks, v
 #endif
     const uint32_t np = (e + cap - 1) / cap, kc = (((e + np - 1) / np) + 3) & ~3u;
     const size_t ecp = (ec + 7) / 8 * 8;  // the kernel pads a chunk to whole groups of PD (<= 8) syndromes
-    const size_t lds = ecp * kc * 20 + (ecp + 8) * 8;  // tables + row offsets (<= 23 KB)
+    size_t lds = ecp * kc * 20 + (ecp + 8) * 8;  // tables + row offsets (<= 23 KB)
+#ifdef RQHIP_EXPERIMENTS
+    if (const char* v = std::getenv("RQHIP_APPLY_LDS")) lds = std::max<size_t>(lds, (size_t)std::atoi(v));  // occupancy cap
+#endif
     const uint32_t nu = (Td + 64 * cpl - 1) / (64 * cpl) * n_blocks;
     const dim3 g((nu + 7) / 8 * 8 * np);
     switch (cpl) {
