@@ -1,6 +1,7 @@
 """Column-program encode: parity spot check + timing at a batch config (GPU).
 
 usage: python tools/colbench.py [K] [T] [N] [blocks] [iters]
+RQBENCH_PAD=bytes pads the source block stride (a view into a wider buffer).
 """
 import os
 import sys
@@ -24,7 +25,8 @@ def main():
     dev = torch.device("cuda:0")
     esis = list(range(K, N))
     g = torch.Generator(device=dev).manual_seed(5)
-    src = torch.randint(0, 256, (B, K * T), dtype=torch.uint8, device=dev, generator=g)
+    pad = int(os.environ.get("RQBENCH_PAD", "0"))
+    src = torch.randint(0, 256, (B, K * T + pad), dtype=torch.uint8, device=dev, generator=g)[:, :K * T]
     out = torch.empty((B, (N - K) * T), dtype=torch.uint8, device=dev)
     t0 = time.time()
     rqhip.encode_batch(src, K, T, esis, out)
