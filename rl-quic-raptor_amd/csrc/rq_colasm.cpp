@@ -515,7 +515,9 @@ bool compile_colprog(const Params& p, const uint32_t* esi, uint32_t n_out, const
                      std::string* err, uint32_t* passes_out, bool search_waves) {
     double best = 0;
     bool have = false;
-    std::vector<uint32_t> cand{0u, 1u, 2u, 3u, 4u, 5u, 6u};
+    // P Horner passes, or no scan at all (SCHED_4R: bh bit by bit, XOR now when the accumulator's
+    // next push is more than 64 productions away); K=1024: P = 2 32.0 k slots, 4R 25.8 k (no spills)
+    std::vector<uint32_t> cand{0u, 1u, 2u, 3u, 4u, 5u, 6u, SCHED_4R | 64u, SCHED_4R};
     if (const char* f = knob("RQHIP_PASSES")) cand = {(uint32_t)std::atoi(f)};  // experiments: fixed schedule
     for (uint32_t P : cand) {
         ColIR cir;

@@ -9,8 +9,11 @@
 #include "rq_colprog.hpp"
 
 #include <algorithm>
+#include <array>
 #include <cstring>
+#include <map>
 #include <queue>
+#include <set>
 
 namespace rq {
 
@@ -356,9 +359,12 @@ struct Builder {
 // Accumulator: pushes are XORed in pairs (one XOR3 per two pushes).
 struct Acc {
     uint32_t val = NOVAL, pend = NOVAL;
-    void push(Builder& B, uint32_t v) {
+    // may_pend = false: the next push is far off, so XOR now rather than keep v alive as the pending
+    // operand of a later XOR3
+    void push(Builder& B, uint32_t v, bool may_pend = true) {
         if (v == NOVAL) return;
         if (val == NOVAL) { val = v; return; }
+        if (!may_pend && pend == NOVAL) { val = B.add(IR_XOR2, val, v); return; }
         if (pend == NOVAL) { pend = v; return; }
         val = B.add(IR_XOR3, val, pend, v);
         pend = NOVAL;
@@ -473,7 +479,167 @@ bool build(const Params& p, const std::vector<OutDesc>& outs, uint32_t passes, C
     std::vector<Acc> b2acc(n2), oacc(no), part(H);
     for (uint32_t i = 0; i < n2; ++i) b2acc[i].push(B, D(e.rem[i]));
     uint32_t t = NOVAL;
-    if (passes) {  // peeling-order production, push-mode dependencies, P Horner passes
+    std::vector<uint32_t> bh_direct;  // SCHED_4R: bh computed without a Horner scan
+    if (passes & SCHED_4R) {
+        // Peeling-order production, push-mode dependencies; no Horner scan.  bh_h = sum_j G[h][j] y_j
+        // (G = MT * Gamma, RQ/params.go:116-133) is accumulated bit by bit: S[h][b] = XOR of the y_j
+        // with bit b of G[h][j] set, bh_h = sum_b alpha^b S[h][b] (7 xtimes per h at the end).  Every
+        // 8 consecutively produced y values form two groups of 4 whose subset XORs (11 per group) are
+        // built once; each of the 8H bit rows then takes one XOR3 (its group-A subset, its group-B
+        // subset).  ~12.75 VALU per y and no y waits for a scan: the live set drops by the scan's
+        // buffer (hundreds of values) for the cost of ~2 Horner passes.
+        std::vector<std::vector<uint32_t>> dependents(npiv);
+        for (uint32_t k = 0; k < npiv; ++k)
+            for (uint32_t j : e.deps[k]) dependents[j].push_back(k);
+        std::vector<Acc> yacc(npiv);
+        // next event (push or consumption) of every accumulator after production k, so a push whose
+        // accumulator is not touched again within `pend_win` productions XORs at once
+        const uint32_t pend_win = (passes & 0xFFFFu) ? (passes & 0xFFFFu) : 0xFFFFu;
+        const uint32_t n_acc = npiv + n2 + no;
+        std::vector<std::vector<uint32_t>> ev(n_acc);
+        for (uint32_t k = 0; k < npiv; ++k) {
+            for (uint32_t d : dependents[k]) ev[d].push_back(k);
+            const uint32_t c = e.piv_col[k];
+            for (uint32_t i : col_rem[c]) ev[npiv + i].push_back(k);
+            for (uint32_t o : col_outs[c]) ev[npiv + n2 + o].push_back(k);
+        }
+        for (uint32_t d = 0; d < npiv; ++d) ev[d].push_back(d);
+        std::vector<uint32_t> evp(n_acc, 0);
+        auto may_pend = [&](uint32_t a, uint32_t k) {
+            auto& v = ev[a];
+            uint32_t& q = evp[a];
+            while (q < v.size() && v[q] <= k) ++q;
+            return q < v.size() && v[q] - k <= pend_win;
+        };
+        std::vector<uint32_t> S8((size_t)H * 8, NOVAL);
+        std::vector<uint32_t> chunk;  // pivot indices of produced y (column < KS)
+        auto flush = [&]() {
+            if (chunk.empty()) return;
+            const size_t ng = (chunk.size() + 3) / 4;
+            std::vector<std::array<uint32_t, 16>> sub(ng);
+            for (size_t g = 0; g < ng; ++g) sub[g].fill(NOVAL);
+            auto subset = [&](size_t g, uint32_t m) -> uint32_t {  // XOR of group g's members in mask m
+                auto& s = sub[g];
+                if (s[m] != NOVAL) return s[m];
+                std::vector<uint32_t> terms;
+                for (uint32_t q = 0; q < 4; ++q)
+                    if (m & (1u << q)) terms.push_back(y[chunk[g * 4 + q]]);
+                if (terms.size() <= 1) { s[m] = terms.empty() ? NOVAL : terms[0]; return s[m]; }
+                if (terms.size() == 4) {  // (pair) ^ y2 ^ y3 with the pair built once
+                    const uint32_t m01 = m & 3u;
+                    std::vector<uint32_t> v{sub[g][m01] != NOVAL ? sub[g][m01] : B.xsum({terms[0], terms[1]}), terms[2], terms[3]};
+                    sub[g][m01] = v[0];
+                    s[m] = B.xsum(v);
+                    return s[m];
+                }
+                s[m] = B.xsum(terms);
+                return s[m];
+            };
+            for (uint32_t h = 0; h < H; ++h)
+                for (uint32_t b = 0; b < 8; ++b) {
+                    std::vector<uint32_t> terms{S8[h * 8 + b]};
+                    for (size_t g = 0; g < ng; ++g) {
+                        uint32_t m = 0;
+                        for (uint32_t q = 0; q < 4 && g * 4 + q < chunk.size(); ++q) {
+                            const uint32_t c = e.piv_col[chunk[g * 4 + q]];
+                            if ((e.G[(size_t)h * KS + c] >> b) & 1) m |= 1u << q;
+                        }
+                        if (m) terms.push_back(subset(g, m));
+                    }
+                    S8[h * 8 + b] = B.xsum(terms);
+                }
+            chunk.clear();
+        };
+        for (uint32_t k = 0; k < npiv; ++k) {
+            std::vector<uint32_t> tt{D(e.piv_row[k]), yacc[k].get(B)};
+            y[k] = B.xsum(tt);
+            ystate[k] = 2;
+            for (uint32_t d : dependents[k]) yacc[d].push(B, y[k], may_pend(d, k));
+            const uint32_t c = e.piv_col[k];
+            for (uint32_t i : col_rem[c]) b2acc[i].push(B, y[k], may_pend(npiv + i, k));
+            for (uint32_t o : col_outs[c]) oacc[o].push(B, y[k], may_pend(npiv + n2 + o, k));
+            if (c < KS && y[k] != NOVAL) {
+                chunk.push_back(k);
+                if (chunk.size() == 8) flush();
+            }
+        }
+        flush();
+        bh_direct.assign(H, NOVAL);
+        for (uint32_t h = 0; h < H; ++h) {
+            uint32_t acc = NOVAL;
+            for (int b = 7; b >= 0; --b) acc = B.xt(acc, S8[h * 8 + b]);
+            bh_direct[h] = acc;
+        }
+    } else if (passes & SCHED_RS) {
+        // Peeling-order production, push-mode dependencies; the Horner chain absorbs the produced y
+        // values by replacement selection: at most `hbuf` of them wait, and whenever the buffer is
+        // over budget the chain advances to the smallest buffered column beyond its cursor.  When no
+        // buffered column lies ahead, the chain parks (its state waits at its cursor) and a new run
+        // starts at the smallest buffered column; a run that reaches a parked cursor merges with it.
+        // The scan is linear, so the runs' pushes and end values add up to the single scan's; a buffer
+        // of ~0.37 npiv gives one run (~KS xtimes) where fixed peeling-order passes need two.
+        const uint32_t hbuf = passes & 0xFFFFu;
+        std::vector<std::vector<uint32_t>> dependents(npiv);
+        for (uint32_t k = 0; k < npiv; ++k)
+            for (uint32_t j : e.deps[k]) dependents[j].push_back(k);
+        std::vector<Acc> yacc(npiv);
+        std::set<uint32_t> buf;                     // buffered (produced, not absorbed) pivoted columns
+        std::map<uint32_t, uint32_t> parked;        // cursor column -> parked chain state
+        int64_t cur = -1;                           // active chain: last column visited
+        uint32_t tp = NOVAL;
+        auto step_to = [&](uint32_t c) {            // advance the active chain through column c
+            uint32_t yj = NOVAL;
+            auto it = buf.find(c);
+            if (it != buf.end()) { yj = y[(uint32_t)e.col_order[c]]; buf.erase(it); }
+            tp = B.xt(tp, yj);
+            if (c + 1 < KS && tp != NOVAL) {
+                part[e.ma[c]].push(B, tp);
+                part[e.mb[c]].push(B, tp);
+            }
+            auto pk = parked.find(c);
+            if (pk != parked.end()) {
+                std::vector<uint32_t> v{tp, pk->second};
+                tp = B.xsum(v);
+                parked.erase(pk);
+            }
+            cur = c;
+        };
+        auto absorb_one = [&]() {
+            auto it = buf.upper_bound((uint32_t)std::max<int64_t>(cur, -1));
+            if (cur < 0) it = buf.begin();
+            if (it == buf.end()) {          // nothing ahead: park this run, start the next one
+                if (tp != NOVAL) {
+                    auto pk = parked.find((uint32_t)cur);
+                    if (pk == parked.end()) parked[(uint32_t)cur] = tp;
+                    else { std::vector<uint32_t> v{tp, pk->second}; pk->second = B.xsum(v); }
+                }
+                tp = NOVAL;
+                it = buf.begin();
+            }
+            const uint32_t target = *it;
+            // a fresh run starts at its first column: the columns before carry a zero state
+            if (tp == NOVAL) cur = (int64_t)target - 1;
+            while ((uint32_t)(cur + 1) <= target) step_to((uint32_t)(cur + 1));
+        };
+        for (uint32_t k = 0; k < npiv; ++k) {
+            std::vector<uint32_t> tt{D(e.piv_row[k]), yacc[k].get(B)};
+            y[k] = B.xsum(tt);
+            ystate[k] = 2;
+            for (uint32_t d : dependents[k]) yacc[d].push(B, y[k]);
+            const uint32_t c = e.piv_col[k];
+            for (uint32_t i : col_rem[c]) b2acc[i].push(B, y[k]);
+            for (uint32_t o : col_outs[c]) oacc[o].push(B, y[k]);
+            if (c < KS && y[k] != NOVAL) buf.insert(c);
+            while (buf.size() > hbuf) absorb_one();
+        }
+        while (!buf.empty()) absorb_one();
+        // finish: the active chain and every parked one run to column KS - 1
+        if (tp != NOVAL || !parked.empty()) {
+            if (tp == NOVAL) { cur = (int64_t)parked.begin()->first; tp = parked.begin()->second; parked.erase(parked.begin()); }
+            while (cur + 1 < (int64_t)KS) step_to((uint32_t)(cur + 1));
+            t = tp;
+        }
+    } else if (passes) {  // peeling-order production, push-mode dependencies, P Horner passes
         std::vector<std::vector<uint32_t>> dependents(npiv);
         for (uint32_t k = 0; k < npiv; ++k)
             for (uint32_t j : e.deps[k]) dependents[j].push_back(k);
@@ -550,7 +716,9 @@ bool build(const Params& p, const std::vector<OutDesc>& outs, uint32_t passes, C
     }
     // bh_h = part_h ^ alpha^h * t_(KS-1)
     std::vector<uint32_t> bh(H), b2(n2);
-    {
+    if (!bh_direct.empty()) {
+        bh = bh_direct;
+    } else {
         uint32_t s = t;
         for (uint32_t h = 0; h < H; ++h) {
             if (h) s = B.xt(s);

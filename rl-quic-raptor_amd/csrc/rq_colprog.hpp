@@ -47,6 +47,11 @@ enum IrKind : uint8_t {
     IR_STORE = 6  // output imm <- a
 };
 constexpr uint32_t NOVAL = 0xFFFFFFFFu;
+// build_colprog's `passes` with this bit set: replacement-selection Horner runs with a buffer of
+// (passes & 0xFFFF) produced y values (see build() in rq_colprog.cpp).
+constexpr uint32_t SCHED_RS = 1u << 16;
+// ... with this bit set instead: no Horner scan, bh accumulated bit by bit over groups of produced y.
+constexpr uint32_t SCHED_4R = 1u << 17;
 
 struct IrNode {
     uint8_t k = IR_ZERO;

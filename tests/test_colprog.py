@@ -117,11 +117,15 @@ def test_program_size_and_assembly(rq):
     assert rq.colprog_assemble(1024, list(range(1024, 1100))) > 131072
 
 
-@pytest.mark.parametrize("passes", [0, 1, 2, 3, 5])
+SCHED_RS, SCHED_4R = 1 << 16, 1 << 17  # rq_colprog.hpp
+
+
+@pytest.mark.parametrize("passes", [0, 1, 2, 3, 5, SCHED_RS | 96, SCHED_RS | 400, SCHED_4R, SCHED_4R | 64, SCHED_4R | 2])
 @pytest.mark.parametrize("K,T,nrep", [(64, 16, 16), (1024, 8, 76), (2048, 4, 30)])
 def test_every_ir_schedule_matches_oracle(rq, oracle, K, T, nrep, passes):
-    """Each IR schedule the engine may choose (one demand-driven scan, or peeling-order production
-    with P Horner passes, rq_colprog.cpp build()) gives the reference bytes, as IR and as the
+    """Each IR schedule the engine may choose (one demand-driven scan, peeling-order production
+    with P Horner passes or replacement-selection Horner runs, or no scan with bh accumulated bit
+    by bit (SCHED_4R), rq_colprog.cpp build()) gives the reference bytes, as IR and as the
     allocated, emulated machine program."""
     rng = np.random.default_rng(K + 11 * passes)
     data = rng.integers(0, 256, K * T, dtype=np.uint8)
