@@ -59,7 +59,49 @@ def parse():
                          "1024 blocks K=256 T=1200 R=26; 5 = mixed K x T stream end to end through the host API")
     ap.add_argument("--dist-backend", default="nccl", help="process-group backend for the timing collectives "
                     "(nccl = RCCL; gloo lets several ranks share one GPU for a functional rehearsal)")
+    ap.add_argument("--total-blocks", type=int, default=0,
+                    help="config 3/4: shard this many blocks over the ranks (strong scaling, BASELINE config 4 = "
+                         "8192); default 0 = --blocks per GPU (weak scaling)")
+    ap.add_argument("--plan-only", action="store_true",
+                    help="print the rank launch plan (ranks, devices, block shards) as JSON and exit; no GPU call")
     return ap.parse_args()
+
+
+def rank_env(world, rank, port):
+    """Environment of rank `rank` of a `world`-rank run on this node (what torch.distributed.run sets)."""
+    env = dict(os.environ)
+    env.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return env
+
+
+def launch_plan(args, world):
+    """Per rank: its GPU (= local rank) and its block range (global block index of its first block, count)."""
+    plan = []
+    for r in range(world):
+        if args.total_blocks:
+            start, count = rqshard.shard(args.total_blocks, world, r)
+        else:
+            start, count = r * args.blocks, args.blocks
+        plan.append({"rank": r, "device": r, "first_block": start, "blocks": count})
+    return plan
+
+
+def spawn_ranks(args):
+    """`--gpus N` without a launcher: start N rank processes of this script (one per GPU, rank r on GPU r)
+    before this process touches the GPU, and exit with the first non-zero rank status.  Rank 0 prints the
+    JSON line.  (Under `torch.distributed.run` WORLD_SIZE is already set and no process is spawned.)"""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=rank_env(args.gpus, r, port))
+             for r in range(args.gpus)]
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc]
+    return bad[0] if bad else 0
 
 
 def erasure_pattern(K, N, n_blocks, n_erase, seed):
@@ -148,14 +190,22 @@ def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as tdist
-        tdist.init_process_group(args.dist_backend)
-        dist = tdist
+    if world != args.gpus:
+        raise SystemExit("bench.py: WORLD_SIZE=%d but --gpus %d" % (world, args.gpus))
+    # rank r pins GPU r (several gloo ranks may share one GPU in a rehearsal on a smaller box)
     gpu = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
+    dist = None
+    if world > 1:
+        import torch.distributed as tdist
+        if args.dist_backend == "nccl":  # bind the RCCL communicator to this rank's GPU explicitly
+            tdist.init_process_group(args.dist_backend, device_id=dev)
+        else:
+            tdist.init_process_group(args.dist_backend)
+        dist = tdist
+        print("bench.py: rank %d of %d on GPU %d (%s)" % (rank, world, gpu, args.dist_backend), file=sys.stderr,
+              flush=True)
     rqhip.lib().rq_set_device(gpu)
     coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
     return world, rank, dist, dev, coll_dev
@@ -293,16 +343,26 @@ def run_config5(args):
 
 def main():
     args = parse()
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if args.plan_only:
+        world = args.gpus
+        print(json.dumps({"world": world, "launcher": "spawn" if "WORLD_SIZE" not in os.environ else "external",
+                          "scaling": "strong" if args.total_blocks else "weak", "ranks": launch_plan(args, world)}))
+        return 0
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn_ranks(args)
     if args.config == 2:
         return run_config2(args)
     if args.config == 5:
         return run_config5(args)
     world, rank, dist, dev, coll_dev = dist_setup(args)
-    K, T, N, B = args.K, args.T, args.N, args.blocks
+    K, T, N = args.K, args.T, args.N
+    first, B = launch_plan(args, world)[rank]["first_block"], launch_plan(args, world)[rank]["blocks"]
     R = N - K
     n_erase = int(round(args.erase * N))
     esis = list(range(K, N))
-    g = torch.Generator(device=dev).manual_seed(rqshard.block_seed(rank * B))
+    g = torch.Generator(device=dev).manual_seed(rqshard.block_seed(first))
     src = torch.randint(0, 256, (B, K * T), dtype=torch.uint8, device=dev, generator=g)
     rep = torch.empty((B, R * T), dtype=torch.uint8, device=dev)
     er, rl = erasure_pattern(K, N, B, n_erase, 7 + rank)
@@ -361,10 +421,12 @@ def main():
         line = {
             "metric": METRIC, "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "higher_is_better": True, "scaling": "strong" if args.total_blocks else "weak", "vs_baseline": None,
+            "dtype": "u8",
             "data": "synthetic (seeded torch.randint payload per rank, seeded exact-count 5% erasures)",
             "config": {"workload": "encode+decode K=%d T=%d N=%d, erase %d of %d symbols per block" % (K, T, N, n_erase, N),
-                       "blocks_per_gpu": B, "bytes_per_gpu": B * K * T, "parallelism": "block-sharded x%d" % world,
+                       "blocks_per_gpu": B, "total_blocks": total_blocks, "bytes_per_gpu": B * K * T,
+                       "parallelism": "block-sharded x%d" % world,
                        "decode_ok_fraction": ok_frac, "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4)},
             "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
@@ -381,4 +443,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -72,7 +72,8 @@ void rq_decoder_free(rq_dec* d);
  * rq_encode_batch returns without synchronising, rq_decode_batch synchronises once to report
  * per-block status. */
 typedef struct {
-    uint32_t T;              /* symbol size in bytes, multiple of 4                            */
+    uint32_t T;              /* symbol size in bytes: a multiple of 4, at least 8 (device-resident
+                                calls; the host-memory calls take any T and pad rows internally) */
     uint32_t K;              /* source symbols per block (library K)                           */
     uint32_t n_blocks;
     const void* src;         /* (device) block b symbol i at src + b*src_stride + i*T          */
@@ -99,7 +100,8 @@ typedef struct {
     const void* repair;          /* (device) repair rows (T bytes each) in repair_esi order     */
     int32_t* status;             /* (host out) [n_blocks]: 1 decoded, 0 rank-deficient (every
                                     received symbol considered), RQ_ERR_NOT_ENOUGH if received < K.
-                                    Any erasure count and any number of received repairs.       */
+                                    Any erasure count; at most 65535 received repairs per block
+                                    (RQ_ERR_UNSUPPORTED beyond).                                  */
     void* stream;
 } rq_decode_desc;
 int rq_decode_batch(const rq_decode_desc* d);
@@ -148,6 +150,17 @@ void rq_host_free(void* p);
 /* ---------------- device control ---------------- */
 int rq_device_count(void);
 int rq_set_device(int device);      /* selects the HIP device for subsequent calls on this thread */
+/* The library keeps per-stream device workspaces for the batched device-resident calls (descriptors,
+ * syndromes, scratch).  At most 8 caller streams per device keep one: beyond that the least recently
+ * used is released (after a device synchronisation).  rq_stream_release frees the workspace of
+ * `stream` (a hipStream_t; NULL = the default stream) on the current device now -- call it when a
+ * stream is retired.  No reference counterpart (the Go library has no device state). */
+int rq_stream_release(void* stream);
+/* Releases every device resource of the library (workspaces, compiled programs, internal streams and
+ * events, staging) after synchronising each device.  Optional: nothing is released at process exit
+ * (static teardown may run after the HIP runtime's), so a process that wants a clean HIP teardown
+ * calls this before exiting.  Any later call re-creates what it needs. */
+int rq_shutdown(void);
 
 /* ---------------- diagnostics (host only; tests and tools) ----------------
  * The encode hot path is a straight-line gfx950 program generated per (K', K, outputs): the
@@ -175,6 +188,9 @@ int rq_debug_colprog_assemble(uint32_t K, const uint32_t* esi, uint32_t n_out, s
  * and re-solve on all of them only if that subset is rank-deficient.  Sets the margin (tests force
  * the second pass with 0) and returns the previous one.  Results never depend on it. */
 uint32_t rq_debug_decode_margin(uint32_t margin);
+/* The engine's LT tuple of ISI X at library K (rq_core.hpp tuple_of; RQ/params.go:83-112):
+ * out = {d, a, b, d1, a1, b1}. */
+int rq_debug_tuple(uint32_t K, uint32_t X, uint32_t out[6]);
 /* The column program's IR schedule for the three rq_debug_colprog_* entry points: -1 (default)
  * chooses like the engine (cost model over the schedules), 0 = one demand-driven column scan,
  * P >= 1 = peeling-order production with P Horner passes.  Returns the previous setting. */

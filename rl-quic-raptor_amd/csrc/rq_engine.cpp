@@ -11,6 +11,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -126,6 +127,11 @@ struct Workspace {
     DevBuf dstatus;                 // zero-copy descriptors: the solver/apply statuses stay on the device
 
     uint32_t flip = 0;
+    uint64_t last_use = 0;          // LRU clock (DevCtx::wsp)
+    ~Workspace() {
+        for (hipEvent_t& e : up)
+            if (e) (void)hipEventDestroy(e);
+    }
 };
 
 // Host-memory batch API: device staging of one pipeline stage (one internal stream).
@@ -152,15 +158,68 @@ struct DevCtx {
     hipStream_t obj_stream = nullptr;  // per-object API: its own stream, pinned staging, device buffer
     HostBuf obj_h;
     DevBuf obj_d;
+    // Per-stream workspaces are bounded: a caller that uses a fresh stream per window would otherwise
+    // grow device memory without limit (each holds r0 / scratch / descriptors, ~130 MB at K=1024 x
+    // 1024 blocks).  Beyond MAX_WS caller streams the least recently used one is released (after a
+    // device synchronisation: its stream may still run kernels reading it); the library's own stage
+    // streams are never evicted.  rq_stream_release() releases one explicitly.
+    static constexpr size_t MAX_WS = 8;
     Workspace* wsp(void* stream) {
         auto& w = ws[stream];
-        if (!w) w.reset(new Workspace());
+        if (!w) {
+            w.reset(new Workspace());
+            evict_ws(stream);
+        }
+        w->last_use = ++tick;
         return w.get();
+    }
+    bool internal(void* s) const {
+        for (const Stage& st : stage)
+            if (st.s && (void*)st.s == s) return true;
+        return obj_stream && (void*)obj_stream == s;
+    }
+    void evict_ws(void* keep) {
+        size_t n_caller = 0;
+        for (auto& kv : ws) n_caller += !internal(kv.first);
+        while (n_caller > MAX_WS) {
+            auto victim = ws.end();
+            for (auto it = ws.begin(); it != ws.end(); ++it)
+                if (it->first != keep && !internal(it->first) &&
+                    (victim == ws.end() || it->second->last_use < victim->second->last_use))
+                    victim = it;
+            if (victim == ws.end()) return;
+            (void)hipDeviceSynchronize();
+            ws.erase(victim);
+            --n_caller;
+        }
+    }
+    ~DevCtx() {  // rq_shutdown only (contexts are never destroyed at exit)
+        (void)hipSetDevice(device);
+        (void)hipDeviceSynchronize();
+        ws.clear();
+        colk.clear();
+        for (Stage& st : stage)
+            if (st.s) (void)hipStreamDestroy(st.s);
+        for (hipEvent_t e : kdone)
+            if (e) (void)hipEventDestroy(e);
+        for (hipEvent_t e : updone)
+            if (e) (void)hipEventDestroy(e);
+        if (obj_stream) (void)hipStreamDestroy(obj_stream);
+    }
+    void release_ws(void* stream) {
+        auto it = ws.find(stream);
+        if (it == ws.end()) return;
+        (void)hipDeviceSynchronize();
+        ws.erase(it);
     }
 };
 
+// Device contexts are created on first use and deliberately never destroyed by static destructors:
+// at process exit the HIP runtime (or a profiler's tool library) may already be torn down, and a
+// hipFree / hipModuleUnload from __cxa_finalize then faults (profiles/r02az: SIGSEGV in
+// __cxa_finalize after rocprofv3's finalisation).  rq_shutdown() releases everything explicitly.
 std::mutex g_ctx_mu;
-std::map<int, std::unique_ptr<DevCtx>> g_ctx;
+std::map<int, std::unique_ptr<DevCtx>>& g_ctx = *new std::map<int, std::unique_ptr<DevCtx>>();
 
 int current_device(int* dev) {
     if (g_device < 0) {
@@ -287,8 +346,15 @@ struct CacheHdr {
     uint32_t n_out, n_slots, n_ins, waves_per_cu, name_len, n_rows;
     uint64_t co_len;
     MProg::Stats st;
+    uint64_t body_hash;  // FNV-1a of the name, code object and row table (checked on load)
 };
-constexpr char CACHE_MAGIC[9] = "RQCO0002";
+constexpr char CACHE_MAGIC[9] = "RQCO0003";
+
+uint64_t cache_body_hash(const std::string& name, const std::vector<char>& co, const std::vector<uint32_t>& rows) {
+    uint64_t h = fnv1a(name.data(), name.size());
+    h = fnv1a(co.data(), co.size(), h);
+    return fnv1a(rows.data(), rows.size() * 4, h);
+}
 
 bool cache_load(const std::string& path, CacheHdr* h, std::string* name, std::vector<char>* co,
                 std::vector<uint32_t>* rows) {
@@ -305,13 +371,21 @@ bool cache_load(const std::string& path, CacheHdr* h, std::string* name, std::ve
              std::fread(rows->data(), 4, h->n_rows, f) == h->n_rows;
     }
     std::fclose(f);
+    // a torn or corrupted entry (the lengths can still look right) is dropped and rebuilt
+    if (ok && cache_body_hash(*name, *co, *rows) != h->body_hash) ok = false;
+    if (!ok) std::remove(path.c_str());
     return ok;
 }
 
 void cache_store(const std::string& path, const CacheHdr& h, const std::string& name, const std::vector<char>& co,
                  const std::vector<uint32_t>& rows) {
     ::mkdir(cache_dir().c_str(), 0755);
-    const std::string tmp = path + ".tmp" + std::to_string(::getpid());
+    // unique per process, thread and call: the per-device compiles of one process (run_sharded threads)
+    // may miss on the same key at the same time
+    static std::atomic<uint64_t> seq{0};
+    const std::string tmp = path + ".tmp" + std::to_string(::getpid()) + "." +
+                            std::to_string(std::hash<std::thread::id>()(std::this_thread::get_id())) + "." +
+                            std::to_string(seq++);
     FILE* f = std::fopen(tmp.c_str(), "wb");
     if (!f) return;
     const bool ok = std::fwrite(&h, sizeof h, 1, f) == 1 && std::fwrite(name.data(), 1, name.size(), f) == name.size() &&
@@ -358,7 +432,18 @@ int get_col_kernel(DevCtx* ctx, const Params& p, const uint32_t* esi, uint32_t n
         CacheHdr ch;
         std::string kname;
         std::vector<char> co;
-        if (path.empty() || !cache_load(path, &ch, &kname, &co, &k->src_rows)) {
+        bool cached = !path.empty() && cache_load(path, &ch, &kname, &co, &k->src_rows);
+        if (cached && (hipModuleLoadData(&k->mod, co.data()) != hipSuccess ||
+                       hipModuleGetFunction(&k->fn, k->mod, kname.c_str()) != hipSuccess)) {
+            // a cached object the runtime refuses: drop the entry and build the program afresh
+            (void)hipGetLastError();
+            if (k->mod) (void)hipModuleUnload(k->mod);
+            k->mod = nullptr;
+            k->fn = nullptr;
+            std::remove(path.c_str());
+            cached = false;
+        }
+        if (!cached) {
             ColIR ir;
             std::string err;
             MProg mp;
@@ -385,12 +470,13 @@ int get_col_kernel(DevCtx* ctx, const Params& p, const uint32_t* esi, uint32_t n
             ch.name_len = (uint32_t)kname.size();
             ch.co_len = co.size();
             ch.st = mp.st;
+            ch.body_hash = cache_body_hash(kname, co, k->src_rows);
+            if (hipModuleLoadData(&k->mod, co.data()) != hipSuccess ||
+                hipModuleGetFunction(&k->fn, k->mod, kname.c_str()) != hipSuccess) {
+                ctx->colk.erase(key);
+                return fail(RQ_ERR_DEVICE, "hipModuleLoadData/GetFunction failed for the column program");
+            }
             if (!path.empty()) cache_store(path, ch, kname, co, k->src_rows);
-        }
-        if (hipModuleLoadData(&k->mod, co.data()) != hipSuccess ||
-            hipModuleGetFunction(&k->fn, k->mod, kname.c_str()) != hipSuccess) {
-            ctx->colk.erase(key);
-            return fail(RQ_ERR_DEVICE, "hipModuleLoadData/GetFunction failed for the column program");
         }
         k->n_out = ch.n_out;
         k->n_slots = ch.n_slots;
@@ -798,6 +884,8 @@ int decode_begin(DevCtx* ctx, DecodeJob* j, const uint32_t* n_erased, PackOut* p
     j->cnt.assign(n_blocks, 0);
     for (uint32_t b = 0; b < n_blocks; ++b) {
         const uint32_t e = n_erased[b], nr = j->n_repair[b];
+        // the solvers keep a received repair's index within its block as uint16 (rowid / xpiv)
+        if (nr > 65535) return fail(RQ_ERR_UNSUPPORTED, "more than 65535 received repair symbols in one block");
         for (uint32_t i = j->eoff[b]; i < j->eoff[b + 1]; ++i)
             if (j->erased[i] >= j->p.K) return fail(RQ_ERR_BAD_ARG, "erased ESI >= K");
         for (uint32_t i = j->roff[b]; i < j->roff[b + 1]; ++i)
@@ -1241,6 +1329,37 @@ int rq_device_count(void) {
     return n;
 }
 
+int rq_debug_tuple(uint32_t K, uint32_t X, uint32_t out[6]) {
+    Params p;
+    const int rc = params_for_K(K, &p);
+    if (rc) return fail(rc, "k is too big");
+    const Tuple t = tuple_of(p, X);
+    const uint32_t v[6] = {t.d, t.a, t.b, t.d1, t.a1, t.b1};
+    std::memcpy(out, v, sizeof v);
+    return RQ_OK;
+}
+
+int rq_stream_release(void* stream) {
+    DevCtx* ctx;
+    int rc = get_ctx(&ctx);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (ctx->internal(stream)) return fail(RQ_ERR_BAD_ARG, "not a caller stream");
+    ctx->release_ws(stream);
+    return RQ_OK;
+}
+
+int rq_shutdown(void) {
+    std::lock_guard<std::mutex> lk(g_ctx_mu);
+    for (auto& kv : g_ctx) {
+        std::lock_guard<std::mutex> l2(kv.second->mu);
+        std::unique_ptr<DevCtx> c = std::move(kv.second);
+        c.reset();  // ~DevCtx: device sync, then every buffer, module, stream and event of the device
+    }
+    g_ctx.clear();
+    return RQ_OK;
+}
+
 int rq_set_device(int device) {
     const int n = rq_device_count();
     if (device < 0 || device >= n) return fail(RQ_ERR_DEVICE, "bad device index");
@@ -1362,7 +1481,8 @@ uint32_t rq_debug_decode_margin(uint32_t margin) {
 
 int rq_encode_batch(const rq_encode_desc* d) {
     if (!d || d->T == 0) return fail(RQ_ERR_SYMBOL_SIZE_ZERO, "symbol size cannot be zero");
-    if (d->T % 4 || d->K == 0 || (!d->src && d->n_blocks)) return fail(RQ_ERR_BAD_ARG, "bad encode descriptor (T % 4, K, src)");
+    if (d->T % 4 || d->T < 8 || d->K == 0 || (!d->src && d->n_blocks))
+        return fail(RQ_ERR_BAD_ARG, "bad encode descriptor (T: a multiple of 4, at least 8; K; src)");
     if (d->n_blocks == 0 || d->n_esi == 0) return RQ_OK;
     if (!d->esi || !d->out) return fail(RQ_ERR_BAD_ARG, "n_esi without esi/out");
     if (d->src_stride < (uint64_t)d->K * d->T || d->out_stride < (uint64_t)d->n_esi * d->T)
@@ -1379,7 +1499,7 @@ int rq_encode_batch(const rq_encode_desc* d) {
 
 int rq_decode_batch(const rq_decode_desc* d) {
     if (!d || d->T == 0) return fail(RQ_ERR_SYMBOL_SIZE_ZERO, "symbol size cannot be zero");
-    if (d->T % 4 || d->K == 0) return fail(RQ_ERR_BAD_ARG, "bad decode descriptor (T % 4, K)");
+    if (d->T % 4 || d->T < 8 || d->K == 0) return fail(RQ_ERR_BAD_ARG, "bad decode descriptor (T: a multiple of 4, at least 8; K)");
     if (d->n_blocks == 0) return RQ_OK;
     Params p;
     int rc = params_for_K(d->K, &p);
@@ -1393,7 +1513,7 @@ int rq_decode_batch(const rq_decode_desc* d) {
 
 int rq_decode_batch_async(const rq_decode_desc* d) {
     if (!d || d->T == 0) return fail(RQ_ERR_SYMBOL_SIZE_ZERO, "symbol size cannot be zero");
-    if (d->T % 4 || d->K == 0) return fail(RQ_ERR_BAD_ARG, "bad decode descriptor (T % 4, K)");
+    if (d->T % 4 || d->T < 8 || d->K == 0) return fail(RQ_ERR_BAD_ARG, "bad decode descriptor (T: a multiple of 4, at least 8; K)");
     if (d->n_blocks == 0) return RQ_OK;
     hipPointerAttribute_t pa;
     if (!d->status || hipPointerGetAttributes(&pa, d->status) != hipSuccess || pa.type != hipMemoryTypeHost) {

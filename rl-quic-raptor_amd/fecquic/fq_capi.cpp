@@ -105,9 +105,10 @@ int fq_test_ingest_full(const char* dir, uint32_t iters) {
 }
 
 // TestRXBudgetDropsRepairs (rxbuf_test.go:66-100): budget 3 KiB, K=6 systematic symbols then 2000
-// repairs (in bursts of `burst` with 2 ms pauses when burst > 0, so the ring does not overflow and
-// the classifier's budget rule is what drops them); out = {drops_repairs, drops_system,
-// budget_drop_repairs}.
+// repairs; out = {drops_repairs, drops_system, budget_drop_repairs}.  burst > 0: the repairs come in
+// bursts of `burst` with 2 ms pauses, so the ring does not overflow and the classifier's budget rule
+// is what drops them -- with K=64 there, so that the block cannot complete during the flood (a
+// completed block's late symbols are dropped at ingest instead, fq_test_guards).
 int fq_test_budget(const char* dir, uint32_t burst, int64_t out[3]) {
     RxOptions o;
     o.budget_bytes = 3 * 1024;
@@ -116,14 +117,14 @@ int fq_test_budget(const char* dir, uint32_t burst, int64_t out[3]) {
     o.max_n = 4096;  // staging room beyond the budget, as the reference's slab pool is unbounded
     o.max_blocks = 4;
     o.decode = false;
-    RxManager m(4096, 256, std::string(dir) + "/budget.recv", o);
+    const uint32_t K = burst ? 64 : 6, N = 2 * K, ds = K * 256;
+    RxManager m(burst ? ds : 4096, 256, std::string(dir) + "/budget.recv", o);
     if (m.start() != 0) return -1;
     std::vector<uint8_t> payload(256);
-    const uint32_t K = 6;
     for (uint32_t i = 0; i < K; ++i)
-        if (!m.ingest(0, i, 12, K, payload.data(), 256, 1536)) return -2;
+        if (!m.ingest(0, i, N, K, payload.data(), 256, ds)) return -2;
     for (uint32_t i = 0; i < 2000; ++i) {
-        (void)m.ingest(0, K + i, 12, K, payload.data(), 256, 1536);
+        (void)m.ingest(0, K + i, N, K, payload.data(), 256, ds);
         if (burst && i % burst == burst - 1) std::this_thread::sleep_for(std::chrono::milliseconds(2));
     }
     std::this_thread::sleep_for(std::chrono::milliseconds(50));
@@ -154,6 +155,36 @@ int fq_test_ready(const char* dir, int held, int wait_ms, int64_t out[4]) {
     out[1] = m.stats.queued_by_ddl.load();
     out[2] = m.stats.add_sym_count.load();
     out[3] = m.stats.decode_attempts.load();
+    uint8_t sha[32] = {};
+    (void)m.close_and_finalize(sha, nullptr);
+    return 0;
+}
+
+// Ingest guards (network input is untrusted): staging slots are sized from the first header (N=8,
+// L=16: 8 rows per slot).  Block 0 (K=4, every source) is decoded on the fast path and written; a
+// late repair of it must then be dropped instead of re-creating the block in a fresh slot.  A block
+// whose header claims K=40 (more rows than a slot holds), and one with N < K, must be dropped
+// without touching the arena.  out = {late symbol accepted, drop_after_q_rep, staging_drops,
+// oversized/short header accepted}.
+int fq_test_guards(const char* dir, int64_t out[4]) {
+    RxOptions o;
+    o.decode = false;
+    o.ready = RxOptions::READY_HELD;
+    o.ddl_ms = 20;
+    o.max_blocks = 4;
+    RxManager m(64 * 16, 16, std::string(dir) + "/guard.recv", o);
+    if (m.start() != 0) return -1;
+    std::vector<uint8_t> payload(16, 7);
+    for (uint32_t i = 0; i < 4; ++i)
+        if (!m.ingest(0, i, 8, 4, payload.data(), 16, 64)) return -2;
+    for (int w = 0; w < 100 && m.written() < 64; ++w) std::this_thread::sleep_for(std::chrono::milliseconds(5));
+    if (m.written() < 64) return -3;
+    out[0] = m.ingest(0, 5, 8, 4, payload.data(), 16, 64) ? 1 : 0;
+    out[1] = m.stats.drop_after_q_rep.load();
+    const bool big = m.ingest(1, 0, 48, 40, payload.data(), 16, 640);   // K_lib = 40 > 8 rows
+    const bool shortn = m.ingest(2, 0, 2, 4, payload.data(), 16, 64);   // N < K
+    out[2] = m.stats.staging_drops.load();
+    out[3] = (big ? 1 : 0) + (shortn ? 1 : 0);
     uint8_t sha[32] = {};
     (void)m.close_and_finalize(sha, nullptr);
     return 0;

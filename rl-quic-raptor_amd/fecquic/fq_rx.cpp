@@ -133,8 +133,19 @@ bool RxManager::ingest(uint32_t block_id, uint32_t esi, uint32_t N, uint32_t K, 
         }
         auto f = blocks_.find(block_id);
         Block* b = f == blocks_.end() ? nullptr : f->second;
+        if (!b && finished_.count(block_id)) {
+            // a late or reordered symbol of a block already written: the reference re-creates the block
+            // (rxbuf.go:437); here that would pin a staging slot that never decodes, so it is dropped
+            if (repair_wire) { stats.drop_after_q_rep++; stats.drops_repairs++; }
+            else { stats.drop_after_q_sys++; stats.drops_system++; }
+            return false;
+        }
         if (!b) {
-            if (free_slots_.empty() || len != L_ || data_size == 0) {
+            // the header's own sizes must fit the block's staging slot (sized from the first header):
+            // the library K = ceil(data_size / L) source rows, and N >= K on the wire
+            const uint64_t k_lib = data_size ? ((uint64_t)data_size + L_ - 1) / L_ : 0;
+            if (free_slots_.empty() || len != L_ || data_size == 0 || N < K ||
+                std::max<uint64_t>(N, k_lib) * L_ > slot_bytes_) {
                 stats.staging_drops++;
                 if (repair_wire) stats.drops_repairs++;
                 else stats.drops_system++;
@@ -400,6 +411,7 @@ void RxManager::release(Block* b) {
     in_use_ -= (int64_t)b->bytes;
     auto f = blocks_.find(b->id);
     if (f != blocks_.end() && f->second == b) blocks_.erase(f);
+    finished_.insert(b->id);
     free_slots_.push_back(b->slot);
     delete b;
 }

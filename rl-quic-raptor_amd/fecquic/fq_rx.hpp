@@ -128,6 +128,7 @@ private:
     std::vector<uint32_t> free_slots_;
     std::mutex mu_;
     std::map<uint32_t, Block*> blocks_;
+    std::unordered_set<uint32_t> finished_;  // ids of blocks already written (their late symbols drop)
     Ring ring_;
     std::atomic<int64_t> in_use_{0};
     std::atomic<uint64_t> written_{0};

@@ -42,7 +42,7 @@ EXPORTED = (
     "rq_encode_batch", "rq_decode_batch", "rq_decode_batch_async", "rq_encode_batch_host", "rq_decode_batch_host", "rq_device_count", "rq_set_device",
     "rq_debug_colprog_eval", "rq_debug_colprog_emulate", "rq_debug_colprog_assemble", "rq_debug_decode_margin",
     "rq_decode_blocks_host", "rq_host_alloc", "rq_host_free", "rq_debug_colprog_passes",
-    "rq_debug_shard_plan", "rq_debug_virtual_shards",
+    "rq_debug_shard_plan", "rq_debug_virtual_shards", "rq_debug_tuple", "rq_stream_release", "rq_shutdown",
 )
 
 
@@ -135,6 +135,9 @@ def lib():
             "rq_debug_shard_plan": ([ctypes.c_uint32, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ip, u32p, u32p,
                                      ctypes.c_uint32], ctypes.c_int),
             "rq_debug_virtual_shards": ([ctypes.c_uint32], ctypes.c_uint32),
+            "rq_debug_tuple": ([ctypes.c_uint32, ctypes.c_uint32, u32p], ctypes.c_int),
+            "rq_stream_release": ([vp], ctypes.c_int),
+            "rq_shutdown": ([], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)

@@ -31,6 +31,7 @@ def fq(rq):  # rq: builds the package (librqhip.so and friends) on demand
     L.fq_test_ingest_full.argtypes = [ctypes.c_char_p, ctypes.c_uint32]
     L.fq_test_budget.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_int64)]
     L.fq_test_ready.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]
+    L.fq_test_guards.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]
     return L
 
 
@@ -118,3 +119,13 @@ def test_readiness_rules(fq, tmp_path):
     assert out[0] == 0 and out[1] >= 2 and out[2] == 32 and out[3] == 0
     assert fq.fq_test_ready(str(tmp_path).encode(), 1, 60, out) == 0
     assert out[0] == 1 and out[2] >= 26 and out[3] == 1
+
+
+def test_ingest_guards(fq, tmp_path):
+    """Untrusted headers: a block whose header claims more source rows than the staging slot holds
+    (slots are sized from the first header), or N < K, is dropped before anything is copied; a late
+    symbol of a block already written is dropped rather than re-creating the block in a fresh slot."""
+    out = (ctypes.c_int64 * 4)()
+    assert fq.fq_test_guards(str(tmp_path).encode(), out) == 0
+    assert out[0] == 0 and out[1] == 1   # late repair of the written block: dropped, counted
+    assert out[2] >= 2 and out[3] == 0   # oversized and short-N headers: dropped at staging

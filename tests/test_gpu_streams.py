@@ -1,0 +1,97 @@
+"""Per-stream device state of the batched device-resident calls: a caller that uses a fresh stream per
+window (a fecquic-style pipeline; go/fecquic/rxbuf.go:336-377 runs repeated worker decodes) must not
+grow device memory without bound (rq_engine.cpp DevCtx::MAX_WS = 8 caller-stream workspaces, LRU), the
+results must not depend on the stream, rq_stream_release frees a stream's workspace, and rq_shutdown
+releases everything and the next call starts afresh."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+K, T, N, NB = 256, 1200, 282, 64
+
+
+def _case(gpu, rq, seed):
+    g = torch.Generator(device=gpu).manual_seed(seed)
+    src = torch.randint(0, 256, (NB, K * T), dtype=torch.uint8, device=gpu, generator=g)
+    rng = np.random.default_rng(seed)
+    er, rl = [], []
+    for _ in range(NB):
+        lost = set(rng.choice(N, 14, replace=False).tolist())
+        er.append(sorted(i for i in lost if i < K))
+        rl.append([e for e in range(K, N) if e not in lost])
+    return src, er, rl
+
+
+def _round(gpu, rq, src, er, rl, stream):
+    esis = list(range(K, N))
+    rep = torch.empty((NB, (N - K) * T), dtype=torch.uint8, device=gpu)
+    with torch.cuda.stream(stream):
+        rq.encode_batch(src, K, T, esis, rep, stream=stream)
+        rv = rep.view(NB, N - K, T)
+        recv = torch.cat([rv[b, [e - K for e in rl[b]]] for b in range(NB)])
+        data = src.clone()
+        for b in range(NB):
+            for i in er[b]:
+                data[b, i * T:(i + 1) * T] = 0x33
+        st = rq.DecodeBatch(K, T, er, rl).run(data, recv, stream=stream)
+    stream.synchronize()
+    return rep.cpu(), data.cpu(), st
+
+
+def _used():
+    free, total = torch.cuda.mem_get_info()
+    return total - free
+
+
+def test_64_streams_bounded_and_identical(gpu, rq):
+    src, er, rl = _case(gpu, rq, 17)
+    ref_rep, ref_data, ref_st = _round(gpu, rq, src, er, rl, torch.cuda.Stream())
+    assert (ref_st == 1).all() and torch.equal(ref_data, src.cpu())
+    streams = [torch.cuda.Stream() for _ in range(64)]
+    used = []
+    for i, s in enumerate(streams):
+        rep, data, st = _round(gpu, rq, src, er, rl, s)
+        assert torch.equal(rep, ref_rep) and torch.equal(data, ref_data) and np.array_equal(st, ref_st), i
+        used.append(_used())
+    # one workspace here is ~10 MB (64 blocks K=256); at most 8 caller streams keep one, so from the 9th
+    # stream on device memory stays flat: the stated bound is 64 MiB of growth over streams 16..64
+    # (allocator noise), against ~55 x 10 MB = 550 MB without the bound
+    grow = max(used[15:]) - used[15]
+    assert grow < 64 << 20, (grow, used[::8])
+
+
+def test_stream_release_and_shutdown(gpu, rq):
+    src, er, rl = _case(gpu, rq, 23)
+    s = torch.cuda.Stream()
+    ref_rep, ref_data, _ = _round(gpu, rq, src, er, rl, s)
+    before = _used()
+    assert rq.lib().rq_stream_release(ctypes.c_void_p(s.cuda_stream)) == 0
+    torch.cuda.synchronize()
+    assert _used() <= before
+    assert rq.lib().rq_shutdown() == 0  # every device resource released ...
+    rep, data, st = _round(gpu, rq, src, er, rl, torch.cuda.Stream())  # ... and re-created on demand
+    assert torch.equal(rep, ref_rep) and torch.equal(data, ref_data) and (st == 1).all()
+
+
+def test_device_resident_symbol_size_limit(gpu, rq):
+    """Device-resident batches take T a multiple of 4 and at least 8 (documented in rqhip.h); T=4 is
+    refused with RQ_ERR_BAD_ARG instead of failing inside the launch, and the host-memory batch (which
+    pads rows) still encodes T=4 blocks."""
+    Ks = 16
+    src = torch.randint(0, 256, (2, Ks * 4), dtype=torch.uint8, device=gpu)
+    out = torch.empty((2, 4 * 4), dtype=torch.uint8, device=gpu)
+    with pytest.raises(rq.RaptorQError) as e:
+        rq.encode_batch(src, Ks, 4, list(range(Ks, Ks + 4)), out)
+    assert e.value.code == rq.RQ_ERR_BAD_ARG
+    hsrc = src.cpu().pin_memory()
+    hout = torch.empty((2, 16), dtype=torch.uint8).pin_memory()
+    rq.encode_batch_host(hsrc, Ks, 4, list(range(Ks, Ks + 4)), hout)
+    o8 = torch.empty((2, 4 * 8), dtype=torch.uint8, device=gpu)
+    s8 = torch.zeros((2, Ks * 8), dtype=torch.uint8, device=gpu)
+    s8.view(2, Ks, 8)[:, :, :4] = src.view(2, Ks, 4)
+    rq.encode_batch(s8, Ks, 8, list(range(Ks, Ks + 4)), o8)  # the same bytes, padded to T=8 by hand
+    assert torch.equal(hout, o8.view(2, 4, 8)[:, :, :4].reshape(2, 16).cpu())

@@ -85,3 +85,42 @@ def test_device_mask_errors_and_virtual_shards(rq):
     plan = rq.shard_plan(1 << 2, 8, 10, virtual_shards=3)  # one device, three host threads
     assert plan == [(2, 0, 3), (2, 3, 6), (2, 6, 10)]
     assert rq.shard_plan(0x6, 8, 10, virtual_shards=3) == [(1, 0, 5), (2, 5, 10)]  # multi-device: ignored
+
+
+# ---- bench.py --gpus N: the launcher spawns N ranks itself (rank r on GPU r) when no launcher did ----
+def _bench(*args, env=None):
+    import json
+    import subprocess
+    e = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    e.update(env or {})
+    out = subprocess.run([sys.executable, str(ROOT / "bench.py"), *args], capture_output=True, text=True, env=e,
+                         timeout=300, check=True).stdout
+    return json.loads(out.strip().splitlines()[-1])
+
+
+def test_bench_gpus_plan_weak():
+    plan = _bench("--gpus", "2", "--plan-only")
+    assert plan["world"] == 2 and plan["launcher"] == "spawn" and plan["scaling"] == "weak"
+    assert [(r["rank"], r["device"], r["first_block"], r["blocks"]) for r in plan["ranks"]] == \
+        [(0, 0, 0, 1024), (1, 1, 1024, 1024)]
+
+
+@pytest.mark.parametrize("n", [1, 2, 4, 8])
+def test_bench_gpus_plan_strong_config4(n):
+    """BASELINE config 4: 8192 blocks sharded over N GPUs, every block exactly once."""
+    plan = _bench("--gpus", str(n), "--total-blocks", "8192", "--plan-only")
+    assert plan["world"] == n and plan["scaling"] == "strong"
+    assert [r["device"] for r in plan["ranks"]] == list(range(n))
+    covered = [b for r in plan["ranks"] for b in range(r["first_block"], r["first_block"] + r["blocks"])]
+    assert covered == list(range(8192))
+
+
+def test_bench_rank_env_and_external_launcher():
+    sys.path.insert(0, str(ROOT))
+    import bench
+    env = bench.rank_env(4, 3, 29555)
+    assert (env["RANK"], env["LOCAL_RANK"], env["WORLD_SIZE"], env["MASTER_ADDR"], env["MASTER_PORT"]) == \
+        ("3", "3", "4", "127.0.0.1", "29555")
+    # under torch.distributed.run the environment already names the world: no spawning
+    plan = _bench("--gpus", "2", "--plan-only", env={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert plan["launcher"] == "external"

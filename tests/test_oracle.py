@@ -157,3 +157,26 @@ def test_add_symbol_bool_semantics(oracle):
     assert dec.add_symbol(3, enc.gen_symbol(3).tobytes())  # duplicate, still >= K
     with pytest.raises(ValueError, match="incorrect symbol size 15, should be 16"):
         dec.add_symbol(40, b"x" * 15)
+
+
+@pytest.mark.parametrize("K,Kp,mean", [(64, 69, 7.19), (256, 257, 7.00), (1024, 1032, 7.14)])
+def test_mean_lt_weight_independent_figure(oracle, rq, K, Kp, mean):
+    """Cross-check of the tuple transcription against a figure computed independently of both
+    transcriptions: the mean LT weight d + d1 per repair tuple over 2000 repair ISIs (ISI K'..K'+1999,
+    i.e. ESIs K..K+1999; SURVEY.md sec. 8 after the parameter table: 7.19 at K'=69, 7.00 at K'=257,
+    7.14 at K'=1032), for the oracle (rq_oracle.c) and the engine's own tuple (rq_core.hpp tuple_of,
+    exported as rq_debug_tuple), which must also agree tuple for tuple."""
+    import ctypes
+    prm, pv = oracle.params(K * 1200, 1200)
+    assert prm["Kp"] == Kp
+    isis = range(Kp, Kp + 2000)
+    w_oracle = [t[0] + t[3] for t in (oracle.tuple_(pv, X) for X in isis)]
+    out = (ctypes.c_uint32 * 6)()
+    w_engine = []
+    for X in isis:
+        assert rq.lib().rq_debug_tuple(K, X, out) == 0
+        w_engine.append(out[0] + out[3])
+        assert list(out) == list(oracle.tuple_(pv, X)), X
+    # the survey quotes two decimals (7.005 at K'=257 prints as 7.00 there)
+    assert abs(sum(w_oracle) / 2000 - mean) <= 0.0051
+    assert abs(sum(w_engine) / 2000 - mean) <= 0.0051
