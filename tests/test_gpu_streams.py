@@ -42,7 +42,9 @@ def _round(gpu, rq, src, er, rl, stream):
     return rep.cpu(), data.cpu(), st
 
 
-def _used():
+def _used():  # device memory in use, torch's per-stream allocator caches emptied first
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
     free, total = torch.cuda.mem_get_info()
     return total - free
 
