@@ -603,7 +603,8 @@ struct Policy {
 // Diagnostic builds (wrong bytes, timing only): RQHIP_DIAG bit 1 drops global scratch traffic,
 // 2 drops LDS spill traffic, 4 replaces source loads by register writes, 8 drops output stores,
 // 16 loads source rows in increasing row order (wrong rows; measures the cost of the random order),
-// 32 drops the XOR / xtime instructions (memory traffic and register moves only).
+// 32 drops the XOR / xtime instructions (memory traffic and register moves only), 64 drops the vmcnt
+// waits (loads then race their uses: wrong bytes, but every address stays valid).
 static uint32_t diag_mask() {
     const char* e = knob("RQHIP_DIAG");
     return e ? (uint32_t)std::atoi(e) : 0u;
@@ -720,7 +721,40 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
                 l.replace(at, std::strlen(nm.first), "v" + std::to_string(nm.second));
         line(l.c_str());
     };
-    for (const char* p : pro_once) put(p);
+    const uint32_t W = std::max<uint32_t>(1, mp.wg_waves);
+    const uint32_t LB = mp.n_lds_slots * 256u;  // LDS bytes per wave
+    if (W == 1) {
+        for (const char* p : pro_once) put(p);
+    } else {
+        // W waves per workgroup (one per SIMD of a CU) take W consecutive items, i.e. the W x 256-B
+        // pieces of the same source rows (1 KiB at W = 4), which then reach the memory system close
+        // together.  Wave w of the workgroup: LDS slots at w * LB (folded into V_SCROFF, the lane's
+        // LDS / scratch voffset), scratch of global wave (wg * W + w), its base moved back by w * LB
+        // because V_SCROFF carries that LDS offset too.
+        for (const char* p : pro_once) {
+            const std::string l(p);
+            if (l.rfind("v_lshlrev_b32_e32 V_SCROFF", 0) == 0 || l.rfind("v_add_u32_e32 V_LDS2", 0) == 0 ||
+                l.rfind("s_mul_i32 s32", 0) == 0 || l.rfind("s_mul_hi_u32 s33", 0) == 0)
+                continue;
+            if (l.rfind("s_add_u32 s32, s8, s32", 0) == 0) {
+                put("v_lshrrev_b32_e32 v1, 6, v0");
+                line("s_nop 4");  // VALU write -> v_readfirstlane of it (a missing wait state read v1 stale)
+                line("v_readfirstlane_b32 s53, v1");
+                put("v_and_b32_e32 v0, 63, v0");
+                put("v_lshlrev_b32_e32 V_SCROFF, 2, v0");
+                std::snprintf(buf, sizeof buf, "s_mul_i32 s41, s53, %u", LB); line(buf);
+                put("v_add_u32_e32 V_SCROFF, s41, V_SCROFF");
+                put("v_add_u32_e32 V_LDS2, 0x10000, V_SCROFF");
+                std::snprintf(buf, sizeof buf, "s_mul_i32 s42, s2, %u", W); line(buf);
+                line("s_add_u32 s42, s42, s53");
+                line("s_mul_i32 s32, s42, s16");
+                line("s_mul_hi_u32 s33, s42, s16");
+                line("s_sub_u32 s32, s32, s41");
+                line("s_subb_u32 s33, s33, 0");
+            }
+            put(p);
+        }
+    }
     // Scratch slot s sits at soffset 4096 * (s / 16) + offset (s % 16) * 256: soffset 0 or one of
     // SCR_BASES SGPRs s56.. loaded once, so a spill or reload carries no SALU; slots beyond them
     // (very large K) form their soffset with an s_mov.
@@ -730,7 +764,19 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
         line(buf);
     }
     s += ".Lloop:\n";
-    for (const char* p : pro_iter) put(p);
+    for (const char* p : pro_iter) {
+        const std::string l(p);
+        if (W > 1 && l.rfind("s_lshl_b32 s20, s39, 6", 0) == 0) {  // item = iteration * W + wave
+            std::snprintf(buf, sizeof buf, "s_mul_i32 s39, s39, %u", W); line(buf);
+            line("s_add_u32 s39, s39, s53");
+        }
+        if (W > 1 && l.rfind("v_lshrrev_b32_e32 v0, 2, V_SCROFF", 0) == 0) {  // lane id (V_SCROFF has w * LB)
+            line("v_mbcnt_lo_u32_b32 v0, -1, 0");
+            line("v_mbcnt_hi_u32_b32 v0, -1, v0");
+            continue;
+        }
+        put(p);
+    }
     // Source row j of the program (in issue order) is read at soffset row_off[j] = row * T, a
     // host-built table (colprog_src_rows) streamed into SGPRs 16 entries at a time by s_load_dwordx16,
     // one group ahead: a source load carries no SALU of its own, only one s_load and one
@@ -799,7 +845,9 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
                 if (diag & 4) break;
                 const int q = srot();
                 std::snprintf(buf, sizeof buf, "s_mul_i32 s%d, s12, %u", q, m.imm); line(buf);
-                std::snprintf(buf, sizeof buf, "s_mov_b32 m0, %u", (uint32_t)m.d * 256u); line(buf);
+                if (W > 1) std::snprintf(buf, sizeof buf, "s_add_u32 m0, s41, %u", (uint32_t)m.d * 256u);
+                else std::snprintf(buf, sizeof buf, "s_mov_b32 m0, %u", (uint32_t)m.d * 256u);
+                line(buf);
                 line("s_nop 0");
                 std::snprintf(buf, sizeof buf, "buffer_load_dword v%d, s[24:27], s%d offen%s lds", V_SRCOFF, q, pol.src.c_str());
                 line(buf);
@@ -833,6 +881,7 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
             case MI_ACCR:
                 std::snprintf(buf, sizeof buf, "v_accvgpr_read_b32 v%d, %s", m.d, R(m.a)); line(buf); break;
             case MI_WAIT:
+                if (diag & 64) break;  // diagnostic: no vmcnt waits (wrong bytes; addresses stay valid)
                 std::snprintf(buf, sizeof buf, "s_waitcnt vmcnt(%u)", m.imm); line(buf); break;
             case MI_NOP:
                 std::snprintf(buf, sizeof buf, "s_nop %u", m.imm); line(buf); break;
@@ -852,7 +901,13 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
                 std::snprintf(buf, sizeof buf, "s_waitcnt lgkmcnt(%u)", m.imm); line(buf); break;
         }
     }
-    line("s_waitcnt vmcnt(0) lgkmcnt(0)");
+    // Loop end: no vmcnt drain.  The item's last memory operations are its output stores (every load
+    // has been consumed), and the next item's program may run while they retire: vmcnt waits in it
+    // then also cover these older stores (conservative, still exact), scratch slots are reused in
+    // program order by the same wave (same-address order), and a store has read its data VGPR at
+    // issue.  RQHIP_DRAIN=1 (experiments) restores the full drain.
+    static const bool drain = [] { const char* e = knob("RQHIP_DRAIN"); return e && e[0] == '1'; }();
+    line(drain ? "s_waitcnt vmcnt(0) lgkmcnt(0)" : "s_waitcnt lgkmcnt(0)");
     line("s_add_u32 s52, s52, s49");
     line("s_getpc_b64 s[54:55]");
     s += ".Lpc:\n";
@@ -863,7 +918,7 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
     s += ".Lfunc_end:\n\t.size " + kname + ", .Lfunc_end-" + kname + "\n";
     s += "\t.p2alignl 6, 3212836864\n\t.fill 256, 4, 3212836864\n";
     s += "\t.section .rodata,\"a\",@progbits\n\t.p2align 6, 0x0\n\t.amdhsa_kernel " + kname + "\n";
-    const std::string lds = std::to_string(mp.n_lds_slots * 256u);
+    const std::string lds = std::to_string(mp.n_lds_slots * 256u * W);
     s += "\t\t.amdhsa_group_segment_fixed_size " + lds + "\n\t\t.amdhsa_private_segment_fixed_size 0\n";
     s += "\t\t.amdhsa_kernarg_size 80\n\t\t.amdhsa_user_sgpr_count 2\n";
     s += "\t\t.amdhsa_user_sgpr_kernarg_segment_ptr 1\n\t\t.amdhsa_system_sgpr_workgroup_id_x 1\n";
@@ -874,7 +929,7 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
     s += "\t.amdgpu_metadata\n---\namdhsa.kernels:\n  - .agpr_count: " + std::to_string(n_regs - acc_off) + "\n    .args:\n";
     s += "      - .offset: 0\n        .size: 80\n        .value_kind: by_value\n";
     s += "    .group_segment_fixed_size: " + lds + "\n    .kernarg_segment_align: 8\n    .kernarg_segment_size: 80\n";
-    s += "    .max_flat_workgroup_size: 64\n    .name: " + kname + "\n    .private_segment_fixed_size: 0\n";
+    s += "    .max_flat_workgroup_size: " + std::to_string(64 * W) + "\n    .name: " + kname + "\n    .private_segment_fixed_size: 0\n";
     s += "    .sgpr_count: " + std::to_string(ROW_WIN + 32) + "\n    .symbol: " + kname + ".kd\n    .vgpr_count: " + std::to_string(n_regs) +
          "\n    .wavefront_size: 64\n";
     s += "amdhsa.target: amdgcn-amd-amdhsa--gfx950\namdhsa.version:\n  - 1\n  - 2\n...\n\t.end_amdgpu_metadata\n";

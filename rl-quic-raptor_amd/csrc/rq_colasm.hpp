@@ -72,6 +72,7 @@ struct MProg {
     uint32_t n_agpr = 256;
     uint32_t n_out = 0;
     uint32_t K = 0;
+    uint32_t wg_waves = 1;       // waves per workgroup (emit_colprog_asm): W consecutive items per CU
     struct Stats {
         uint32_t valu = 0, ldsrc = 0, stout = 0, spst = 0, spld = 0, accw = 0, accr = 0, wait = 0, nop = 0;
         uint32_t sync_reload = 0;  // reloads that were not prefetched
@@ -110,8 +111,9 @@ struct ColKernArgs {
     uint32_t scr_per_wave;  // bytes
     uint32_t xcd_q, xcd_n;  // XCD-aware item order: q = items / 8, n = 8q (0, 0 = identity order)
     uint32_t pad;
-    uint32_t n_items;     // 64-column items (waves' worth of work) in this launch
-    uint32_t n_wg;        // persistent grid size: wave w takes items w, w + n_wg, ...
+    uint32_t n_items;     // workgroup iterations: ceil(64-column items / W) (W = MProg::wg_waves)
+    uint32_t n_wg;        // persistent grid size (workgroups): workgroup g takes iterations g, g + n_wg, ...
+                          // and its wave w the item iteration * W + w
     uint64_t row_off;     // uint32 table: soffset of the program's j-th source load (colprog_src_rows[j] * T)
 };
 static_assert(sizeof(ColKernArgs) == 80, "kernarg layout");

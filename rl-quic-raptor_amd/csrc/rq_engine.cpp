@@ -84,6 +84,7 @@ struct ColKernel {
     std::vector<uint32_t> esi;     // outputs (empty: all L intermediate symbols)
     uint32_t n_out = 0, n_slots = 0, n_ins = 0;
     uint32_t waves_per_cu = 4;     // residency of the code object (registers, LDS)
+    uint32_t wg_waves = 1;         // waves per workgroup (MProg::wg_waves)
     MProg::Stats st{};
     uint64_t last_use = 0;         // LRU clock of the per-device cache
     DevBuf mrep;                   // decode: outputs on the identity payload
@@ -343,12 +344,12 @@ uint64_t library_hash() {
 
 struct CacheHdr {
     char magic[8];
-    uint32_t n_out, n_slots, n_ins, waves_per_cu, name_len, n_rows;
+    uint32_t n_out, n_slots, n_ins, waves_per_cu, name_len, n_rows, wg_waves, pad;
     uint64_t co_len;
     MProg::Stats st;
     uint64_t body_hash;  // FNV-1a of the name, code object and row table (checked on load)
 };
-constexpr char CACHE_MAGIC[9] = "RQCO0003";
+constexpr char CACHE_MAGIC[9] = "RQCO0004";
 
 uint64_t cache_body_hash(const std::string& name, const std::vector<char>& co, const std::vector<uint32_t>& rows) {
     uint64_t h = fnv1a(name.data(), name.size());
@@ -394,6 +395,29 @@ void cache_store(const std::string& path, const CacheHdr& h, const std::string& 
     std::fclose(f);
     if (ok) std::rename(tmp.c_str(), path.c_str());
     else std::remove(tmp.c_str());
+}
+
+// Waves per workgroup of a column program.  W = 4 at one wave per SIMD makes the four waves of a CU
+// take four consecutive items, i.e. the four 256-B pieces of the same source rows (1 KiB): the
+// memory-only pattern reads 4.87 -> 5.53 TB/s that way (tools/micro/sync_gen.py), but the full
+// program measured the same for W = 1 / 2 / 4 (0.404-0.414 ms, profiles/r03e), so W = 1 stays the
+// default; RQHIP_WG selects W in experiments builds (parity-tested at W = 4).
+uint32_t colprog_wg_waves(uint32_t waves_per_cu, uint32_t lds_per_wave) {
+    static const int forced = [] { const char* e = knob("RQHIP_WG"); return e ? std::atoi(e) : 0; }();
+    uint32_t w = forced > 0 ? (uint32_t)forced : 1u;  // W = 4 measured neutral in the full program (r03e)
+    while (w > 1 && (waves_per_cu % w || (uint64_t)lds_per_wave * w > 163840u)) w /= 2;
+    return std::max<uint32_t>(1, w);
+}
+
+// Residency (waves per CU, from registers and LDS) of an allocated program; sets its waves per
+// workgroup.  The engine and the debug entry points emit the same code.
+uint32_t colprog_launch_shape(MProg* mp) {
+    const uint32_t regs = colprog_regs(*mp), lds = mp->n_lds_slots * 256u;
+    uint32_t w = 4 * std::max<uint32_t>(1, 512 / regs);
+    if (lds) w = std::min<uint32_t>(w, 163840u / lds);
+    const uint32_t wpc = std::max<uint32_t>(1, std::min<uint32_t>(w, 32));
+    mp->wg_waves = colprog_wg_waves(wpc, lds);
+    return wpc;
 }
 
 // ---------------- column programs (the encode hot path) ----------------
@@ -454,19 +478,18 @@ int get_col_kernel(DevCtx* ctx, const Params& p, const uint32_t* esi, uint32_t n
             }
             // distinct symbol per program so kernel traces separate encode, decode and C programs
             kname = "rq_colprog_K" + std::to_string(p.K) + (all_C ? "_C" : "_n" + std::to_string(n_esi));
+            const uint32_t wpc = colprog_launch_shape(&mp);
             co.clear();
             if (!comgr_assemble(emit_colprog_asm(mp, kname), &co, &err)) { ctx->colk.erase(key); return fail(RQ_ERR_PLAN, err); }
             std::memset(&ch, 0, sizeof ch);
+            ch.waves_per_cu = wpc;
             std::memcpy(ch.magic, CACHE_MAGIC, 8);
             k->src_rows = colprog_src_rows(mp);
             ch.n_rows = (uint32_t)k->src_rows.size();
             ch.n_out = ir.n_out;
             ch.n_slots = mp.n_slots;
             ch.n_ins = (uint32_t)mp.ins.size();
-            const uint32_t regs = colprog_regs(mp), lds = mp.n_lds_slots * 256u;
-            uint32_t w = 4 * std::max<uint32_t>(1, 512 / regs);
-            if (lds) w = std::min<uint32_t>(w, 163840u / lds);
-            ch.waves_per_cu = std::max<uint32_t>(1, std::min<uint32_t>(w, 32));
+            ch.wg_waves = mp.wg_waves;
             ch.name_len = (uint32_t)kname.size();
             ch.co_len = co.size();
             ch.st = mp.st;
@@ -481,6 +504,7 @@ int get_col_kernel(DevCtx* ctx, const Params& p, const uint32_t* esi, uint32_t n
         k->n_out = ch.n_out;
         k->n_slots = ch.n_slots;
         k->waves_per_cu = ch.waves_per_cu;
+        k->wg_waves = std::max<uint32_t>(1, ch.wg_waves);
         k->st = ch.st;
         k->n_ins = ch.n_ins;
         slot = std::move(k);
@@ -512,16 +536,19 @@ int launch_col(DevCtx* ctx, ColKernel* k, uint32_t T, uint32_t n_blocks, const v
     if ((uint64_t)per * src_stride > lim || (uint64_t)per * out_stride > lim)
         return fail(RQ_ERR_UNSUPPORTED, "block stride beyond the 4 GiB buffer-offset range");
     if ((uint64_t)per * Td > 0x7FFFFFFFull) return fail(RQ_ERR_UNSUPPORTED, "batch too large");
+    const uint32_t Wg = k->wg_waves;
     const uint32_t max_items = (uint32_t)(((uint64_t)per * Td + 63) / 64);
-    // persistent grid: at most the resident wave count (scratch is per grid wave; RQHIP_WAVES caps it
-    // in experiments builds)
+    const uint32_t max_iters = (max_items + Wg - 1) / Wg;  // workgroup iterations
+    // persistent grid: at most the resident workgroup count (scratch is per grid wave; RQHIP_WAVES caps
+    // the waves in experiments builds)
     static const uint32_t cap = [] { const char* e = knob("RQHIP_WAVES"); return e ? (uint32_t)std::atoi(e) : 0u; }();
-    const uint32_t resident = cap ? std::min(cap, ctx->n_cu * k->waves_per_cu) : ctx->n_cu * k->waves_per_cu;
-    const uint32_t max_wg = std::min(max_items, resident);
+    const uint32_t resident_w = cap ? std::min(cap, ctx->n_cu * k->waves_per_cu) : ctx->n_cu * k->waves_per_cu;
+    const uint32_t resident = std::max<uint32_t>(1, resident_w / Wg);  // workgroups
+    const uint32_t max_wg = std::min(max_iters, resident);
     const size_t spw = (size_t)std::max<uint32_t>(k->n_slots, 1) * 256;
     int rc;
     Workspace* w = ctx->wsp(stream);
-    if ((rc = w->scratch.ensure(spw * max_wg))) return rc;
+    if ((rc = w->scratch.ensure(spw * max_wg * Wg))) return rc;
     auto& tab = k->row_off[T];
     if (!tab) {  // once per (program, T): the source loads' soffsets, padded to whole 16-entry groups
         std::unique_ptr<DevBuf> b(new DevBuf());
@@ -550,20 +577,20 @@ int launch_col(DevCtx* ctx, ColKernel* k, uint32_t T, uint32_t n_blocks, const v
         if (!divmagic(Td, a.n_cols, &a.magic, &a.shift)) return fail(RQ_ERR_UNSUPPORTED, "no division magic");
         size_t sz = sizeof a;
         void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
-        const uint32_t items = (a.n_cols + 63) / 64;
-        // Balanced rounds: as many waves as spread the items evenly over the rounds the resident set
-        // needs (a multiple of 8 for the XCD remap), not the whole resident set with a partial last
-        // round -- 1024 blocks K=1024 = 4 800 items: 960 waves x 5 instead of 704 x 5 + 320 x 4, the
-        // busy waves then share HBM with fewer others (0.49 -> 0.47 ms, profiles/r02at).
-        const uint32_t rounds = (items + resident - 1) / resident;
-        const uint32_t waves = std::min(resident, ((items + rounds - 1) / rounds + 7) / 8 * 8);
-        a.n_items = items;
-        a.n_wg = waves;
-        if (xcd_order() && waves % 8 == 0) {  // the remap needs the stride to keep w % 8 fixed
-            a.xcd_q = items / 8;
+        const uint32_t items = (a.n_cols + 63) / 64, iters = (items + Wg - 1) / Wg;
+        // Balanced rounds: as many workgroups as spread the iterations evenly over the rounds the
+        // resident set needs (a multiple of 8 for the XCD remap), not the whole resident set with a
+        // partial last round -- 1024 blocks K=1024 = 4 800 items: 960 waves x 5 instead of 704 x 5 +
+        // 320 x 4, the busy waves then share HBM with fewer others (0.49 -> 0.47 ms, profiles/r02at).
+        const uint32_t rounds = (iters + resident - 1) / resident;
+        const uint32_t wgs = std::min(resident, ((iters + rounds - 1) / rounds + 7) / 8 * 8);
+        a.n_items = iters;
+        a.n_wg = wgs;
+        if (xcd_order() && wgs % 8 == 0) {  // the remap needs the stride to keep g % 8 fixed
+            a.xcd_q = iters / 8;
             a.xcd_n = a.xcd_q * 8;
         }
-        HIP_TRY(hipModuleLaunchKernel(k->fn, waves, 1, 1, 64, 1, 1, 0, (hipStream_t)stream, nullptr, cfg));
+        HIP_TRY(hipModuleLaunchKernel(k->fn, wgs, 1, 1, 64 * Wg, 1, 1, 0, (hipStream_t)stream, nullptr, cfg));
     }
     return RQ_OK;
 }
@@ -1433,6 +1460,7 @@ int rq_debug_colprog_emulate(uint32_t K, uint32_t T, const uint32_t* esi, uint32
         std::memcpy(stats, v, sizeof v);
     }
     if (asm_len) {
+        (void)colprog_launch_shape(&mp);
         const std::string a = emit_colprog_asm(mp, "rq_colprog");
         *asm_len = a.size();
         if (asm_buf && asm_cap >= a.size()) std::memcpy(asm_buf, a.data(), a.size());
@@ -1448,6 +1476,7 @@ int rq_debug_colprog_assemble(uint32_t K, const uint32_t* esi, uint32_t n_out, s
     std::string err;
     MProg mp;
     if (!debug_compile(p, esi, n_out, alloc_options(), &ir, &mp, &err)) return fail(RQ_ERR_PLAN, err);
+    (void)colprog_launch_shape(&mp);
     std::vector<char> co;
     if (!comgr_assemble(emit_colprog_asm(mp, "rq_colprog"), &co, &err)) return fail(RQ_ERR_PLAN, err);
     if (code_bytes) *code_bytes = co.size();
