@@ -118,7 +118,7 @@ def pmc_traffic(kernel, K, T, N, B):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary of this exact
     workload (profiles/rNN_traffic.json, written by tools/gpu_profile.sh); (None, None) if absent."""
     def tag_order(path):  # r02y < r02z < r02aa < r02af: round, then the length and letters of the tag
-        m = re.match(r"r(\d+)([a-z]*)_traffic\.json$", path.name)
+        m = re.match(r"r(\d+)([a-z]*)(_k\d+)?_traffic\.json$", path.name)
         return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
     for path in sorted((ROOT / "profiles").glob("r*_traffic.json"), key=tag_order, reverse=True):
         t = json.loads(path.read_text())
@@ -186,6 +186,80 @@ def cpu_baseline(K, T, N, n_erase, n_blocks):
             "reference_go_1core_gbs": 0.094}
 
 
+def cpu_baseline_encode(K, T, esis, n_blocks):
+    """Config 2's CPU baseline: librqcpu.so encode (the same column program on host cores) of a sample of
+    the same workload, 16 threads (the GPU box's CPU share) and 1 thread."""
+    import rqcpu
+    threads = max(1, min(16, os.cpu_count() or 1))
+    rng = np.random.default_rng(4343)
+    src = rng.integers(0, 256, (n_blocks, K * T), dtype=np.uint8)
+    rqcpu.encode(src[:1], K, T, esis)  # program compile outside the timed region, as on the GPU
+    t0 = time.perf_counter()
+    rqcpu.encode(src, K, T, esis, threads)
+    tN = time.perf_counter() - t0
+    n1 = max(8, n_blocks // 8)
+    t0 = time.perf_counter()
+    rqcpu.encode(src[:n1], K, T, esis, 1)
+    t1 = time.perf_counter() - t0
+    gb = lambda nb, t: round(nb * K * T / t / 1e9, 4)
+    return {"value": gb(n_blocks, tN), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": "%d blocks K=%d T=%d, %d repairs, %d threads on '%s': librqcpu.so encode (the engine's column "
+                      "program on host cores, bit-exact to the oracle), %.3f s" % (n_blocks, K, T, len(esis), threads,
+                                                                                 cpu_model(), tN),
+            "one_thread": {"value": gb(n1, t1), "cores": 1, "sample": "%d blocks" % n1}}
+
+
+def cpu_baseline_mixed(shapes, frac_div):
+    """Config 5's CPU baseline: librqcpu.so encode + decode of a sample of every shape of the stream (1 /
+    frac_div of its blocks, at least 2), 16 threads; every decode checked against the source."""
+    import rqcpu
+    threads = max(1, min(16, os.cpu_count() or 1))
+    t_all, nbytes = 0.0, 0
+    for sh in shapes:
+        K, T, B = sh["K"], sh["T"], max(2, sh["B"] // frac_div)
+        src = sh["src"][:B].numpy()
+        esis = sh["esis"]
+        rqcpu.encode(src[:1], K, T, esis)
+        er, rl = sh["er"][:B], sh["rl"][:B]
+        t0 = time.perf_counter()
+        rep = rqcpu.encode(src, K, T, esis, threads)
+        R = len(esis)
+        rows = np.concatenate([rep[b].reshape(R, T)[[e - K for e in rl[b]]] for b in range(B)])
+        data = src.copy()
+        for b in range(B):
+            for i in er[b]:
+                data[b, i * T:(i + 1) * T] = 0
+        st = rqcpu.decode(data, K, T, er, rl, rows, threads)
+        t_all += time.perf_counter() - t0
+        ok = st == 1
+        assert np.array_equal(data[ok], src[ok]), "CPU baseline decode mismatch"
+        nbytes += B * K * T
+    return {"value": round(nbytes / t_all / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": "1/%d of every shape's blocks (>= 2), encode + decode from host memory, %d threads on '%s': "
+                      "librqcpu.so (bit-exact to the oracle)" % (frac_div, threads, cpu_model())}
+
+
+def pcie_copy_peak(dev, mib=256, reps=5):
+    """Pinned host <-> device copy rates on this box (GB/s): the roofline of the host-memory paths."""
+    n = mib << 20
+    h = torch.empty(n, dtype=torch.uint8).pin_memory()
+    d = torch.empty(n, dtype=torch.uint8, device=dev)
+    s = torch.cuda.current_stream(dev)
+    out = {}
+    for name, fn in (("h2d", lambda: d.copy_(h, non_blocking=True)), ("d2h", lambda: h.copy_(d, non_blocking=True))):
+        fn()
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(s)
+        for _ in range(reps):
+            fn()
+        b.record(s)
+        torch.cuda.synchronize()
+        out[name] = n * reps / (a.elapsed_time(b) * 1e-3) / 1e9
+    del h, d
+    return out
+
+
 def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -249,7 +323,9 @@ def run_config2(args):
     total = rqshard.sum_over_ranks(B, dist, coll_dev)
     if rank == 0:
         achieved = B * K * T / (enc_ms * 1e-3) / 1e9
-        print(json.dumps({
+        kname = "rq_colprog_K%d_n%d" % (K, R)
+        traffic, traffic_src = pmc_traffic(kname, K, T, K + R, B)
+        line = {
             "metric": "RaptorQ encode GB/s device-resident, 1024 blocks K=256 T=1200B R=26 (BASELINE config 2)",
             "value": round(total * K * T * args.steps / dt / 1e9, 3), "unit": "GB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
@@ -257,10 +333,14 @@ def run_config2(args):
             "data": "synthetic (seeded torch.randint payload)",
             "config": {"workload": "encode-only K=%d T=%d, %d repairs per block" % (K, T, R), "blocks_per_gpu": B,
                        "verified_blocks_vs_cpu_port": 0 if args.no_verify else 8},
-            "roofline": {"bound": "hbm", "kernel": "rq_colprog_K%d_n%d" % (K, R), "achieved": round(achieved, 2),
+            "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": None, "launch_ms": round(enc_ms, 4),
-                         "achieved_read_write": round(B * (K + R) * T / (enc_ms * 1e-3) / 1e9, 2)}}), flush=True)
+                         "traffic": traffic, "traffic_source": traffic_src, "algorithmic_bytes_per_launch": B * K * T,
+                         "launch_ms": round(enc_ms, 4),
+                         "achieved_read_write": round(B * (K + R) * T / (enc_ms * 1e-3) / 1e9, 2)}}
+        if args.cpu_sample > 0 and world == 1:
+            line["cpu_baseline"] = cpu_baseline_encode(K, T, esis, args.cpu_sample)
+        print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 
@@ -293,7 +373,7 @@ def run_config5(args):
             st = rqhip.decode_batch_host(db, data, repair)
             ok = torch.from_numpy(st == 1)
             assert torch.equal(data[ok], src[ok]), (K, T)
-            shapes.append(dict(K=K, T=T, N=N, B=B, esis=esis, src=src, rep=rep, repair=repair, data=data, db=db,
+            shapes.append(dict(K=K, T=T, N=N, B=B, esis=esis, src=src, rep=rep, repair=repair, data=data, db=db, er=er, rl=rl,
                                ok=float(ok.float().mean()), t_enc=0.0, t_dec=0.0))
 
     def step():
@@ -324,11 +404,16 @@ def run_config5(args):
         assert torch.equal(sh["data"][ok], sh["src"][ok]), (sh["K"], sh["T"])
     src_bytes = sum(sh["B"] * sh["K"] * sh["T"] for sh in shapes)
     total = rqshard.sum_over_ranks(src_bytes, dist, coll_dev)
+    # PCIe bytes of one step (host-memory batch API): encode H2D source, D2H repairs; decode H2D data
+    # blocks + received repair rows, D2H the recovered rows of the blocks that decoded
+    h2d = sum(sh["B"] * sh["K"] * sh["T"] * 2 + sh["repair"].numel() for sh in shapes)
+    d2h = sum(sh["rep"].numel() + sum(len(x) for x in sh["er"]) * sh["T"] for sh in shapes)
+    link = pcie_copy_peak(dev) if rank == 0 else None
     if rank == 0:
         per = [{"K": sh["K"], "T": sh["T"], "N": sh["N"], "blocks": sh["B"], "ok_fraction": sh["ok"],
                 "encode_GBps": round(sh["B"] * sh["K"] * sh["T"] * args.steps / sh["t_enc"] / 1e9, 2),
                 "decode_GBps": round(sh["B"] * sh["K"] * sh["T"] * args.steps / sh["t_dec"] / 1e9, 2)} for sh in shapes]
-        print(json.dumps({
+        line = {
             "metric": "RaptorQ encode+decode GB/s end to end incl. pinned H2D/D2H, mixed K{128,512,2048} x "
                       "T{256,1200} stream at 5% loss (BASELINE config 5)",
             "value": round(total * args.steps / dt / 1e9, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
@@ -336,7 +421,19 @@ def run_config5(args):
             "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (seeded numpy payload, seeded exact-count erasures), pinned host buffers",
             "config": {"workload": "mixed stream, %d MiB of source per shape per step, host-memory batch API" % mb,
-                       "shapes": per}}), flush=True)
+                       "shapes": per},
+            # the path is bound by the PCIe link (pinned copies measured on this box), not HBM: achieved =
+            # H2D bytes per second of the whole stream (the busier direction) against the box's pinned
+            # H2D copy rate; D2H beside it
+            "roofline": {"bound": "pcie", "achieved": round(h2d * args.steps / dt / 1e9, 2),
+                         "peak": round(link["h2d"], 2), "unit": "GB/s",
+                         "frac": round(h2d * args.steps / dt / 1e9 / link["h2d"], 4), "traffic": h2d + d2h,
+                         "h2d_bytes_per_step": h2d, "d2h_bytes_per_step": d2h,
+                         "d2h_achieved": round(d2h * args.steps / dt / 1e9, 2), "d2h_peak": round(link["d2h"], 2),
+                         "peak_source": "torch pinned copy_ of 256 MiB, 5 reps, this box"}}
+        if args.cpu_sample > 0 and world == 1:
+            line["cpu_baseline"] = cpu_baseline_mixed(shapes, max(1, args.cpu_sample // 128))
+        print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 

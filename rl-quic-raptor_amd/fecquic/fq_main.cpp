@@ -3,7 +3,7 @@
 //
 //   fecquic loopback --file F --out PATH [--K 26 --N 32 --L 1200 --drop 0 --seed 1 --window 64
 //                    --transport inproc|udp --ready ref|held --workers 1 --ddl-ms 50 --budget BYTES
-//                    --max-blocks 128 --ring 4096 --header-version 0|1|2 --timeout-s 120]
+//                    --max-blocks 128 --ring 4096 --header-version 0|1|2 --timeout-s 120 --dump PATH]
 //
 // The file header ("QFEC", size, SHA-256, L) travels first on a reliable channel (a TCP connection
 // for --transport udp, standing in for the QUIC stream of transfer.go:94-114), then every symbol as
@@ -164,21 +164,34 @@ int loopback(int argc, char** argv) {
             }
         });
     }
+    // --dump PATH: every datagram the sender emits, as [u32 length][bytes] records (tests compare the
+    // symbols on the wire with the oracle's GenSymbol)
+    const std::string dump_path = arg(argc, argv, "--dump", "");
+    FILE* dump = dump_path.empty() ? nullptr : std::fopen(dump_path.c_str(), "wb");
+    auto dump_dg = [&](const uint8_t* b, size_t n) {
+        if (!dump) return;
+        const uint32_t len = (uint32_t)n;
+        std::fwrite(&len, 4, 1, dump);
+        std::fwrite(b, 1, n, dump);
+    };
     TxStats ts;
     const auto t0 = std::chrono::steady_clock::now();
     int rc;
     if (udp_tx >= 0) {
         rc = send_file(file, to, [&](const uint8_t* b, size_t n) {
+            dump_dg(b, n);
             while (::send(udp_tx, b, n, 0) < 0 && errno == ENOBUFS) std::this_thread::yield();
         }, &ts);
     } else {
         // in-process datagrams with flow control: a full ingest ring makes the sender wait (as a
         // blocking socket would), so the only loss is the sender's --drop
         rc = send_file(file, to, [&](const uint8_t* b, size_t n) {
+            dump_dg(b, n);
             while (rx.ring_full()) std::this_thread::sleep_for(std::chrono::microseconds(50));
             deliver(rx, rh, b, n);
         }, &ts);
     }
+    if (dump) std::fclose(dump);
     // wait until the file is complete (transfer.go:349-359) or the timeout
     while (rc == 0 && rx.written() < rh.file_size &&
            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() < timeout_s)

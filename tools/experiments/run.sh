@@ -22,7 +22,7 @@ for step in "$@"; do
           cp $log/b_kernel_stats.csv $O/kernel_stats_$n.csv 2>/dev/null || find $log -name "*kernel_stats.csv" -exec cp {} $O/kernel_stats_$n.csv \;
           head -6 $O/kernel_stats_$n.csv | cut -d, -f1-4 ;;
     col) timeout -k 10 150 python3 tools/colbench.py ${arg//,/ } > $log.log 2>&1 || { tail -10 $log.log; exit 1; }; grep -h encode $log.log ;;
-    traffic) bash tools/gpu_profile.sh $TAG > $log.log 2>&1 || { tail -10 $log.log; exit 1; }; cp gpurun_out/pmc_traffic/summary.json $O/traffic.json; cat $O/traffic.json ;;
+    traffic) bash tools/gpu_profile.sh $TAG > $log.log 2>&1 || { tail -10 $log.log; exit 1; }; cp gpurun_out/pmc_traffic/summary.json $O/traffic.json; cp gpurun_out/pmc_traffic/summary_k256.json $O/traffic_k256.json; cat $O/traffic.json $O/traffic_k256.json ;;
     sq) timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU SQ_INSTS_LDS \
           --kernel-include-regex rq_colprog --output-format csv -d $log -o sq -- python3 tools/colbench.py ${arg:-1024 1200 1100 1024 3} > $log.log 2>&1 || { tail -5 $log.log; exit 1; } ;;
     py) s=${arg%%:*}; a=""; [ "$arg" != "$s" ] && a=${arg#*:}

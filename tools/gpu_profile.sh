@@ -8,5 +8,6 @@ TAG=${1:-r01}
 mkdir -p gpurun_out/pmc_traffic
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex rq_colprog --output-format csv -d gpurun_out/pmc_traffic/fetch -o fetch -- python3 tools/pmc_workload.py > gpurun_out/pmc_traffic/fetch.log 2>&1 && \
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex rq_colprog --output-format csv -d gpurun_out/pmc_traffic/write -o write -- python3 tools/pmc_workload.py > gpurun_out/pmc_traffic/write.log 2>&1 && \
-python3 tools/prof_summary.py traffic gpurun_out/pmc_traffic $TAG > gpurun_out/pmc_traffic/summary.json
+python3 tools/prof_summary.py traffic gpurun_out/pmc_traffic $TAG > gpurun_out/pmc_traffic/summary.json && \
+python3 tools/prof_summary.py traffic gpurun_out/pmc_traffic $TAG rq_colprog_K256_n26 > gpurun_out/pmc_traffic/summary_k256.json
 echo EXIT $?

@@ -6,6 +6,7 @@
    it reads and writes exactly blocks*10*T bytes and FETCH_SIZE / WRITE_SIZE of that launch calibrate
    the counters for this access width (rq_colprog_K10_n10).
 2. The bench workload's encode launch: K=1024 T=1200 N=1100, 1024 blocks (rq_colprog_K1024_n76).
+3. BASELINE config 2's encode launch: K=256 T=1200, 26 repairs, 1024 blocks (rq_colprog_K256_n26).
 """
 import sys
 from pathlib import Path
@@ -34,7 +35,16 @@ def main():
     for _ in range(3):
         rqhip.encode_batch(src, K, T, list(range(K, N)), rep)
     torch.cuda.synchronize()
-    print("calibration bytes per launch", Bc * 10 * Tc, "encode source bytes per launch", B * K * T)
+    del src, rep
+    # 3. BASELINE config 2's encode launch: K=256 T=1200, 26 repairs, 1024 blocks (rq_colprog_K256_n26)
+    K2, R2 = 256, 26
+    src = torch.randint(0, 256, (B, K2 * T), dtype=torch.uint8, device=dev)
+    rep = torch.empty((B, R2 * T), dtype=torch.uint8, device=dev)
+    for _ in range(3):
+        rqhip.encode_batch(src, K2, T, list(range(K2, K2 + R2)), rep)
+    torch.cuda.synchronize()
+    print("calibration bytes per launch", Bc * 10 * Tc, "encode source bytes per launch", B * K * T, "config 2",
+          B * K2 * T)
 
 
 if __name__ == "__main__":

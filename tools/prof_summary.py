@@ -2,8 +2,9 @@
 
   prof_summary.py trace TRACE_CSV [COUNTER_CSV ...]   per (kernel, grid) count and mean duration,
                                                       plus per-dispatch counter means
-  prof_summary.py traffic DIR TAG                     FETCH_SIZE / WRITE_SIZE passes of
-                                                      tools/gpu_profile.sh (copied to profiles/TAG_traffic.json)
+  prof_summary.py traffic DIR TAG [KERNEL]            FETCH_SIZE / WRITE_SIZE passes of
+                                                      tools/gpu_profile.sh (copied to profiles/TAG_traffic.json;
+                                                      KERNEL rq_colprog_K256_n26: TAG_k256_traffic.json)
 
 FETCH_SIZE / WRITE_SIZE are in KiB.  Calibration (MI355X_MICROARCH.md, HBM section): the counters are
 exact only for some access widths, so each is divided by its ratio on a same-pattern copy launch of
@@ -38,18 +39,25 @@ def counter_means(path):
     return {k: sum(v) / len(v) for k, v in g.items()}
 
 
-def traffic(d, tag):
+WORKLOADS = {  # encode launches of tools/pmc_workload.py: kernel -> (K, T, N, blocks)
+    "rq_colprog_K1024_n76": (1024, 1200, 1100, 1024),  # the bench metric (config 3)
+    "rq_colprog_K256_n26": (256, 1200, 282, 1024),     # BASELINE config 2
+}
+
+
+def traffic(d, tag, enc="rq_colprog_K1024_n76"):
     fetch = counter_means(glob.glob(os.path.join(d, "fetch", "*counter_collection.csv"))[0])
     write = counter_means(glob.glob(os.path.join(d, "write", "*counter_collection.csv"))[0])
     cal_bytes = 65536 * 10 * 1024
-    cal, enc = "rq_colprog_K10_n10", "rq_colprog_K1024_n76"
+    cal = "rq_colprog_K10_n10"
+    K, T, N, B = WORKLOADS[enc]
     f_cal, w_cal = fetch[(cal, "FETCH_SIZE")] / cal_bytes, write[(cal, "WRITE_SIZE")] / cal_bytes
     f_enc, w_enc = fetch[(enc, "FETCH_SIZE")] / f_cal, write[(enc, "WRITE_SIZE")] / w_cal
     out = {
         "kernel": enc,
-        "workload": {"K": 1024, "T": 1200, "N": 1100, "blocks": 1024},
+        "workload": {"K": K, "T": T, "N": N, "blocks": B},
         "fetch_bytes": round(f_enc), "write_bytes": round(w_enc), "traffic_bytes": round(f_enc + w_enc),
-        "algorithmic_bytes": {"read": 1024 * 1024 * 1200, "write": 1024 * 76 * 1200},
+        "algorithmic_bytes": {"read": B * K * T, "write": B * (N - K) * T},
         "calibration": {"kernel": cal, "bytes_read_and_written": cal_bytes, "fetch_ratio": round(f_cal, 4),
                         "write_ratio": round(w_cal, 4)},
         "raw_kib": {"fetch": fetch[(enc, "FETCH_SIZE")] / 1024, "write": write[(enc, "WRITE_SIZE")] / 1024},
@@ -62,7 +70,7 @@ def traffic(d, tag):
 
 if __name__ == "__main__":
     if sys.argv[1] == "traffic":
-        print(json.dumps(traffic(sys.argv[2], sys.argv[3]), indent=1))
+        print(json.dumps(traffic(sys.argv[2], sys.argv[3], *sys.argv[4:5]), indent=1))
     else:
         res = {"trace": trace_summary(sys.argv[2]), "counters": []}
         for p in sys.argv[3:]:
