@@ -91,6 +91,15 @@ def lib():
                 raise RaptorQError(RQ_ERR_DEVICE, "librqhip.so could not be built: %s" % ex) from ex
             if not LIB_PATH.exists():
                 raise RaptorQError(RQ_ERR_DEVICE, "librqhip.so not built (run `make -C rl-quic-raptor_amd`)")
+        # One HIP runtime per process: PyTorch-ROCm bundles its own libamdhip64.so.7 (same soname as
+        # /opt/rocm's).  Loaded first, torch's copy also serves librqhip.so's NEEDED entry; loaded after
+        # librqhip.so, a second runtime initialises the device beside the first and the library's
+        # hipGetDeviceCount then fails (seen on the GPU box, r03h).  The Python mirror exchanges device
+        # tensors and streams with torch, so it loads torch's runtime first when torch is present.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(str(LIB_PATH))
         u8p = ctypes.POINTER(ctypes.c_uint8)
         u16p = ctypes.POINTER(ctypes.c_uint16)
