@@ -722,6 +722,7 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
         line(l.c_str());
     };
     const uint32_t W = std::max<uint32_t>(1, mp.wg_waves);
+    static const uint32_t wgbar = [] { const char* e = knob("RQHIP_WGBAR"); return e ? (uint32_t)std::atoi(e) : 0u; }();
     const uint32_t LB = mp.n_lds_slots * 256u;  // LDS bytes per wave
     if (W == 1) {
         for (const char* p : pro_once) put(p);
@@ -762,6 +763,15 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
     for (uint32_t j = 0; j < n_bases; ++j) {
         std::snprintf(buf, sizeof buf, "s_mov_b32 s%u, %u", 56 + j, 4096u * (j + 1));
         line(buf);
+    }
+    // experiments: RQHIP_STAGGER=n delays the odd workgroups' start by n x 127 x 64 cycles (do the
+    // first rounds' coinciding load bursts cost time?)
+    static const uint32_t stagger = [] { const char* e = knob("RQHIP_STAGGER"); return e ? (uint32_t)std::atoi(e) : 0u; }();
+    if (stagger) {
+        line("s_bitcmp1_b32 s2, 0");
+        line("s_cbranch_scc0 .Lnostagger");
+        for (uint32_t i = 0; i < stagger; ++i) line("s_sleep 127");
+        s += ".Lnostagger:\n";
     }
     s += ".Lloop:\n";
     for (const char* p : pro_iter) {
@@ -835,6 +845,9 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
                         line(buf);
                     }
                 }
+                // W > 1, experiments: an s_barrier every `wgbar` source loads keeps the workgroup's waves
+                // at the same rows (every wave runs this same stream, so the barrier counts match)
+                if (W > 1 && wgbar && src_j && src_j % wgbar == 0) line("s_barrier");
                 ++src_j;
                 std::snprintf(buf, sizeof buf, "buffer_load_dword %s, v%d, s[24:27], s%u offen%s", R(m.d), V_SRCOFF, win + i,
                               pol.src.c_str());
