@@ -743,8 +743,9 @@ uint32_t solve_lds_e_max() {
 // load/store instruction is one contiguous 256-B segment).  The slice's tables are built from X
 // straight into LDS (perm_tables: A = the four 8-entry halves (b128), B = the 2-bit table), for
 // MC syndromes m at a time (one chunk whenever e <= MC).
-template <int KC, int CPL, int PD>
-__global__ void __launch_bounds__(64) k_apply(ApplyArgs a, uint32_t n_units, uint32_t np, uint32_t MC) {
+template <int KC, int CPL, int PD, int OCC>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC)))
+k_apply(ApplyArgs a, uint32_t n_units, uint32_t np, uint32_t MC) {
     extern __shared__ __attribute__((aligned(16))) uint32_t xsh[];
     const uint32_t strips = ((a.T >> 2) + 64 * CPL - 1) / (64 * CPL);
     const uint32_t w = blockIdx.x, slice = (w / 8) % np, unit = (w / (8 * np)) * 8 + (w & 7);
@@ -768,7 +769,9 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a, uint32_t n_units, uin
         __builtin_amdgcn_make_buffer_rsrc((void*)(a.recv + (size_t)r0b * a.T), (short)0, -1, 0x20000);
     const __amdgpu_buffer_rsrc_t rs0 =
         __builtin_amdgcn_make_buffer_rsrc((void*)(a.r0 + (size_t)b * a.n_union * a.T), (short)0, -1, 0x20000);
-    uint8_t* blk = a.data + (size_t)b * a.data_stride;
+    // the block's rows likewise (g_E in, x_E out): a row's byte offset E_k * T < 4 GiB (K' * T)
+    const __amdgpu_buffer_rsrc_t rsD =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(a.data + (size_t)b * a.data_stride), (short)0, -1, 0x20000);
     // a chunk's syndromes are processed in whole groups of PD: the padding m's get zero tables and
     // a valid row offset, so the ring needs no branch (and the compiler no register copies)
     const uint32_t mc_max = (min(MC, e) + PD - 1) / PD * PD;
@@ -778,24 +781,30 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a, uint32_t n_units, uin
     uint32_t* off0 = offr + mc_max + PD;
     const uint8_t* xc = a.xcoef + 64ull * a.xoff[bi];
     const uint32_t xs = x_stride(e);
-    uint32_t col[CPL], vo[CPL];
+    // a lane's byte offset in a row per column (dead columns past T/4 read column 0, store nothing)
+    uint32_t vo[CPL];
     bool live[CPL];
 #pragma unroll
     for (int j = 0; j < CPL; ++j) {
         const uint32_t c = strip * 64 * CPL + j * 64 + lane;
         live[j] = c < Td;
-        col[j] = live[j] ? c : 0;
-        vo[j] = col[j] * 4;
+        vo[j] = live[j] ? c * 4 : 0u;
     }
     // The erased rows were not cleared before the syndrome program, so s = M (x_E ^ g_E) with g_E their
     // current bytes: start every output from g_E and X s completes it to x_E.
     const uint32_t kn = min((uint32_t)KC, e - k0);
     uint32_t acc[KC][CPL];
+    // lane k holds output k's row offset (one load for the slice, KC <= 64; made scalar per k, so the
+    // row loads and stores need no waterfall over a per-lane offset)
+    const uint32_t erow = E[k0 + min(lane, kn - 1)] * a.T;
 #pragma unroll
     for (int k = 0; k < KC; ++k) {
-        const uint32_t* grow = reinterpret_cast<const uint32_t*>(blk + (size_t)E[k0 + min((uint32_t)k, kn - 1)] * a.T);
+        const int go = __builtin_amdgcn_readlane((int)erow, k);
 #pragma unroll
-        for (int j = 0; j < CPL; ++j) acc[k][j] = ((uint32_t)k < kn && live[j]) ? grow[col[j]] : 0u;
+        for (int j = 0; j < CPL; ++j) {
+            const uint32_t g = __builtin_amdgcn_raw_buffer_load_b32(rsD, (int)vo[j], go, 0);
+            acc[k][j] = (uint32_t)k < kn ? g : 0u;
+        }
     }
     // syndromes are loaded PD m ahead into a ring (received row and r0 row, XORed on use); MC is a
     // multiple of PD, so ring slot d always holds syndrome m = d (mod PD) across chunks
@@ -832,7 +841,8 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a, uint32_t n_units, uin
         if (c0 == 0) {
 #pragma unroll
             for (int d = 0; d < PD; ++d) {
-                const int sr = (int)__builtin_amdgcn_readfirstlane(offr[d]), s0o = (int)__builtin_amdgcn_readfirstlane(off0[d]);
+                const int sr = (int)__builtin_amdgcn_readfirstlane(offr[d]);
+                const int s0o = (int)__builtin_amdgcn_readfirstlane(off0[d]);
 #pragma unroll
                 for (int j = 0; j < CPL; ++j) {
                     ra[d][j] = __builtin_amdgcn_raw_buffer_load_b32(rsR, (int)vo[j], sr, 0);
@@ -842,6 +852,13 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a, uint32_t n_units, uin
         }
         // (taking the syndromes in pairs, six lookups folded by three XOR3, measured 3 % slower:
         // profiles/r02w)
+        // Software pipeline: the tables of the next (m, k) and the next ring offsets are read from LDS
+        // one step ahead, and sched_barrier keeps the scheduler from sinking those reads next to their
+        // use (it did: one exposed LDS round trip per 25 VALU).  The last step's look-ahead reads one
+        // entry past the chunk (inside the allocation, launch_apply) and is discarded.
+        uint4 An = tA[0];
+        uint32_t Bn = tB[0];
+        uint32_t nsr = offr[PD], ns0o = off0[PD];  // read one step ahead, made scalar at use
         for (uint32_t mb = 0; mb < mcp; mb += PD) {
 #pragma unroll
             for (int d = 0; d < PD; ++d) {
@@ -855,18 +872,23 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a, uint32_t n_units, uin
                     s2[j] = (x >> 6) & 0x03030303u;
                 }
                 {  // past e the ring reads row 0 (zero tables consume it)
-                    const int sr = (int)__builtin_amdgcn_readfirstlane(offr[m + PD]);
-                    const int s0o = (int)__builtin_amdgcn_readfirstlane(off0[m + PD]);
+                    const int sr = (int)__builtin_amdgcn_readfirstlane(nsr);
+                    const int s0o = (int)__builtin_amdgcn_readfirstlane(ns0o);
 #pragma unroll
                     for (int j = 0; j < CPL; ++j) {
                         ra[d][j] = __builtin_amdgcn_raw_buffer_load_b32(rsR, (int)vo[j], sr, 0);
                         rb[d][j] = __builtin_amdgcn_raw_buffer_load_b32(rs0, (int)vo[j], s0o, 0);
                     }
+                    nsr = offr[m + PD + 1];
+                    ns0o = off0[m + PD + 1];
                 }
 #pragma unroll
                 for (int k = 0; k < KC; ++k) {
-                    const uint4 A = tA[m * KC + k];
-                    const uint32_t B = tB[m * KC + k];
+                    const uint4 A = An;
+                    const uint32_t B = Bn;
+                    An = tA[m * KC + k + 1];
+                    Bn = tB[m * KC + k + 1];
+                    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                     for (int j = 0; j < CPL; ++j) {
                         const uint32_t p0 = __builtin_amdgcn_perm(A.y, A.x, s0[j]);
@@ -881,48 +903,62 @@ __global__ void __launch_bounds__(64) k_apply(ApplyArgs a, uint32_t n_units, uin
 #pragma unroll
     for (int k = 0; k < KC; ++k) {
         if ((uint32_t)k < kn) {
-            uint32_t* row = reinterpret_cast<uint32_t*>(blk + (size_t)E[k0 + k] * a.T);
+            const int go = __builtin_amdgcn_readlane((int)erow, k);
 #pragma unroll
             for (int j = 0; j < CPL; ++j)
-                if (live[j]) row[col[j]] = acc[k][j];
+                if (live[j]) __builtin_amdgcn_raw_buffer_store_b32(acc[k][j], rsD, (int)vo[j], go, 0);
         }
     }
 }
 
-template <int CPL, int PD>
-static void launch_apply_cpl(const ApplyArgs& a, uint32_t kc, dim3 g, size_t lds, hipStream_t st, uint32_t nu,
-                             uint32_t np, uint32_t mc) {
-    switch (kc) {
-        case 4: hipLaunchKernelGGL((k_apply<4, CPL, PD>), g, dim3(64), lds, st, a, nu, np, mc); break;
-        case 8: hipLaunchKernelGGL((k_apply<8, CPL, PD>), g, dim3(64), lds, st, a, nu, np, mc); break;
-        case 12: hipLaunchKernelGGL((k_apply<12, CPL, PD>), g, dim3(64), lds, st, a, nu, np, mc); break;
-        case 16: hipLaunchKernelGGL((k_apply<16, CPL, PD>), g, dim3(64), lds, st, a, nu, np, mc); break;
-        case 20: hipLaunchKernelGGL((k_apply<20, CPL, PD>), g, dim3(64), lds, st, a, nu, np, mc); break;
-        case 24: hipLaunchKernelGGL((k_apply<24, CPL, PD>), g, dim3(64), lds, st, a, nu, np, mc); break;
-        case 28: hipLaunchKernelGGL((k_apply<28, CPL, PD>), g, dim3(64), lds, st, a, nu, np, mc); break;
-        default: hipLaunchKernelGGL((k_apply<32, CPL, PD>), g, dim3(64), lds, st, a, nu, np, mc); break;
+// KC is at most 8 in the shipped library (launch_apply's cap); experiments builds (RQHIP_APPLY_KC)
+// reach the wider slices.
+template <int CPL, int PD, int OCC, int KCMAX>
+static void launch_apply_cpl(const ApplyArgs& a, uint32_t kc, dim3 g, uint32_t ec, size_t lds_min, hipStream_t st,
+                             uint32_t nu, uint32_t np, uint32_t mc) {
+    // the kernel's LDS: tables (20 or 24 B per coefficient) for a chunk of up to ec syndromes padded to
+    // whole groups of PD, the two row-offset arrays (PD past the chunk) and 16 B for the pipelined
+    // look-ahead past the last offset -- sized exactly, so four 64-lane waves per SIMD also fit the
+    // LDS (e ~ 58, KC 8: 9.8 KB per wave)
+    const size_t mcx = (ec + PD - 1) / PD * PD;
+    const size_t lds = std::max(lds_min, mcx * kc * 20 + (mcx + PD) * 8 + 16);
+    if (kc <= 4) { hipLaunchKernelGGL((k_apply<4, CPL, PD, OCC>), g, dim3(64), lds, st, a, nu, np, mc); return; }
+    if constexpr (KCMAX > 8) {
+        switch (kc) {
+            case 12: { hipLaunchKernelGGL((k_apply<12, CPL, PD, OCC>), g, dim3(64), lds, st, a, nu, np, mc); return; }
+            case 16: { hipLaunchKernelGGL((k_apply<16, CPL, PD, OCC>), g, dim3(64), lds, st, a, nu, np, mc); return; }
+            case 20: { hipLaunchKernelGGL((k_apply<20, CPL, PD, OCC>), g, dim3(64), lds, st, a, nu, np, mc); return; }
+            case 24: { hipLaunchKernelGGL((k_apply<24, CPL, PD, OCC>), g, dim3(64), lds, st, a, nu, np, mc); return; }
+            default: break;
+        }
     }
+    hipLaunchKernelGGL((k_apply<8, CPL, PD, OCC>), g, dim3(64), lds, st, a, nu, np, mc);
 }
 
 #ifdef RQHIP_EXPERIMENTS
-// Syndrome prefetch depth of k_apply (RQHIP_APPLY_PD = 2 / 4 / 8 in experiments builds; else 4).
+// Syndrome prefetch depth of k_apply (RQHIP_APPLY_PD = 4 / 8 in experiments builds; else 2 at four
+// waves per SIMD).
 static int apply_pd() {
     static const int pd = [] {
         const char* e = std::getenv("RQHIP_APPLY_PD");
-        return e ? std::atoi(e) : 4;
+        return e ? std::atoi(e) : 2;
     }();
     return pd;
 }
 #endif
 
 template <int CPL>
-static void launch_apply_pd(const ApplyArgs& a, uint32_t kc, dim3 g, size_t lds, hipStream_t st, uint32_t nu,
-                            uint32_t np, uint32_t mc) {
+static void launch_apply_pd(const ApplyArgs& a, uint32_t kc, dim3 g, uint32_t ec, size_t lds_min, hipStream_t st,
+                            uint32_t nu, uint32_t np, uint32_t mc) {
 #ifdef RQHIP_EXPERIMENTS
-    if (apply_pd() == 2) return launch_apply_cpl<CPL, 2>(a, kc, g, lds, st, nu, np, mc);
-    if (apply_pd() == 8) return launch_apply_cpl<CPL, 8>(a, kc, g, lds, st, nu, np, mc);
+    // RQHIP_APPLY_OCC=3: the round-2 shape (PD 4, no occupancy bound, ~3 waves per SIMD at CPL 5)
+    static const bool occ3 = [] { const char* e = std::getenv("RQHIP_APPLY_OCC"); return e && e[0] == '3'; }();
+    if (apply_pd() == 8) return launch_apply_cpl<CPL, 8, 1, 24>(a, kc, g, ec, lds_min, st, nu, np, mc);
+    if (occ3 || apply_pd() == 4 || kc > 8) return launch_apply_cpl<CPL, 4, 1, 24>(a, kc, g, ec, lds_min, st, nu, np, mc);
 #endif
-    launch_apply_cpl<CPL, 4>(a, kc, g, lds, st, nu, np, mc);
+    // four waves per SIMD (<= 128 VGPRs, spill-free for KC <= 8 with a two-deep ring): 200 -> 192 us
+    // at 1 024 blocks K=1024 (profiles/r03q)
+    launch_apply_cpl<CPL, 2, 4, 8>(a, kc, g, ec, lds_min, st, nu, np, mc);
 }
 
 int launch_apply(const ApplyArgs& a, uint32_t /*n_strips*/, uint32_t n_blocks, void* stream) {
@@ -940,21 +976,20 @@ int launch_apply(const ApplyArgs& a, uint32_t /*n_strips*/, uint32_t n_blocks, v
     const uint32_t e = std::max<uint32_t>(a.max_e, 1), ec = std::min(e, MC);
     uint32_t cap = std::max<uint32_t>(4, std::min<uint32_t>(8, (21504 / (20 * ec)) & ~3u));
 #ifdef RQHIP_EXPERIMENTS
-    if (const char* v = std::getenv("RQHIP_APPLY_KC")) cap = std::max(4, std::min(32, std::atoi(v))) & ~3u;
+    if (const char* v = std::getenv("RQHIP_APPLY_KC")) cap = std::max(4, std::min(24, std::atoi(v))) & ~3u;
 #endif
     const uint32_t np = (e + cap - 1) / cap, kc = (((e + np - 1) / np) + 3) & ~3u;
-    const size_t ecp = (ec + 7) / 8 * 8;  // the kernel pads a chunk to whole groups of PD (<= 8) syndromes
-    size_t lds = ecp * kc * 20 + (ecp + 8) * 8;  // tables + row offsets (<= 23 KB)
+    size_t lds = 0;
 #ifdef RQHIP_EXPERIMENTS
-    if (const char* v = std::getenv("RQHIP_APPLY_LDS")) lds = std::max<size_t>(lds, (size_t)std::atoi(v));  // occupancy cap
+    if (const char* v = std::getenv("RQHIP_APPLY_LDS")) lds = (size_t)std::atoi(v);  // occupancy cap
 #endif
     const uint32_t nu = (Td + 64 * cpl - 1) / (64 * cpl) * n_blocks;
     const dim3 g((nu + 7) / 8 * 8 * np);
     switch (cpl) {
-        case 1: launch_apply_pd<1>(a, kc, g, lds, st, nu, np, MC); break;
-        case 2: launch_apply_pd<2>(a, kc, g, lds, st, nu, np, MC); break;
-        case 4: launch_apply_pd<4>(a, kc, g, lds, st, nu, np, MC); break;
-        default: launch_apply_pd<5>(a, kc, g, lds, st, nu, np, MC); break;
+        case 1: launch_apply_pd<1>(a, kc, g, ec, lds, st, nu, np, MC); break;
+        case 2: launch_apply_pd<2>(a, kc, g, ec, lds, st, nu, np, MC); break;
+        case 4: launch_apply_pd<4>(a, kc, g, ec, lds, st, nu, np, MC); break;
+        default: launch_apply_pd<5>(a, kc, g, ec, lds, st, nu, np, MC); break;
     }
     return (int)hipGetLastError();
 }

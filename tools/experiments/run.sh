@@ -25,6 +25,14 @@ for step in "$@"; do
     traffic) bash tools/gpu_profile.sh $TAG > $log.log 2>&1 || { tail -10 $log.log; exit 1; }; cp gpurun_out/pmc_traffic/summary.json $O/traffic.json; cp gpurun_out/pmc_traffic/summary_k256.json $O/traffic_k256.json; cat $O/traffic.json $O/traffic_k256.json ;;
     sq) timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU SQ_INSTS_LDS \
           --kernel-include-regex rq_colprog --output-format csv -d $log -o sq -- python3 tools/colbench.py ${arg:-1024 1200 1100 1024 3} > $log.log 2>&1 || { tail -5 $log.log; exit 1; } ;;
+    pmc) # SQ/GRBM counters (two passes) of the kernels matching ARG (default k_apply) over a short bench
+        for pass in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT" \
+                    "SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_SCA"; do
+          k=$((${k:-0} + 1))
+          timeout -s KILL 90 rocprofv3 --pmc $pass --kernel-include-regex "${arg:-k_apply}" --output-format csv -d $log/p$k -o p \
+            -- python3 $BENCH --cpu-sample 0 --steps 3 --warmup 1 > $log.p$k.log 2>&1 || { tail -5 $log.p$k.log; exit 1; }
+        done
+        python3 tools/experiments/pmc_sum.py $log ;;
     py) s=${arg%%:*}; a=""; [ "$arg" != "$s" ] && a=${arg#*:}
         timeout -k 10 300 python3 $s $a > $log.log 2>&1 || { tail -20 $log.log; exit 1; }; tail -5 $log.log ;;
     *) echo "unknown step $name"; exit 2 ;;
