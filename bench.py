@@ -260,6 +260,14 @@ def pcie_copy_peak(dev, mib=256, reps=5):
     return out
 
 
+_JSON_OUT = None  # the process's original stdout once the rank's fd 1 is redirected (dist_setup)
+
+
+def emit(line):
+    """The bench line: the ONE line rank 0 writes to the original stdout."""
+    print(json.dumps(line), file=_JSON_OUT or sys.stdout, flush=True)
+
+
 def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -272,6 +280,13 @@ def dist_setup(args):
     dev = torch.device("cuda", gpu)
     dist = None
     if world > 1:
+        # the communication libraries write to fd 1 (gloo's "connected to N peer ranks"): point fd 1 at
+        # stderr for the rest of the rank's life and keep the original stdout for the bench line only
+        global _JSON_OUT
+        if _JSON_OUT is None:
+            sys.stdout.flush()
+            _JSON_OUT = os.fdopen(os.dup(1), "w")
+            os.dup2(2, 1)
         import torch.distributed as tdist
         if args.dist_backend == "nccl":  # bind the RCCL communicator to this rank's GPU explicitly
             tdist.init_process_group(args.dist_backend, device_id=dev)
@@ -340,7 +355,7 @@ def run_config2(args):
                          "achieved_read_write": round(B * (K + R) * T / (enc_ms * 1e-3) / 1e9, 2)}}
         if args.cpu_sample > 0 and world == 1:
             line["cpu_baseline"] = cpu_baseline_encode(K, T, esis, args.cpu_sample)
-        print(json.dumps(line), flush=True)
+        emit(line)
     if dist is not None:
         dist.destroy_process_group()
 
@@ -433,7 +448,7 @@ def run_config5(args):
                          "peak_source": "torch pinned copy_ of 256 MiB, 5 reps, this box"}}
         if args.cpu_sample > 0 and world == 1:
             line["cpu_baseline"] = cpu_baseline_mixed(shapes, max(1, args.cpu_sample // 128))
-        print(json.dumps(line), flush=True)
+        emit(line)
     if dist is not None:
         dist.destroy_process_group()
 
@@ -534,7 +549,7 @@ def main():
         }
         if args.cpu_sample > 0 and world == 1:
             line["cpu_baseline"] = cpu_baseline(K, T, N, n_erase, args.cpu_sample)
-        print(json.dumps(line), flush=True)
+        emit(line)
     if dist is not None:
         dist.destroy_process_group()
 
