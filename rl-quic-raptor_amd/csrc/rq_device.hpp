@@ -63,6 +63,9 @@ struct SolveArgs {
     // first solver launch in place of an upload (nullptr: status already holds them)
     const int32_t* status_init;
     uint32_t n_all;
+    // first pass (k_solve_pm<1, ...>): use at most e + row_margin received repairs (0 = up to 64); a
+    // block rank-deficient on them is deferred to the later passes like one beyond 64
+    uint32_t row_margin;
 };
 constexpr int32_t ST_PENDING = -100;   // queued for the solver
 constexpr int32_t ST_FALLBACK = -101;  // beyond the fast solvers: the general solver decides

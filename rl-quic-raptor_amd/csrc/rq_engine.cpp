@@ -698,6 +698,16 @@ void decode_collect(const Workspace* w, const std::vector<uint32_t>& blk_map, co
     }
 }
 
+// Received repairs the first solver pass takes beyond e: k_solve_pm then carries e + 4 rows and as many
+// identity columns instead of 64 (seven 16-byte quads per row at e ~ 51 instead of eight): 81.8 ->
+// 77.0 us at 1 024 blocks (profiles/r03sm).  A block rank-deficient on those rows (~256^-5 for e ~ 51)
+// goes to the general solver with every received repair.  Experiments builds: RQHIP_SOLVE_MARGIN
+// (0 = the first 64).
+uint32_t solve_row_margin() {
+    static const uint32_t m = [] { const char* e = knob("RQHIP_SOLVE_MARGIN"); return e ? (uint32_t)std::atoi(e) : 4u; }();
+    return m;
+}
+
 // One solve pass over the blocks of `blocks` (each pending; cnt[b] = candidate repairs offered).
 // Caller holds ctx->mu.  Host arrays as in rq_decode_desc.
 int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, void* data, uint64_t data_stride,
@@ -717,7 +727,7 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
         const uint32_t b = blk_map[bi], e = eoff[b + 1] - eoff[b];
         max_e = std::max(max_e, e);
         if (e <= lds_e_max()) max_lds_e = std::max(max_lds_e, e);
-        need_general |= (e > 64 || cnt[b] > 64);
+        need_general |= (e > 64 || cnt[b] > std::min<uint32_t>(64, e + solve_row_margin()));
         wide |= (e > 64 && e <= 128);
         cand.insert(cand.end(), repair_esi + roff[b], repair_esi + roff[b] + cnt[b]);
         xoff[bi] = (uint32_t)xo;
@@ -841,6 +851,7 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     s.lds_e = lds_e_max();
     s.status_init = zero_copy ? reinterpret_cast<const int32_t*>(di + o_st) : nullptr;
     s.n_all = n_blocks;
+    s.row_margin = solve_row_margin();
     if (launch_solve(s, nw, need_general, wide, max_lds_e, stream)) return fail(RQ_ERR_DEVICE, "k_solve launch failed");
     // 3) apply: x_E = X * s
     ApplyArgs ap;

@@ -338,7 +338,7 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pm(SolveArgs a) {
         if (tid == 0) a.status[b] = ST_FALLBACK;
         return;
     }
-    const uint32_t nrow = min(nr, NROWS);
+    const uint32_t nrow = (RPL == 1 && a.row_margin) ? min(min(nr, NROWS), e + a.row_margin) : min(nr, NROWS);
     const uint32_t* E = a.erased + a.erased_off[b];
     const uint32_t* U = a.rep_uidx + a.rep_off[b];
     for (uint32_t i = tid; i < e; i += NT) Es[i] = E[i];
