@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <array>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <queue>
 #include <set>
@@ -330,9 +331,10 @@ bool eliminate(const Params& p, Elim* e, std::string* err) {
 // ---- IR construction helpers ----
 struct Builder {
     ColIR* ir;
+    uint8_t grp = 0;  // tag of the nodes added (IrNode::grp)
     uint32_t add(uint8_t k, uint32_t a = NOVAL, uint32_t b = NOVAL, uint32_t c = NOVAL, uint32_t imm = 0) {
         IrNode n;
-        n.k = k; n.a = a; n.b = b; n.c = c; n.imm = imm;
+        n.k = k; n.a = a; n.b = b; n.c = c; n.imm = imm; n.grp = grp;
         ir->nodes.push_back(n);
         return (uint32_t)ir->nodes.size() - 1;
     }
@@ -373,6 +375,12 @@ struct Acc {
         if (pend != NOVAL) { val = B.add(IR_XOR2, val, pend); pend = NOVAL; }
         return val;
     }
+    // the accumulated terms as operands of a larger sum (no XOR of their own): val, then pend
+    void append_to(std::vector<uint32_t>& t) {
+        if (val != NOVAL) t.push_back(val);
+        if (pend != NOVAL) t.push_back(pend);
+        val = pend = NOVAL;
+    }
 };
 
 // Output specification: the set of C columns XORed (XOR semantics) or a source row.
@@ -389,6 +397,16 @@ struct OutDesc {
 // linear, so the P chains' pushes and end values add up to the single scan's).  A y value then lives
 // only until its pass instead of until its column comes up in one global scan, which bounds the live
 // set by about npiv / P plus the open accumulators, at 2 ops per column per extra pass.
+// Group size of the four-Russians dense part and outputs (0: the direct sums of rounds 1-2;
+// RQHIP_DENSE_GROUP in experiments builds).
+static uint32_t dense_group() {
+    static const uint32_t g = [] {
+        const char* m = knob("RQHIP_DENSE_GROUP");
+        return m ? (uint32_t)std::min(6, std::max(0, std::atoi(m))) : 4u;
+    }();
+    return g;
+}
+
 static bool interleave_passes() {
     static const bool on = [] { const char* m = knob("RQHIP_WEAVE"); return m && m[0] == '1'; }();
     return on;
@@ -515,6 +533,7 @@ bool build(const Params& p, const std::vector<OutDesc>& outs, uint32_t passes, C
         std::vector<uint32_t> chunk;  // pivot indices of produced y (column < KS)
         auto flush = [&]() {
             if (chunk.empty()) return;
+            B.grp = 1;
             const size_t ng = (chunk.size() + 3) / 4;
             std::vector<std::array<uint32_t, 16>> sub(ng);
             for (size_t g = 0; g < ng; ++g) sub[g].fill(NOVAL);
@@ -549,15 +568,20 @@ bool build(const Params& p, const std::vector<OutDesc>& outs, uint32_t passes, C
                     S8[h * 8 + b] = B.xsum(terms);
                 }
             chunk.clear();
+            B.grp = 0;
         };
         for (uint32_t k = 0; k < npiv; ++k) {
-            std::vector<uint32_t> tt{D(e.piv_row[k]), yacc[k].get(B)};
+            std::vector<uint32_t> tt{D(e.piv_row[k])};
+            yacc[k].append_to(tt);
             y[k] = B.xsum(tt);
             ystate[k] = 2;
             for (uint32_t d : dependents[k]) yacc[d].push(B, y[k], may_pend(d, k));
             const uint32_t c = e.piv_col[k];
             for (uint32_t i : col_rem[c]) b2acc[i].push(B, y[k], may_pend(npiv + i, k));
             for (uint32_t o : col_outs[c]) oacc[o].push(B, y[k], may_pend(npiv + n2 + o, k));
+            ir->st.push_dep += (uint32_t)dependents[k].size();
+            ir->st.push_rem += (uint32_t)col_rem[c].size();
+            ir->st.push_out += (uint32_t)col_outs[c].size();
             if (c < KS && y[k] != NOVAL) {
                 chunk.push_back(k);
                 if (chunk.size() == 8) flush();
@@ -565,11 +589,13 @@ bool build(const Params& p, const std::vector<OutDesc>& outs, uint32_t passes, C
         }
         flush();
         bh_direct.assign(H, NOVAL);
+        B.grp = 1;
         for (uint32_t h = 0; h < H; ++h) {
             uint32_t acc = NOVAL;
             for (int b = 7; b >= 0; --b) acc = B.xt(acc, S8[h * 8 + b]);
             bh_direct[h] = acc;
         }
+        B.grp = 0;
     } else if (passes & SCHED_RS) {
         // Peeling-order production, push-mode dependencies; the Horner chain absorbs the produced y
         // values by replacement selection: at most `hbuf` of them wait, and whenever the buffer is
@@ -622,7 +648,8 @@ bool build(const Params& p, const std::vector<OutDesc>& outs, uint32_t passes, C
             while ((uint32_t)(cur + 1) <= target) step_to((uint32_t)(cur + 1));
         };
         for (uint32_t k = 0; k < npiv; ++k) {
-            std::vector<uint32_t> tt{D(e.piv_row[k]), yacc[k].get(B)};
+            std::vector<uint32_t> tt{D(e.piv_row[k])};
+            yacc[k].append_to(tt);
             y[k] = B.xsum(tt);
             ystate[k] = 2;
             for (uint32_t d : dependents[k]) yacc[d].push(B, y[k]);
@@ -672,7 +699,8 @@ bool build(const Params& p, const std::vector<OutDesc>& outs, uint32_t passes, C
         const bool weave = interleave_passes();
         uint32_t q = 1, lo = 0, credit = 0;
         for (uint32_t k = 0; k < npiv; ++k) {
-            std::vector<uint32_t> tt{D(e.piv_row[k]), yacc[k].get(B)};
+            std::vector<uint32_t> tt{D(e.piv_row[k])};
+            yacc[k].append_to(tt);
             y[k] = B.xsum(tt);
             ystate[k] = 2;
             for (uint32_t d : dependents[k]) yacc[d].push(B, y[k]);
@@ -729,35 +757,122 @@ bool build(const Params& p, const std::vector<OutDesc>& outs, uint32_t passes, C
     for (uint32_t i = 0; i < n2; ++i) b2[i] = b2acc[i].get(B);
 
     // ---- dense part: C_F[f] = sum_bit alpha^bit X_bit[f], X_bit[f] = bits of Zi[f]*bh ^ Q[f]*b2
+    // ---- outputs: out_o = oacc_o ^ V1_o*b2 ^ V2_o*C_F
     ir->phase_start[2] = (uint32_t)ir->nodes.size();
     std::vector<uint32_t> CF(H, NOVAL);
-    for (uint32_t f = 0; f < H; ++f) {
-        uint32_t acc = NOVAL;
-        for (int bt = 7; bt >= 0; --bt) {
-            std::vector<uint32_t> terms;
-            for (uint32_t h = 0; h < H; ++h)
-                if ((e.Zi[(size_t)f * H + h] >> bt) & 1) terms.push_back(bh[h]);
+    std::vector<uint32_t> outv(no, NOVAL);
+    const uint32_t dg = dense_group();
+    if (dg) {
+        // Four Russians over the inputs (round 3): the 8H bit rows X_bit[f] and the output rows are
+        // GF(2) combinations of the n2 + H values b2 ++ bh, then the outputs of the H values C_F.  The
+        // inputs are cut into groups of dg; a group's subset XORs are built once (only the subsets
+        // some row uses) and every row takes one subset per group, so a row costs one XOR3 per two
+        // groups instead of one per two terms (~half its n2/2 terms).  The output rows' b2 part rides
+        // along with the dense rows; their C_F part follows the Horner chains.  Same XOR sets as the
+        // direct sums: bit-identical.
+        struct Row { Acc acc; std::vector<uint32_t> idx; };  // input indices with a one
+        auto run = [&](const std::vector<uint32_t>& in, std::vector<Row*>& rws) {
+            const uint32_t ni = (uint32_t)in.size(), ng = (ni + dg - 1) / dg;
+            std::vector<std::vector<uint32_t>> mask(rws.size(), std::vector<uint32_t>(ng, 0));
+            for (size_t r = 0; r < rws.size(); ++r)
+                for (uint32_t x : rws[r]->idx) mask[r][x / dg] ^= 1u << (x % dg);
+            for (uint32_t g0 = 0; g0 < ng; ++g0) {
+                std::vector<uint32_t> sub(1u << dg, NOVAL);
+                std::vector<uint8_t> built(1u << dg, 0);
+                std::function<uint32_t(uint32_t)> subset = [&](uint32_t m) -> uint32_t {
+                    if (built[m]) return sub[m];
+                    built[m] = 1;
+                    std::vector<uint32_t> mem;
+                    for (uint32_t q = 0; q < dg; ++q)
+                        if (m >> q & 1) mem.push_back(g0 * dg + q < ni ? in[g0 * dg + q] : NOVAL);
+                    uint32_t v;
+                    if (mem.size() <= 2) {
+                        v = B.xsum(mem);
+                    } else {  // the subset without its two highest members, then XOR3 those in
+                        uint32_t rest = m, hi2[2], k = 0;
+                        for (int q = (int)dg - 1; q >= 0 && k < 2; --q)
+                            if (rest >> q & 1) { hi2[k++] = (uint32_t)q; rest &= ~(1u << q); }
+                        std::vector<uint32_t> t{subset(rest), g0 * dg + hi2[0] < ni ? in[g0 * dg + hi2[0]] : NOVAL,
+                                                g0 * dg + hi2[1] < ni ? in[g0 * dg + hi2[1]] : NOVAL};
+                        v = B.xsum(t);
+                    }
+                    sub[m] = v;
+                    return v;
+                };
+                for (size_t r = 0; r < rws.size(); ++r)
+                    if (mask[r][g0]) rws[r]->acc.push(B, subset(mask[r][g0]));
+            }
+        };
+        std::vector<uint32_t> in1(b2);
+        in1.insert(in1.end(), bh.begin(), bh.end());
+        std::vector<Row> drow((size_t)H * 8), orow(no);
+        std::vector<Row*> rws;
+        for (uint32_t f = 0; f < H; ++f)
+            for (uint32_t bt = 0; bt < 8; ++bt) {
+                Row& r = drow[(size_t)f * 8 + bt];
+                for (uint32_t h = 0; h < H; ++h)
+                    if ((e.Zi[(size_t)f * H + h] >> bt) & 1) r.idx.push_back(n2 + h);
+                for (uint32_t m = 0; m < n2; ++m)
+                    if ((e.Q[(size_t)f * n2 + m] >> bt) & 1) r.idx.push_back(m);
+                rws.push_back(&r);
+            }
+        for (uint32_t o = 0; o < no; ++o) {
+            if (outs[o].source) continue;
+            Row& r = orow[o];
+            std::vector<uint32_t> t0;
+            oacc[o].append_to(t0);
+            for (uint32_t v : t0) r.acc.push(B, v);
             for (uint32_t m = 0; m < n2; ++m)
-                if ((e.Q[(size_t)f * n2 + m] >> bt) & 1) terms.push_back(b2[m]);
-            const uint32_t x = B.xsum(terms);
-            acc = B.xt(acc, x);
+                if (bit(V1[o].data(), m)) r.idx.push_back(m);
+            rws.push_back(&r);
         }
-        CF[f] = acc;
-    }
-    // ---- outputs
-    ir->phase_start[3] = (uint32_t)ir->nodes.size();
-    for (uint32_t o = 0; o < no; ++o) {
-        uint32_t v;
-        if (outs[o].source) {
-            v = outs[o].row < K ? B.add(IR_LOAD, NOVAL, NOVAL, NOVAL, outs[o].row) : NOVAL;
-        } else {
-            std::vector<uint32_t> terms{oacc[o].get(B)};
+        run(in1, rws);
+        for (uint32_t f = 0; f < H; ++f) {
+            uint32_t acc = NOVAL;
+            for (int bt = 7; bt >= 0; --bt) acc = B.xt(acc, drow[(size_t)f * 8 + bt].acc.get(B));
+            CF[f] = acc;
+        }
+        ir->phase_start[3] = (uint32_t)ir->nodes.size();
+        std::vector<Row*> rw2;
+        for (uint32_t o = 0; o < no; ++o) {
+            if (outs[o].source) continue;
+            orow[o].idx.clear();
+            for (uint32_t f = 0; f < H; ++f)
+                if (bit(V2[o].data(), f)) orow[o].idx.push_back(f);
+            rw2.push_back(&orow[o]);
+        }
+        run(CF, rw2);
+        for (uint32_t o = 0; o < no; ++o)
+            if (!outs[o].source) outv[o] = orow[o].acc.get(B);
+    } else {
+        for (uint32_t f = 0; f < H; ++f) {
+            uint32_t acc = NOVAL;
+            for (int bt = 7; bt >= 0; --bt) {
+                std::vector<uint32_t> terms;
+                for (uint32_t h = 0; h < H; ++h)
+                    if ((e.Zi[(size_t)f * H + h] >> bt) & 1) terms.push_back(bh[h]);
+                for (uint32_t m = 0; m < n2; ++m)
+                    if ((e.Q[(size_t)f * n2 + m] >> bt) & 1) terms.push_back(b2[m]);
+                const uint32_t x = B.xsum(terms);
+                acc = B.xt(acc, x);
+            }
+            CF[f] = acc;
+        }
+        ir->phase_start[3] = (uint32_t)ir->nodes.size();
+        for (uint32_t o = 0; o < no; ++o) {
+            if (outs[o].source) continue;
+            std::vector<uint32_t> terms;
+            oacc[o].append_to(terms);
             for (uint32_t m = 0; m < n2; ++m)
                 if (bit(V1[o].data(), m)) terms.push_back(b2[m]);
             for (uint32_t f = 0; f < H; ++f)
                 if (bit(V2[o].data(), f)) terms.push_back(CF[f]);
-            v = B.xsum(terms);
+            outv[o] = B.xsum(terms);
         }
+    }
+    for (uint32_t o = 0; o < no; ++o) {
+        uint32_t v = outv[o];
+        if (outs[o].source) v = outs[o].row < K ? B.add(IR_LOAD, NOVAL, NOVAL, NOVAL, outs[o].row) : NOVAL;
         if (v == NOVAL) v = B.add(IR_ZERO);
         B.add(IR_STORE, v, NOVAL, NOVAL, o);
     }

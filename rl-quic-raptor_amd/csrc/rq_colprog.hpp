@@ -57,6 +57,7 @@ struct IrNode {
     uint8_t k = IR_ZERO;
     uint32_t a = NOVAL, b = NOVAL, c = NOVAL;  // operand value ids (node indices)
     uint32_t imm = 0;
+    uint8_t grp = 0;  // 1: HDPC bit accumulation (SCHED_4R subset sums, bit rows, bh); else 0
 };
 
 struct ColIR {
@@ -67,6 +68,7 @@ struct ColIR {
     struct Stats {
         uint32_t xor2 = 0, xor3 = 0, xt = 0, xtx = 0, load = 0, store = 0, zero = 0;
         uint32_t u = 0, npiv = 0, n2 = 0;
+        uint32_t push_dep = 0, push_rem = 0, push_out = 0;  // SCHED_4R production pushes by target
     } st;
 };
 

@@ -66,6 +66,8 @@ struct SolveArgs {
     // first pass (k_solve_pm<1, ...>): use at most e + row_margin received repairs (0 = up to 64); a
     // block rank-deficient on them is deferred to the later passes like one beyond 64
     uint32_t row_margin;
+    uint32_t n_map;             // entries of blk_map (the general solver's grid strides over them)
+    uint32_t diag_steps;        // experiments builds (RQHIP_SOLVE_STEPS): pivot steps of k_solve_pq (timing only)
 };
 constexpr int32_t ST_PENDING = -100;   // queued for the solver
 constexpr int32_t ST_FALLBACK = -101;  // beyond the fast solvers: the general solver decides

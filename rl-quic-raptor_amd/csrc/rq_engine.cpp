@@ -852,6 +852,8 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     s.status_init = zero_copy ? reinterpret_cast<const int32_t*>(di + o_st) : nullptr;
     s.n_all = n_blocks;
     s.row_margin = solve_row_margin();
+    s.n_map = nw;
+    s.diag_steps = 0;
     if (launch_solve(s, nw, need_general, wide, max_lds_e, stream)) return fail(RQ_ERR_DEVICE, "k_solve launch failed");
     // 3) apply: x_E = X * s
     ApplyArgs ap;

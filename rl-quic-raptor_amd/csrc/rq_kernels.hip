@@ -459,6 +459,157 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pm(SolveArgs a) {
     if (tid == 0) a.status[b] = 1;
 }
 
+// k_solve_pm (LUT) with a shorter dependent chain per pivot step: each wave issues the loads of its
+// row quads for the step (at most QW per row) at the step's start, reads pinfo[f] of its own
+// coefficient (log f, and the pivot-lane coefficient's log) instead of lg[f] after pinfo[f_p] (f_p's
+// log is then a v_readlane of the pivot lane's entry), and loads all its pivot-row quads at once: a
+// step is three dependent LDS round trips (f, pinfo[f], the tables) plus the barrier, where the
+// quad-at-a-time loop had two more per quad.
+template <int RPL, int NW>
+__global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
+    constexpr uint32_t NT = 64 * NW;
+    constexpr uint32_t NROWS = 64 * RPL, SW = 32 * RPL + 4;  // rows, row stride (dwords)
+    constexpr uint32_t QW = (8 * RPL + NW - 1) / NW;          // quads per row a wave may update
+    __shared__ __attribute__((aligned(16))) uint32_t rows[NROWS * SW];
+    __shared__ __attribute__((aligned(4))) uint8_t ex[512], lg[256];
+    __shared__ uint8_t pivl[NROWS];
+    __shared__ uint32_t Es[NROWS];
+    __shared__ __attribute__((aligned(16))) uint4 tlA[255];
+    __shared__ uint32_t tlB[255];
+    __shared__ uint32_t pinfo[256];
+    const uint32_t b = a.blk_map[blockIdx.x];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
+    if (a.status_init)
+        for (uint32_t i = blockIdx.x * NT + tid; i < a.n_all; i += gridDim.x * NT)
+            if (a.status_init[i] != ST_PENDING) a.status[i] = a.status_init[i];
+    if (RPL > 1 && a.status[b] != ST_FALLBACK) return;
+    const uint32_t e = a.erased_off[b + 1] - a.erased_off[b];
+    const uint32_t nr = a.rep_cnt[b];
+    if (e > NROWS) {
+        if (tid == 0) a.status[b] = ST_FALLBACK;
+        return;
+    }
+    const uint32_t nrow = (RPL == 1 && a.row_margin) ? min(min(nr, NROWS), e + a.row_margin) : min(nr, NROWS);
+    const uint32_t* E = a.erased + a.erased_off[b];
+    const uint32_t* U = a.rep_uidx + a.rep_off[b];
+    for (uint32_t i = tid; i < e; i += NT) Es[i] = E[i];
+    gf_tables_copy(ex, lg);
+    for (uint32_t l = tid; l < 255; l += NT) perm_tables(kGf.ex[l], &tlA[l], &tlB[l]);
+    for (uint32_t i = tid; i < NROWS * SW; i += NT) rows[i] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < RPL; ++q) {
+        const uint32_t row = lane + 64 * q;
+        if (row < nrow) {
+            uint8_t* myb = reinterpret_cast<uint8_t*>(rows + row * SW);
+            const uint8_t* mr = a.mrep + (size_t)U[row] * a.mrep_stride;
+            gather_row<NW>(myb, mr, Es, e, g);
+            if (g == 0) myb[e + row] = 1;
+        }
+    }
+    // pinfo[f] = log f | log(1 ^ 1/f) << 8 | (1 ^ 1/f != 0) << 16; pinfo[0] = 0
+    for (uint32_t x = tid; x < 256; x += NT) {
+        uint32_t v = 0;
+        if (x) {
+            const uint32_t lx = lg[x], cp = 1u ^ ex[255u - lx];
+            v = lx | (cp ? (uint32_t)lg[cp] << 8 | 1u << 16 : 0u);
+        }
+        pinfo[x] = v;
+    }
+    __syncthreads();
+    const uint32_t q1 = (e + nrow + 15) >> 4;  // quads holding live columns
+    bool used[RPL];
+#pragma unroll
+    for (int q = 0; q < RPL; ++q) used[q] = lane + 64 * q >= nrow;
+    const uint8_t* rb = reinterpret_cast<const uint8_t*>(rows);
+    const uint32_t ksteps = a.diag_steps ? min(e, a.diag_steps) : e;
+    for (uint32_t k = 0; k < ksteps; ++k) {
+        // (1) this wave's row quads for the step and every row's coefficient in column k
+        const uint32_t w0 = (k >> 4) + g;
+        uint4 R[RPL][QW];
+#pragma unroll
+        for (int j = 0; j < (int)QW; ++j)
+#pragma unroll
+            for (int q = 0; q < RPL; ++q)
+                R[q][j] = (w0 + NW * j < q1) ? reinterpret_cast<const uint4*>(rows + (lane + 64 * q) * SW)[w0 + NW * j]
+                                             : make_uint4(0, 0, 0, 0);
+        uint32_t f[RPL], pif[RPL];
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) f[q] = (rows[(lane + 64 * q) * SW + (k >> 2)] >> ((k & 3) * 8)) & 0xFFu;
+        // (2) pinfo of every row's coefficient, beside the ballot
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) pif[q] = pinfo[f[q]];
+        uint32_t p = 0xFFFFFFFFu;
+#pragma unroll
+        for (int q = RPL - 1; q >= 0; --q) {
+            const uint64_t bal = __ballot(f[q] != 0 && !used[q]);
+            if (bal) p = 64 * q + (uint32_t)__ffsll((unsigned long long)bal) - 1;
+        }
+        if (p == 0xFFFFFFFFu) {  // uniform over the block: every wave saw the same rows
+            if (tid == 0) a.status[b] = (nr > nrow) ? ST_FALLBACK : 0;
+            return;
+        }
+#pragma unroll
+        for (int q = 0; q < RPL; ++q)
+            if (lane + 64 * q == p) used[q] = true;
+        if (tid == 0) pivl[k] = (uint8_t)p;
+        uint4 P[QW];
+        const uint4* prow = reinterpret_cast<const uint4*>(rows + p * SW);
+#pragma unroll
+        for (int j = 0; j < (int)QW; ++j) P[j] = (w0 + NW * j < q1) ? prow[w0 + NW * j] : make_uint4(0, 0, 0, 0);
+        uint32_t pip = 0;
+#pragma unroll
+        for (int q = 0; q < RPL; ++q)
+            if ((p >> 6) == (uint32_t)q) pip = __builtin_amdgcn_readlane(pif[q], p & 63);
+        const uint32_t lgp = pip & 0xFFu;
+        // (3) the tables of c = f / f_p (the pivot lane: 1 ^ 1/f_p, which leaves row_p / f_p)
+        uint4 A[RPL];
+        uint32_t B[RPL];
+        bool act[RPL];
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+            uint32_t l;
+            if (lane + 64 * q == p) {
+                act[q] = (pif[q] >> 16) != 0;
+                l = (pif[q] >> 8) & 0xFFu;
+            } else {
+                act[q] = f[q] != 0;
+                l = (pif[q] & 0xFFu) + 255u - lgp;
+                l = l >= 255u ? l - 255u : l;
+            }
+            A[q] = tlA[l];
+            B[q] = tlB[l];
+        }
+        // columns < k are zero in the pivot row (all are earlier pivot columns): quads from k/16
+#pragma unroll
+        for (int j = 0; j < (int)QW; ++j) {
+            const uint32_t w = w0 + NW * j;
+            if (w >= q1) break;
+            const uint32_t px = __builtin_amdgcn_readfirstlane(P[j].x), py = __builtin_amdgcn_readfirstlane(P[j].y);
+            const uint32_t pz = __builtin_amdgcn_readfirstlane(P[j].z), pw = __builtin_amdgcn_readfirstlane(P[j].w);
+#pragma unroll
+            for (int q = 0; q < RPL; ++q) {
+                uint4 r = R[q][j];
+                r.x ^= perm_mul(A[q], B[q], px);
+                r.y ^= perm_mul(A[q], B[q], py);
+                r.z ^= perm_mul(A[q], B[q], pz);
+                r.w ^= perm_mul(A[q], B[q], pw);
+                if (act[q]) reinterpret_cast<uint4*>(rows + (lane + 64 * q) * SW)[w] = r;
+            }
+        }
+        __syncthreads();
+    }
+    uint8_t* xc = a.xcoef + 64ull * a.xoff[blockIdx.x];
+    const uint32_t xs = x_stride(e);
+    uint16_t* XP = a.xpiv + a.erased_off[b];
+    for (uint32_t m = tid; m < e; m += NT) XP[m] = pivl[m];
+    for (uint32_t idx = tid; idx < e * e; idx += NT) {
+        const uint32_t m = idx / e, k = idx - m * e;
+        xc[m * xs + k] = rb[pivl[k] * SW * 4 + e + pivl[m]];
+    }
+    if (tid == 0) a.status[b] = 1;
+}
+
 // One wave per block for e <= 64 on the first <= 64 received repairs, the rows held in registers:
 // lane j owns received repair j as 32 dwords (e coefficient bytes, then the identity part at byte
 // e + j).  Each step k takes the lowest unused row with a nonzero coefficient in column k (ballot),
@@ -560,9 +711,27 @@ __global__ void __launch_bounds__(256) k_solve(SolveArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
     __shared__ __attribute__((aligned(4))) uint8_t ex[512], lg[256];
     __shared__ int piv;
-    const uint32_t bi = blockIdx.x, b = a.blk_map[bi];
-    if (a.status[b] != ST_FALLBACK) return;
+    __shared__ uint32_t todo[256], ntodo;
     const uint32_t tid = threadIdx.x, nthr = blockDim.x;
+    bool tables = false;  // the exp/log tables are copied before the first block this workgroup solves
+    // A persistent grid of at most one workgroup per CU: each pass, every thread checks one block's
+    // status (all of a workgroup's checks in flight at once) and the workgroup solves the deferred
+    // ones.  Almost every decode defers none, and the launch then costs one status read per thread.
+    for (uint32_t base = blockIdx.x; base < a.n_map; base += gridDim.x * 256) {
+    if (tid == 0) ntodo = 0;
+    __syncthreads();
+    {
+        const uint32_t bi = base + tid * gridDim.x;
+        if (tid < 256 && bi < a.n_map && a.status[a.blk_map[bi]] == ST_FALLBACK) todo[atomicAdd(&ntodo, 1u)] = bi;
+    }
+    __syncthreads();
+    const uint32_t nt = ntodo;
+    for (uint32_t ti = 0; ti < nt; ++ti) {
+    const uint32_t bi = todo[ti], b = a.blk_map[bi];
+    if (!tables) {
+        gf_tables_copy(ex, lg);
+        tables = true;
+    }
     const uint32_t e = a.erased_off[b + 1] - a.erased_off[b];
     const uint32_t nr = a.rep_cnt[b];
     const uint32_t* E = a.erased + a.erased_off[b];
@@ -575,7 +744,6 @@ __global__ void __launch_bounds__(256) k_solve(SolveArgs a) {
     uint16_t* pc = reinterpret_cast<uint16_t*>(cf + ((e + 15) & ~15u));
     uint16_t* rowid = pc + ((e + 7) & ~7u);
     uint8_t* A = reinterpret_cast<uint8_t*>(rowid + ((e + 7) & ~7u));
-    gf_tables_copy(ex, lg);
     __syncthreads();
     auto gm = [&](uint8_t x, uint8_t y) -> uint8_t { return (x && y) ? ex[lg[x] + lg[y]] : (uint8_t)0; };
     uint32_t np = 0;
@@ -621,7 +789,8 @@ __global__ void __launch_bounds__(256) k_solve(SolveArgs a) {
     }
     if (np < e) {
         if (tid == 0) a.status[b] = 0;
-        return;
+        __syncthreads();
+        continue;
     }
     // basis row i solves erased column pc[i]: x_pc[i] = sum_m A[i][e + m] s_rowid[m]
     uint8_t* xc = a.xcoef + 64ull * a.xoff[bi];
@@ -633,6 +802,10 @@ __global__ void __launch_bounds__(256) k_solve(SolveArgs a) {
         xc[(size_t)m * xs + pc[i]] = A[(size_t)i * W2 + e + m];
     }
     if (tid == 0) a.status[b] = 1;
+    __syncthreads();  // the next block reuses the LDS
+    }
+    __syncthreads();  // todo / ntodo are rewritten by the next pass
+    }
 }
 
 // k_solve's working set for e erased rows (LDS when e <= lds_e, else global workspace).
@@ -670,6 +843,16 @@ static bool solve_lut() {
 #endif
 }
 
+// k_solve_pq (the default) against k_solve_pm (RQHIP_SOLVE_PQ=0 in experiments builds)
+static bool solve_pq() {
+#ifdef RQHIP_EXPERIMENTS
+    static const bool on = [] { const char* e = std::getenv("RQHIP_SOLVE_PQ"); return !(e && e[0] == '0'); }();
+    return on;
+#else
+    return true;
+#endif
+}
+
 static int solve_nw() {
 #ifdef RQHIP_EXPERIMENTS
     static const int nw = [] {
@@ -686,19 +869,36 @@ int launch_solve(const SolveArgs& a_in, uint32_t n_blocks, bool need_general, bo
                  void* stream) {
     // the first k_solve_pm launch copies the host-decided statuses (a_in.status_init); the other
     // solvers get them uploaded first, and later launches never copy
-    SolveArgs a = a_in;
+    SolveArgs first = a_in;  // the first pass copies the host-decided statuses
+    first.diag_steps = 0;
+#ifdef RQHIP_EXPERIMENTS
+    static const uint32_t dsteps = [] { const char* e = std::getenv("RQHIP_SOLVE_STEPS"); return e ? (uint32_t)std::atoi(e) : 0u; }();
+    first.diag_steps = dsteps;
+#endif
+    SolveArgs a = first;
     a.status_init = nullptr;
-    if (a_in.status_init && !(solve_pm() && solve_nw() == 4) &&
+    const bool pm_first = solve_pm() && (solve_nw() == 1 || solve_nw() == 2 || solve_nw() == 4);
+    if (a_in.status_init && !pm_first &&
         hipMemcpyAsync(a.status, a_in.status_init, (size_t)a_in.n_all * 4, hipMemcpyHostToDevice,
                        (hipStream_t)stream) != hipSuccess)
         return (int)hipGetLastError();
     switch (solve_nw()) {
-        case 1: hipLaunchKernelGGL((k_solve_fast<1, 1>), dim3(n_blocks), dim3(64), 0, (hipStream_t)stream, a); break;
+        case 1:
+            if (solve_pm() && solve_pq()) hipLaunchKernelGGL((k_solve_pq<1, 1>), dim3(n_blocks), dim3(64), 0, (hipStream_t)stream, first);
+            else if (solve_pm()) hipLaunchKernelGGL((k_solve_pm<1, 1, true>), dim3(n_blocks), dim3(64), 0, (hipStream_t)stream, first);
+            else hipLaunchKernelGGL((k_solve_fast<1, 1>), dim3(n_blocks), dim3(64), 0, (hipStream_t)stream, a);
+            break;
+        case 2:
+            if (solve_pq()) hipLaunchKernelGGL((k_solve_pq<1, 2>), dim3(n_blocks), dim3(128), 0, (hipStream_t)stream, first);
+            else hipLaunchKernelGGL((k_solve_pm<1, 2, true>), dim3(n_blocks), dim3(128), 0, (hipStream_t)stream, first);
+            break;
         case 4:
-            if (solve_pm() && solve_lut())
-                hipLaunchKernelGGL((k_solve_pm<1, 4, true>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a_in);
+            if (solve_pm() && solve_lut() && solve_pq())
+                hipLaunchKernelGGL((k_solve_pq<1, 4>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, first);
+            else if (solve_pm() && solve_lut())
+                hipLaunchKernelGGL((k_solve_pm<1, 4, true>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, first);
             else if (solve_pm())
-                hipLaunchKernelGGL((k_solve_pm<1, 4, false>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a_in);
+                hipLaunchKernelGGL((k_solve_pm<1, 4, false>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, first);
             else hipLaunchKernelGGL((k_solve_fast<1, 4>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a);
             break;
         default: hipLaunchKernelGGL(k_solve_reg, dim3(n_blocks), dim3(64), 0, (hipStream_t)stream, a); break;
@@ -706,7 +906,9 @@ int launch_solve(const SolveArgs& a_in, uint32_t n_blocks, bool need_general, bo
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !need_general) return (int)e;
     if (wide) {  // blocks with 64 < e <= 128; the rare rank-deficient-on-64-rows block goes to k_solve
-        if (solve_pm() && solve_lut())
+        if (solve_pm() && solve_lut() && solve_pq())
+            hipLaunchKernelGGL((k_solve_pq<2, 4>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a);
+        else if (solve_pm() && solve_lut())
             hipLaunchKernelGGL((k_solve_pm<2, 4, true>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a);
         else if (solve_pm())
             hipLaunchKernelGGL((k_solve_pm<2, 4, false>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a);
@@ -719,7 +921,8 @@ int launch_solve(const SolveArgs& a_in, uint32_t n_blocks, bool need_general, bo
         attr = true;
     }
     const size_t lds = solve_ws_bytes(std::min<uint32_t>(max_lds_e, a.lds_e));
-    hipLaunchKernelGGL(k_solve, dim3(n_blocks), dim3(256), lds, (hipStream_t)stream, a);
+    a.n_map = n_blocks;
+    hipLaunchKernelGGL(k_solve, dim3(std::min<uint32_t>(n_blocks, 256)), dim3(256), lds, (hipStream_t)stream, a);
     return (int)hipGetLastError();
 }
 
