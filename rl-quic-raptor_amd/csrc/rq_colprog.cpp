@@ -529,7 +529,9 @@ bool build(const Params& p, const std::vector<OutDesc>& outs, uint32_t passes, C
             while (q < v.size() && v[q] <= k) ++q;
             return q < v.size() && v[q] - k <= pend_win;
         };
-        std::vector<uint32_t> S8((size_t)H * 8, NOVAL);
+        // bit-row accumulators: two subset operands per chunk make one XOR3; a row that gets one
+        // operand keeps it pending for the next chunk's (Acc) instead of an XOR2 now
+        std::vector<Acc> S8((size_t)H * 8);
         std::vector<uint32_t> chunk;  // pivot indices of produced y (column < KS)
         auto flush = [&]() {
             if (chunk.empty()) return;
@@ -555,18 +557,15 @@ bool build(const Params& p, const std::vector<OutDesc>& outs, uint32_t passes, C
                 return s[m];
             };
             for (uint32_t h = 0; h < H; ++h)
-                for (uint32_t b = 0; b < 8; ++b) {
-                    std::vector<uint32_t> terms{S8[h * 8 + b]};
+                for (uint32_t b = 0; b < 8; ++b)
                     for (size_t g = 0; g < ng; ++g) {
                         uint32_t m = 0;
                         for (uint32_t q = 0; q < 4 && g * 4 + q < chunk.size(); ++q) {
                             const uint32_t c = e.piv_col[chunk[g * 4 + q]];
                             if ((e.G[(size_t)h * KS + c] >> b) & 1) m |= 1u << q;
                         }
-                        if (m) terms.push_back(subset(g, m));
+                        if (m) S8[h * 8 + b].push(B, subset(g, m));
                     }
-                    S8[h * 8 + b] = B.xsum(terms);
-                }
             chunk.clear();
             B.grp = 0;
         };
@@ -592,7 +591,7 @@ bool build(const Params& p, const std::vector<OutDesc>& outs, uint32_t passes, C
         B.grp = 1;
         for (uint32_t h = 0; h < H; ++h) {
             uint32_t acc = NOVAL;
-            for (int b = 7; b >= 0; --b) acc = B.xt(acc, S8[h * 8 + b]);
+            for (int b = 7; b >= 0; --b) acc = B.xt(acc, S8[h * 8 + b].get(B));
             bh_direct[h] = acc;
         }
         B.grp = 0;

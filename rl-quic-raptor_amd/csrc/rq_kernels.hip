@@ -526,13 +526,13 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
     for (uint32_t k = 0; k < ksteps; ++k) {
         // (1) this wave's row quads for the step and every row's coefficient in column k
         const uint32_t w0 = (k >> 4) + g;
-        uint4 R[RPL][QW];
+        uint4 R[RPL][QW];  // quads past q1 are neither loaded nor used (no zero fill)
 #pragma unroll
         for (int j = 0; j < (int)QW; ++j)
+            if (w0 + NW * j < q1)
 #pragma unroll
-            for (int q = 0; q < RPL; ++q)
-                R[q][j] = (w0 + NW * j < q1) ? reinterpret_cast<const uint4*>(rows + (lane + 64 * q) * SW)[w0 + NW * j]
-                                             : make_uint4(0, 0, 0, 0);
+                for (int q = 0; q < RPL; ++q)
+                    R[q][j] = reinterpret_cast<const uint4*>(rows + (lane + 64 * q) * SW)[w0 + NW * j];
         uint32_t f[RPL], pif[RPL];
 #pragma unroll
         for (int q = 0; q < RPL; ++q) f[q] = (rows[(lane + 64 * q) * SW + (k >> 2)] >> ((k & 3) * 8)) & 0xFFu;
@@ -556,7 +556,8 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
         uint4 P[QW];
         const uint4* prow = reinterpret_cast<const uint4*>(rows + p * SW);
 #pragma unroll
-        for (int j = 0; j < (int)QW; ++j) P[j] = (w0 + NW * j < q1) ? prow[w0 + NW * j] : make_uint4(0, 0, 0, 0);
+        for (int j = 0; j < (int)QW; ++j)
+            if (w0 + NW * j < q1) P[j] = prow[w0 + NW * j];
         uint32_t pip = 0;
 #pragma unroll
         for (int q = 0; q < RPL; ++q)
@@ -1054,7 +1055,8 @@ k_apply(ApplyArgs a, uint32_t n_units, uint32_t np, uint32_t MC) {
             }
         }
         // (taking the syndromes in pairs, six lookups folded by three XOR3, measured 3 % slower:
-        // profiles/r02w)
+        // profiles/r02w; skipping a last slice's padding outputs by a uniform branch per k, 188 ->
+        // 203 us: profiles/r03_dense/r03e)
         // Software pipeline: the tables of the next (m, k) and the next ring offsets are read from LDS
         // one step ahead, and sched_barrier keeps the scheduler from sinking those reads next to their
         // use (it did: one exposed LDS round trip per 25 VALU).  The last step's look-ahead reads one
