@@ -162,6 +162,15 @@ int rq_stream_release(void* stream);
  * calls this before exiting.  Any later call re-creates what it needs. */
 int rq_shutdown(void);
 
+/* Measurement (bench.py's roofline): while timing is on for the current device, every column-program
+ * launch (the encode hot path and decode's syndrome pass) is issued with start / stop events recorded
+ * by its own dispatch (hipExtModuleLaunchKernel), so the time is the kernel's alone, with no marker
+ * command between it and its neighbours.  rq_launch_time waits for the launches timed since the last
+ * reset and returns their summed milliseconds and count (reset != 0: then starts a new window).  No
+ * reference counterpart. */
+int rq_launch_timing(int enable);
+int rq_launch_time(double* ms_total, uint32_t* n_launches, int reset);
+
 /* ---------------- diagnostics (host only; tests and tools) ----------------
  * The encode hot path is a straight-line gfx950 program generated per (K', K, outputs): the
  * "column program" (rl-quic-raptor_amd/csrc/rq_colprog.hpp).  These entry points expose its

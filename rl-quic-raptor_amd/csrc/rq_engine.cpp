@@ -7,6 +7,10 @@
 // without a usable gfx950 device the calls fail with RQ_ERR_DEVICE.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Wc++20-extensions"
+#include <hip/hip_ext.h>  // hipExtModuleLaunchKernel (rq_launch_timing)
+#pragma clang diagnostic pop
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -156,6 +160,12 @@ struct DevCtx {
     // at the link's full rate instead of sharing it (all chunks' uploads finished together, and the
     // first chunk's kernels waited for the last upload: profiles/r02ae)
     hipEvent_t updone[NST] = {};
+    // rq_launch_timing: while on, every column-program launch records this pair list's next
+    // start / stop events as part of its own dispatch (hipExtModuleLaunchKernel): the kernel's time
+    // without any marker command between it and its neighbours in the stream
+    bool timing = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> tev;
+    size_t tev_used = 0;
     hipStream_t obj_stream = nullptr;  // per-object API: its own stream, pinned staging, device buffer
     HostBuf obj_h;
     DevBuf obj_d;
@@ -206,6 +216,10 @@ struct DevCtx {
         for (hipEvent_t e : updone)
             if (e) (void)hipEventDestroy(e);
         if (obj_stream) (void)hipStreamDestroy(obj_stream);
+        for (auto& pr : tev) {
+            (void)hipEventDestroy(pr.first);
+            (void)hipEventDestroy(pr.second);
+        }
     }
     void release_ws(void* stream) {
         auto it = ws.find(stream);
@@ -589,6 +603,21 @@ int launch_col(DevCtx* ctx, ColKernel* k, uint32_t T, uint32_t n_blocks, const v
         if (xcd_order() && wgs % 8 == 0) {  // the remap needs the stride to keep g % 8 fixed
             a.xcd_q = iters / 8;
             a.xcd_n = a.xcd_q * 8;
+        }
+        if (ctx->timing) {  // measurement: the dispatch itself records the kernel's start / stop
+            if (ctx->tev_used == ctx->tev.size()) {
+                hipEvent_t e0, e1;
+                HIP_TRY(hipEventCreate(&e0));
+                if (hipEventCreate(&e1) != hipSuccess) {
+                    (void)hipEventDestroy(e0);
+                    return fail(RQ_ERR_DEVICE, "hipEventCreate failed");
+                }
+                ctx->tev.push_back({e0, e1});
+            }
+            const auto& pr = ctx->tev[ctx->tev_used++];
+            HIP_TRY(hipExtModuleLaunchKernel(k->fn, wgs * 64 * Wg, 1, 1, 64 * Wg, 1, 1, 0, (hipStream_t)stream, nullptr,
+                                             cfg, pr.first, pr.second, 0));
+            continue;
         }
         HIP_TRY(hipModuleLaunchKernel(k->fn, wgs, 1, 1, 64 * Wg, 1, 1, 0, (hipStream_t)stream, nullptr, cfg));
     }
@@ -1386,6 +1415,34 @@ int rq_stream_release(void* stream) {
     std::lock_guard<std::mutex> lk(ctx->mu);
     if (ctx->internal(stream)) return fail(RQ_ERR_BAD_ARG, "not a caller stream");
     ctx->release_ws(stream);
+    return RQ_OK;
+}
+
+int rq_launch_timing(int enable) {
+    DevCtx* ctx;
+    int rc = get_ctx(&ctx);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->timing = enable != 0;
+    return RQ_OK;
+}
+
+int rq_launch_time(double* ms_total, uint32_t* n_launches, int reset) {
+    if (!ms_total || !n_launches) return fail(RQ_ERR_BAD_ARG, "null output");
+    DevCtx* ctx;
+    int rc = get_ctx(&ctx);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    double sum = 0;
+    for (size_t i = 0; i < ctx->tev_used; ++i) {
+        HIP_TRY(hipEventSynchronize(ctx->tev[i].second));
+        float ms = 0;
+        HIP_TRY(hipEventElapsedTime(&ms, ctx->tev[i].first, ctx->tev[i].second));
+        sum += ms;
+    }
+    *ms_total = sum;
+    *n_launches = (uint32_t)ctx->tev_used;
+    if (reset) ctx->tev_used = 0;  // a new window
     return RQ_OK;
 }
 

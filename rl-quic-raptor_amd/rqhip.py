@@ -43,6 +43,7 @@ EXPORTED = (
     "rq_debug_colprog_eval", "rq_debug_colprog_emulate", "rq_debug_colprog_assemble", "rq_debug_decode_margin",
     "rq_decode_blocks_host", "rq_host_alloc", "rq_host_free", "rq_debug_colprog_passes",
     "rq_debug_shard_plan", "rq_debug_virtual_shards", "rq_debug_tuple", "rq_stream_release", "rq_shutdown",
+    "rq_launch_timing", "rq_launch_time",
 )
 
 
@@ -147,6 +148,8 @@ def lib():
             "rq_debug_tuple": ([ctypes.c_uint32, ctypes.c_uint32, u32p], ctypes.c_int),
             "rq_stream_release": ([vp], ctypes.c_int),
             "rq_shutdown": ([], ctypes.c_int),
+            "rq_launch_timing": ([ctypes.c_int], ctypes.c_int),
+            "rq_launch_time": ([ctypes.POINTER(ctypes.c_double), u32p, ctypes.c_int], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -154,6 +157,20 @@ def lib():
             f.restype = res
         _lib = L
     return _lib
+
+
+def launch_timing(enable):
+    """rq_launch_timing: column-program launches of the current device record their own start/stop
+    events (the dispatch's, no stream markers) while enabled."""
+    _check(lib().rq_launch_timing(1 if enable else 0))
+
+
+def launch_time(reset=True):
+    """rq_launch_time: (summed kernel milliseconds, launch count) timed since the last reset."""
+    ms = ctypes.c_double(0)
+    n = ctypes.c_uint32(0)
+    _check(lib().rq_launch_time(ctypes.byref(ms), ctypes.byref(n), 1 if reset else 0))
+    return ms.value, n.value
 
 
 def _check(rc):

@@ -97,3 +97,28 @@ def test_device_resident_symbol_size_limit(gpu, rq):
     s8.view(2, Ks, 8)[:, :, :4] = src.view(2, Ks, 4)
     rq.encode_batch(s8, Ks, 8, list(range(Ks, Ks + 4)), o8)  # the same bytes, padded to T=8 by hand
     assert torch.equal(hout, o8.view(2, 4, 8)[:, :, :4].reshape(2, 16).cpu())
+
+
+def test_launch_timing(gpu, rq):
+    """rq_launch_timing / rq_launch_time (bench.py's roofline): only launches issued while timing is on
+    are counted, their dispatch-recorded kernel time fits inside the stream events around them, and the
+    timed launches compute the same bytes as untimed ones."""
+    src, _, _ = _case(gpu, rq, 29)
+    esis = list(range(K, N))
+    ref = torch.empty((NB, (N - K) * T), dtype=torch.uint8, device=gpu)
+    rq.encode_batch(src, K, T, esis, ref)
+    rep = torch.empty_like(ref)
+    rq.launch_time(reset=True)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    rq.launch_timing(True)
+    for _ in range(3):
+        rq.encode_batch(src, K, T, esis, rep)
+    rq.launch_timing(False)
+    b.record()
+    rq.encode_batch(src, K, T, esis, rep)  # not timed
+    torch.cuda.synchronize()
+    ms, n = rq.launch_time(reset=True)
+    assert n == 3 and 0 < ms <= a.elapsed_time(b) * 1.01, (ms, n, a.elapsed_time(b))
+    assert torch.equal(rep, ref)
+    assert rq.launch_time(reset=True) == (0.0, 0)
