@@ -130,12 +130,19 @@ struct Workspace {
     HostBuf h_idx[2];
     hipEvent_t up[2] = {nullptr, nullptr};
     DevBuf dstatus;                 // zero-copy descriptors: the solver/apply statuses stay on the device
+    // side-stream descriptor upload (the default): set n's H2D copy runs on `cs` beside the syndrome
+    // program; the caller's stream waits for `cpy[n % 2]` before the solve
+    hipStream_t cs = nullptr;
+    hipEvent_t cpy[2] = {nullptr, nullptr};
 
     uint32_t flip = 0;
     uint64_t last_use = 0;          // LRU clock (DevCtx::wsp)
     ~Workspace() {
         for (hipEvent_t& e : up)
             if (e) (void)hipEventDestroy(e);
+        for (hipEvent_t& e : cpy)
+            if (e) (void)hipEventDestroy(e);
+        if (cs) (void)hipStreamDestroy(cs);
     }
 };
 
@@ -829,8 +836,21 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     // statuses alone go to the device); `up` then marks the end of the call's kernels.  Measured
     // 1-2 % faster per step than the in-stream copy (profiles/r02aa; RQHIP_DEC_ZC=0 restores it in
     // experiments builds).
-    static const bool zero_copy = [] { const char* e = knob("RQHIP_DEC_ZC"); return !(e && e[0] == '0'); }();
-    HIP_TRY(hipEventSynchronize(w->up[set]));  // the staging's previous contents have been read
+    // Descriptor mode (RQHIP_DEC_ZC in experiments builds): 2 = side-stream upload (the default), 1 =
+    // zero copy, 0 = in-stream upload.  Measured at 1 024 blocks K=1024 (profiles/r03_solve2): zero
+    // copy leaves the solve and the apply reading every descriptor over PCIe (solve 77 us, apply 188)
+    // against 58 / 176 us from device memory, but an in-stream upload costs more than that before the
+    // solve (decode 0.663 against 0.647 ms); the side stream's copy runs beside the syndrome program.
+    static const int desc_mode = [] { const char* e = knob("RQHIP_DEC_ZC"); return e ? std::atoi(e) : 2; }();
+    const bool zero_copy = desc_mode != 0;  // statuses in dstatus, `up` after the last kernel
+    const bool side = desc_mode == 2;
+    if (side && !w->cs) {
+        HIP_TRY(hipStreamCreateWithFlags(&w->cs, hipStreamNonBlocking));
+        for (int i = 0; i < 2; ++i) HIP_TRY(hipEventCreateWithFlags(&w->cpy[i], hipEventDisableTiming));
+    }
+    // the set's staging and (zero copy / side upload) its device copy were last read by call n - 2's
+    // kernels, which precede `up[set]`
+    HIP_TRY(hipEventSynchronize(w->up[set]));
     if ((rc = w->h_idx[set].ensure(idx.size() * 4)) || (rc = w->h_status.ensure((size_t)n_blocks * 4))) return rc;
     if (w->idx[set].cap < idx.size() * 4 || w->dstatus.cap < (size_t)n_blocks * 4)
         HIP_TRY(hipStreamSynchronize((hipStream_t)stream));  // realloc: idle
@@ -838,7 +858,13 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     std::memcpy(w->h_idx[set].p, idx.data(), idx.size() * 4);
     const uint32_t* di;
     int32_t* dst_status;
-    if (zero_copy) {
+    if (side) {
+        if ((rc = w->dstatus.ensure((size_t)n_blocks * 4))) return rc;
+        HIP_TRY(hipMemcpyAsync(w->idx[set].p, w->h_idx[set].p, idx.size() * 4, hipMemcpyHostToDevice, w->cs));
+        HIP_TRY(hipEventRecord(w->cpy[set], w->cs));
+        di = w->idx[set].as<uint32_t>();
+        dst_status = w->dstatus.as<int32_t>();  // the host-decided statuses: copied by the first solver
+    } else if (zero_copy) {
         if ((rc = w->dstatus.ensure((size_t)n_blocks * 4))) return rc;
         di = static_cast<const uint32_t*>(w->h_idx[set].p);
         dst_status = w->dstatus.as<int32_t>();  // the host-decided statuses: copied by the first solver
@@ -861,7 +887,8 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     z.T = T; z.n = nz; z.pack = nullptr;
     if ((rc = launch_col(ctx, k, T, n_blocks, data, data_stride, w->r0.p, (uint64_t)uni.size() * T, stream)))
         return rc;
-    // 2) per-block solve
+    // 2) per-block solve (after the side stream's descriptor upload)
+    if (side) HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, w->cpy[set], 0));
     SolveArgs s;
     s.blk_map = di + o_map;
     s.erased_off = di + o_eoff;

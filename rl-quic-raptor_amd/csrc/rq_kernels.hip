@@ -526,13 +526,14 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
     for (uint32_t k = 0; k < ksteps; ++k) {
         // (1) this wave's row quads for the step and every row's coefficient in column k
         const uint32_t w0 = (k >> 4) + g;
-        uint4 R[RPL][QW];  // quads past q1 are neither loaded nor used (no zero fill)
+        // quads past q1 are loaded from a clamped (valid, unused) position: unconditional loads keep
+        // the compiler from carrying the arrays across iterations in register copies
+        uint4 R[RPL][QW];
 #pragma unroll
         for (int j = 0; j < (int)QW; ++j)
-            if (w0 + NW * j < q1)
 #pragma unroll
-                for (int q = 0; q < RPL; ++q)
-                    R[q][j] = reinterpret_cast<const uint4*>(rows + (lane + 64 * q) * SW)[w0 + NW * j];
+            for (int q = 0; q < RPL; ++q)
+                R[q][j] = reinterpret_cast<const uint4*>(rows + (lane + 64 * q) * SW)[min(w0 + NW * j, 8u * RPL)];
         uint32_t f[RPL], pif[RPL];
 #pragma unroll
         for (int q = 0; q < RPL; ++q) f[q] = (rows[(lane + 64 * q) * SW + (k >> 2)] >> ((k & 3) * 8)) & 0xFFu;
@@ -556,8 +557,7 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
         uint4 P[QW];
         const uint4* prow = reinterpret_cast<const uint4*>(rows + p * SW);
 #pragma unroll
-        for (int j = 0; j < (int)QW; ++j)
-            if (w0 + NW * j < q1) P[j] = prow[w0 + NW * j];
+        for (int j = 0; j < (int)QW; ++j) P[j] = prow[min(w0 + NW * j, 8u * RPL)];
         uint32_t pip = 0;
 #pragma unroll
         for (int q = 0; q < RPL; ++q)
@@ -600,13 +600,18 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
         }
         __syncthreads();
     }
+    if (ksteps < e) {  // diagnostic step limit (timing only): valid pivot rows, meaningless X
+        __syncthreads();
+        for (uint32_t m = ksteps + tid; m < e; m += NT) pivl[m] = (uint8_t)m;
+        __syncthreads();
+    }
     uint8_t* xc = a.xcoef + 64ull * a.xoff[blockIdx.x];
     const uint32_t xs = x_stride(e);
     uint16_t* XP = a.xpiv + a.erased_off[b];
     for (uint32_t m = tid; m < e; m += NT) XP[m] = pivl[m];
-    for (uint32_t idx = tid; idx < e * e; idx += NT) {
-        const uint32_t m = idx / e, k = idx - m * e;
-        xc[m * xs + k] = rb[pivl[k] * SW * 4 + e + pivl[m]];
+    for (uint32_t m = g; m < e; m += NW) {  // wave g writes rows m = g, g + NW, ... (no index division)
+        const uint32_t pm = pivl[m];
+        for (uint32_t k = lane; k < e; k += 64) xc[m * xs + k] = rb[pivl[k] * SW * 4 + e + pm];
     }
     if (tid == 0) a.status[b] = 1;
 }
