@@ -297,6 +297,31 @@ __device__ __forceinline__ void perm_tables(uint32_t c, uint4* A, uint32_t* B) {
     *B = pack(0, m[6], m[7], m[6] ^ m[7]);
 }
 
+// perm_tables of every nonzero coefficient alpha^l (l < 255), constant-initialised in device memory:
+// the solvers copy them into LDS (five dword loads per entry) instead of building 255 table sets per
+// block (~70 VALU each).
+struct alignas(16) PermTabs {
+    uint32_t A[255][4];
+    uint32_t B[255];
+};
+constexpr PermTabs make_perm_tabs() {
+    PermTabs t{};
+    const GfTabs g = make_gf_tabs();
+    for (int l = 0; l < 255; ++l) {
+        uint32_t m[8] = {g.ex[l], 0, 0, 0, 0, 0, 0, 0};
+        for (int i = 1; i < 8; ++i) m[i] = ((m[i - 1] << 1) ^ ((m[i - 1] & 0x80u) ? 0x1Du : 0u)) & 0xFFu;
+        auto lo = [&](uint32_t x) { return ((x & 1u) ? m[0] : 0u) ^ ((x & 2u) ? m[1] : 0u) ^ ((x & 4u) ? m[2] : 0u); };
+        auto pack = [](uint32_t a, uint32_t b, uint32_t c2, uint32_t d) { return a | (b << 8) | (c2 << 16) | (d << 24); };
+        t.A[l][0] = pack(0, lo(1), lo(2), lo(3));
+        t.A[l][1] = pack(lo(4), lo(5), lo(6), lo(7));
+        t.A[l][2] = pack(0, m[3], m[4], m[3] ^ m[4]);
+        t.A[l][3] = pack(m[5], m[5] ^ m[3], m[5] ^ m[4], m[5] ^ m[4] ^ m[3]);
+        t.B[l] = pack(0, m[6], m[7], m[6] ^ m[7]);
+    }
+    return t;
+}
+__device__ const PermTabs kPerm = make_perm_tabs();
+
 // c * x on four bytes with c's perm_tables: three v_perm lookups (3 + 3 + 2 bits of each byte).
 __device__ __forceinline__ uint32_t perm_mul(const uint4& A, uint32_t B, uint32_t x) {
     const uint32_t s0 = x & 0x07070707u, s1 = (x >> 3) & 0x07070707u, s2 = (x >> 6) & 0x03030303u;
@@ -494,7 +519,10 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
     const uint32_t* U = a.rep_uidx + a.rep_off[b];
     for (uint32_t i = tid; i < e; i += NT) Es[i] = E[i];
     gf_tables_copy(ex, lg);
-    for (uint32_t l = tid; l < 255; l += NT) perm_tables(kGf.ex[l], &tlA[l], &tlB[l]);
+    for (uint32_t l = tid; l < 255; l += NT) {
+        tlA[l] = make_uint4(kPerm.A[l][0], kPerm.A[l][1], kPerm.A[l][2], kPerm.A[l][3]);
+        tlB[l] = kPerm.B[l];
+    }
     for (uint32_t i = tid; i < NROWS * SW; i += NT) rows[i] = 0;
     __syncthreads();
 #pragma unroll
@@ -1030,15 +1058,19 @@ k_apply(ApplyArgs a, uint32_t n_units, uint32_t np, uint32_t MC) {
                 const uint32_t idx = i0 + 64 * u, m = idx / KC, k = idx - m * KC;
                 cv[u] = (idx < mc * KC && k0 + k < e) ? xc[(size_t)(c0 + m) * xs + k0 + k] : 0u;
             }
+            // the coefficient's tables from the constant set by its log (five loads) instead of built
+            // from its alpha-multiples (~70 VALU each); c = 0 gives all-zero tables
+            uint32_t lc[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) lc[u] = kGf.lg[cv[u]];
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 const uint32_t idx = i0 + 64 * u;
                 if (idx >= mcp * KC) break;
-                uint4 A = make_uint4(0, 0, 0, 0);
-                uint32_t B = 0;
-                perm_tables(cv[u], &A, &B);  // c = 0 gives all-zero tables
-                tA[idx] = A;
-                tB[idx] = B;
+                const bool nz = cv[u] != 0;
+                const uint32_t* pa = kPerm.A[lc[u]];
+                tA[idx] = nz ? make_uint4(pa[0], pa[1], pa[2], pa[3]) : make_uint4(0, 0, 0, 0);
+                tB[idx] = nz ? kPerm.B[lc[u]] : 0u;
             }
         }
         for (uint32_t m = lane; m < mcp + PD; m += 64) {  // byte offsets in the block (row 0 past e)
