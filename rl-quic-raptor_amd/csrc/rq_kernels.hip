@@ -911,7 +911,7 @@ int launch_solve(const SolveArgs& a_in, uint32_t n_blocks, bool need_general, bo
 #endif
     SolveArgs a = first;
     a.status_init = nullptr;
-    const bool pm_first = solve_pm() && (solve_nw() == 1 || solve_nw() == 2 || solve_nw() == 4);
+    const bool pm_first = solve_nw() == 8 || (solve_pm() && (solve_nw() == 1 || solve_nw() == 2 || solve_nw() == 4));
     if (a_in.status_init && !pm_first &&
         hipMemcpyAsync(a.status, a_in.status_init, (size_t)a_in.n_all * 4, hipMemcpyHostToDevice,
                        (hipStream_t)stream) != hipSuccess)
@@ -921,6 +921,9 @@ int launch_solve(const SolveArgs& a_in, uint32_t n_blocks, bool need_general, bo
             if (solve_pm() && solve_pq()) hipLaunchKernelGGL((k_solve_pq<1, 1>), dim3(n_blocks), dim3(64), 0, (hipStream_t)stream, first);
             else if (solve_pm()) hipLaunchKernelGGL((k_solve_pm<1, 1, true>), dim3(n_blocks), dim3(64), 0, (hipStream_t)stream, first);
             else hipLaunchKernelGGL((k_solve_fast<1, 1>), dim3(n_blocks), dim3(64), 0, (hipStream_t)stream, a);
+            break;
+        case 8:  // experiments: eight waves per block
+            hipLaunchKernelGGL((k_solve_pq<1, 8>), dim3(n_blocks), dim3(512), 0, (hipStream_t)stream, first);
             break;
         case 2:
             if (solve_pq()) hipLaunchKernelGGL((k_solve_pq<1, 2>), dim3(n_blocks), dim3(128), 0, (hipStream_t)stream, first);
