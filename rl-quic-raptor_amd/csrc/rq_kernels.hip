@@ -983,7 +983,7 @@ uint32_t solve_lds_e_max() {
 // load/store instruction is one contiguous 256-B segment).  The slice's tables are built from X
 // straight into LDS (perm_tables: A = the four 8-entry halves (b128), B = the 2-bit table), for
 // MC syndromes m at a time (one chunk whenever e <= MC).
-template <int KC, int CPL, int PD, int OCC>
+template <int KC, int CPL, int PD, int OCC, bool PAIR = false>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC)))
 k_apply(ApplyArgs a, uint32_t n_units, uint32_t np, uint32_t MC) {
     extern __shared__ __attribute__((aligned(16))) uint32_t xsh[];
@@ -1101,6 +1101,58 @@ k_apply(ApplyArgs a, uint32_t n_units, uint32_t np, uint32_t MC) {
         // one step ahead, and sched_barrier keeps the scheduler from sinking those reads next to their
         // use (it did: one exposed LDS round trip per 25 VALU).  The last step's look-ahead reads one
         // entry past the chunk (inside the allocation, launch_apply) and is discarded.
+        if constexpr (PAIR) {
+            static_assert(PD == 2, "paired syndromes take the ring two at a time");
+            // Experiments (RQHIP_APPLY_PAIR): syndromes m, m + 1 folded into each accumulator together,
+            // six lookups by three XOR3 (4.5 VALU per mul-add instead of 5); both syndromes' fields and
+            // both tables live at once.
+            uint4 An0 = tA[0], An1 = tA[KC];
+            uint32_t Bn0 = tB[0], Bn1 = tB[KC];
+            for (uint32_t mb = 0; mb < mcp; mb += 2) {
+                uint32_t f0[2][CPL], f1[2][CPL], f2[2][CPL];
+#pragma unroll
+                for (int d = 0; d < 2; ++d)
+#pragma unroll
+                    for (int j = 0; j < CPL; ++j) {
+                        const uint32_t x = ra[d][j] ^ rb[d][j];
+                        f0[d][j] = x & 0x07070707u;
+                        f1[d][j] = (x >> 3) & 0x07070707u;
+                        f2[d][j] = (x >> 6) & 0x03030303u;
+                    }
+#pragma unroll
+                for (int d = 0; d < 2; ++d) {  // the next pair's rows (row 0 past e)
+                    const int sr = (int)__builtin_amdgcn_readfirstlane(offr[mb + 2 + d]);
+                    const int s0o = (int)__builtin_amdgcn_readfirstlane(off0[mb + 2 + d]);
+#pragma unroll
+                    for (int j = 0; j < CPL; ++j) {
+                        ra[d][j] = __builtin_amdgcn_raw_buffer_load_b32(rsR, (int)vo[j], sr, 0);
+                        rb[d][j] = __builtin_amdgcn_raw_buffer_load_b32(rs0, (int)vo[j], s0o, 0);
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < KC; ++k) {
+                    const uint4 A0 = An0, A1 = An1;
+                    const uint32_t B0 = Bn0, B1 = Bn1;
+                    const uint32_t n0 = (k + 1 < KC) ? mb * KC + k + 1 : (mb + 2) * KC;
+                    An0 = tA[n0];
+                    Bn0 = tB[n0];
+                    An1 = tA[n0 + KC];
+                    Bn1 = tB[n0 + KC];
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int j = 0; j < CPL; ++j) {
+                        const uint32_t p0 = __builtin_amdgcn_perm(A0.y, A0.x, f0[0][j]);
+                        const uint32_t p1 = __builtin_amdgcn_perm(A0.w, A0.z, f1[0][j]);
+                        const uint32_t p2 = __builtin_amdgcn_perm(B0, B0, f2[0][j]);
+                        const uint32_t q0 = __builtin_amdgcn_perm(A1.y, A1.x, f0[1][j]);
+                        const uint32_t q1 = __builtin_amdgcn_perm(A1.w, A1.z, f1[1][j]);
+                        const uint32_t q2 = __builtin_amdgcn_perm(B1, B1, f2[1][j]);
+                        acc[k][j] = xor3(xor3(xor3(acc[k][j], p0, p1), p2, q0), q1, q2);
+                    }
+                }
+            }
+            continue;
+        }
         uint4 An = tA[0];
         uint32_t Bn = tB[0];
         uint32_t nsr = offr[PD], ns0o = off0[PD];  // read one step ahead, made scalar at use
@@ -1167,6 +1219,14 @@ static void launch_apply_cpl(const ApplyArgs& a, uint32_t kc, dim3 g, uint32_t e
     // LDS (e ~ 58, KC 8: 9.8 KB per wave)
     const size_t mcx = (ec + PD - 1) / PD * PD;
     const size_t lds = std::max(lds_min, mcx * kc * 20 + (mcx + PD) * 8 + 16);
+#ifdef RQHIP_EXPERIMENTS
+    static const bool pair = [] { const char* e = std::getenv("RQHIP_APPLY_PAIR"); return e && e[0] == '1'; }();
+    if constexpr (PD == 2 && KCMAX == 8)
+        if (pair && kc == 8) {  // the look-ahead of the last pair reads up to 2 KC entries past the chunk
+            hipLaunchKernelGGL((k_apply<8, CPL, 2, OCC, true>), g, dim3(64), lds + 40 * kc, st, a, nu, np, mc);
+            return;
+        }
+#endif
     if (kc <= 4) { hipLaunchKernelGGL((k_apply<4, CPL, PD, OCC>), g, dim3(64), lds, st, a, nu, np, mc); return; }
     if constexpr (KCMAX > 8) {
         switch (kc) {
