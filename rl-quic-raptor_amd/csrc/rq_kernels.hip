@@ -1094,18 +1094,18 @@ k_apply(ApplyArgs a, uint32_t n_units, uint32_t np, uint32_t MC) {
                 }
             }
         }
-        // (taking the syndromes in pairs, six lookups folded by three XOR3, measured 3 % slower:
-        // profiles/r02w; skipping a last slice's padding outputs by a uniform branch per k, 188 ->
-        // 203 us: profiles/r03_dense/r03e)
+        // (round 2 measured the syndromes in pairs 3 % slower, profiles/r02w; the round-3 pair loop
+        // above is 4 % faster; skipping a last slice's padding outputs by a uniform branch per k, 188
+        // -> 203 us: profiles/r03_dense/r03e)
         // Software pipeline: the tables of the next (m, k) and the next ring offsets are read from LDS
         // one step ahead, and sched_barrier keeps the scheduler from sinking those reads next to their
         // use (it did: one exposed LDS round trip per 25 VALU).  The last step's look-ahead reads one
         // entry past the chunk (inside the allocation, launch_apply) and is discarded.
         if constexpr (PAIR) {
             static_assert(PD == 2, "paired syndromes take the ring two at a time");
-            // Experiments (RQHIP_APPLY_PAIR): syndromes m, m + 1 folded into each accumulator together,
-            // six lookups by three XOR3 (4.5 VALU per mul-add instead of 5); both syndromes' fields and
-            // both tables live at once.
+            // Syndromes m, m + 1 folded into each accumulator together: six lookups by three XOR3 (4.5
+            // VALU per mul-add instead of 5); both syndromes' fields and both tables live at once (11
+            // VGPRs spill at KC 8, CPL 5 under the four-waves-per-SIMD bound, and it is still faster).
             uint4 An0 = tA[0], An1 = tA[KC];
             uint32_t Bn0 = tB[0], Bn1 = tB[KC];
             for (uint32_t mb = 0; mb < mcp; mb += 2) {
@@ -1219,14 +1219,25 @@ static void launch_apply_cpl(const ApplyArgs& a, uint32_t kc, dim3 g, uint32_t e
     // LDS (e ~ 58, KC 8: 9.8 KB per wave)
     const size_t mcx = (ec + PD - 1) / PD * PD;
     const size_t lds = std::max(lds_min, mcx * kc * 20 + (mcx + PD) * 8 + 16);
+    // Syndromes in pairs (the default at PD = 2; RQHIP_APPLY_PAIR=0 in experiments builds restores the
+    // one-at-a-time loop): 185 -> 178 us at 1 024 blocks K=1024, two interleaved rounds on one box
+    // (profiles/r03_apply2).  The look-ahead of a chunk's last pair reads up to 2 KC table entries past
+    // it, hence the slack.
 #ifdef RQHIP_EXPERIMENTS
-    static const bool pair = [] { const char* e = std::getenv("RQHIP_APPLY_PAIR"); return e && e[0] == '1'; }();
-    if constexpr (PD == 2 && KCMAX == 8)
-        if (pair && kc == 8) {  // the look-ahead of the last pair reads up to 2 KC entries past the chunk
-            hipLaunchKernelGGL((k_apply<8, CPL, 2, OCC, true>), g, dim3(64), lds + 40 * kc, st, a, nu, np, mc);
+    static const bool pair = [] { const char* e = std::getenv("RQHIP_APPLY_PAIR"); return !(e && e[0] == '0'); }();
+#else
+    constexpr bool pair = true;
+#endif
+    if constexpr (PD == 2 && KCMAX == 8) {
+        if (pair && kc <= 4) {
+            hipLaunchKernelGGL((k_apply<4, CPL, 2, OCC, true>), g, dim3(64), lds + 40 * 4, st, a, nu, np, mc);
             return;
         }
-#endif
+        if (pair && kc == 8) {
+            hipLaunchKernelGGL((k_apply<8, CPL, 2, OCC, true>), g, dim3(64), lds + 40 * 8, st, a, nu, np, mc);
+            return;
+        }
+    }
     if (kc <= 4) { hipLaunchKernelGGL((k_apply<4, CPL, PD, OCC>), g, dim3(64), lds, st, a, nu, np, mc); return; }
     if constexpr (KCMAX > 8) {
         switch (kc) {
