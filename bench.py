@@ -323,7 +323,7 @@ def run_config2(args):
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
-    sampled = [s for s in range(args.steps) if s % 5 == 1] or [0]  # timing events on a sample (config 3)
+    sampled = [s for s in range(args.steps) if s % 2 == 1] or [0]  # timing events on a sample (config 3)
     ev = {s: tuple(torch.cuda.Event(enable_timing=True) for _ in range(2)) for s in sampled}
     rqhip.launch_time(reset=True)
     t0 = time.perf_counter()
@@ -517,10 +517,10 @@ def main():
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
-    # Timing events on a sample of the timed steps (every fifth, from the second): the stream markers and
-    # the dispatch-recorded events of rq_launch_timing add ~1 % each to a step they bracket
-    # (profiles/r03_dense/r03tb, r03f), so the other steps run as a caller would run them.
-    sampled = [s for s in range(args.steps) if s % 5 == 1] or [0]
+    # Timing events on every other timed step (from the second): the stream markers and the
+    # dispatch-recorded events of rq_launch_timing add ~1 % each to a step they bracket
+    # (profiles/r03_dense/r03tb, r03f), so the other half run as a caller would run them.
+    sampled = [s for s in range(args.steps) if s % 2 == 1] or [0]
     ev = {s: tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for s in sampled}
     rqhip.launch_time(reset=True)
     t0 = time.perf_counter()
