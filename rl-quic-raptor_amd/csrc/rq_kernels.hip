@@ -499,8 +499,9 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
     __shared__ __attribute__((aligned(4))) uint8_t ex[512], lg[256];
     __shared__ uint8_t pivl[NROWS];
     __shared__ uint32_t Es[NROWS];
-    __shared__ __attribute__((aligned(16))) uint4 tlA[255];
-    __shared__ uint32_t tlB[255];
+    // tables by log, twice over (entry l + 255 = entry l), so that log f - log f_p + 255 needs no mod
+    __shared__ __attribute__((aligned(16))) uint4 tlA[510];
+    __shared__ uint32_t tlB[510];
     __shared__ uint32_t pinfo[256];
     const uint32_t b = a.blk_map[blockIdx.x];
     const uint32_t tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
@@ -519,9 +520,10 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
     const uint32_t* U = a.rep_uidx + a.rep_off[b];
     for (uint32_t i = tid; i < e; i += NT) Es[i] = E[i];
     gf_tables_copy(ex, lg);
-    for (uint32_t l = tid; l < 255; l += NT) {
-        tlA[l] = make_uint4(kPerm.A[l][0], kPerm.A[l][1], kPerm.A[l][2], kPerm.A[l][3]);
-        tlB[l] = kPerm.B[l];
+    for (uint32_t l = tid; l < 510; l += NT) {
+        const uint32_t lm = l < 255 ? l : l - 255;
+        tlA[l] = make_uint4(kPerm.A[lm][0], kPerm.A[lm][1], kPerm.A[lm][2], kPerm.A[lm][3]);
+        tlB[l] = kPerm.B[lm];
     }
     for (uint32_t i = tid; i < NROWS * SW; i += NT) rows[i] = 0;
     __syncthreads();
@@ -590,22 +592,16 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
 #pragma unroll
         for (int q = 0; q < RPL; ++q)
             if ((p >> 6) == (uint32_t)q) pip = __builtin_amdgcn_readlane(pif[q], p & 63);
-        const uint32_t lgp = pip & 0xFFu;
+        const uint32_t ilgp = 255u - (pip & 0xFFu);  // log(1 / f_p) + 255 - 255, uniform
         // (3) the tables of c = f / f_p (the pivot lane: 1 ^ 1/f_p, which leaves row_p / f_p)
         uint4 A[RPL];
         uint32_t B[RPL];
         bool act[RPL];
 #pragma unroll
         for (int q = 0; q < RPL; ++q) {
-            uint32_t l;
-            if (lane + 64 * q == p) {
-                act[q] = (pif[q] >> 16) != 0;
-                l = (pif[q] >> 8) & 0xFFu;
-            } else {
-                act[q] = f[q] != 0;
-                l = (pif[q] & 0xFFu) + 255u - lgp;
-                l = l >= 255u ? l - 255u : l;
-            }
+            const bool piv = lane + 64 * q == p;
+            act[q] = piv ? (pif[q] >> 16) != 0 : f[q] != 0;
+            const uint32_t l = piv ? (pif[q] >> 8) & 0xFFu : (pif[q] & 0xFFu) + ilgp;  // < 510
             A[q] = tlA[l];
             B[q] = tlB[l];
         }
@@ -959,7 +955,11 @@ int launch_solve(const SolveArgs& a_in, uint32_t n_blocks, bool need_general, bo
     }
     const size_t lds = solve_ws_bytes(std::min<uint32_t>(max_lds_e, a.lds_e));
     a.n_map = n_blocks;
-    hipLaunchKernelGGL(k_solve, dim3(std::min<uint32_t>(n_blocks, 256)), dim3(256), lds, (hipStream_t)stream, a);
+    uint32_t grid = std::min<uint32_t>(n_blocks, 256);
+#ifdef RQHIP_EXPERIMENTS
+    if (const char* g = std::getenv("RQHIP_GSOLVE_GRID")) grid = std::max(1, std::min(256, std::atoi(g)));
+#endif
+    hipLaunchKernelGGL(k_solve, dim3(grid), dim3(256), lds, (hipStream_t)stream, a);
     return (int)hipGetLastError();
 }
 
