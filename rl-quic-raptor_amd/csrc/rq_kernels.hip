@@ -1234,7 +1234,17 @@ static void launch_apply_cpl(const ApplyArgs& a, uint32_t kc, dim3 g, uint32_t e
             return;
         }
         if (pair && kc == 8) {
-            hipLaunchKernelGGL((k_apply<8, CPL, 2, OCC, true>), g, dim3(64), lds + 40 * 8, st, a, nu, np, mc);
+            // the KC = 8 pair loop at three waves per SIMD: under four's 128 VGPRs it spills 11 (CPL 5);
+            // 170.9 against 177.1 us, three interleaved rounds (profiles/r03_apply2/occ);
+            // RQHIP_APPLY_PAIROCC=4 in experiments builds restores four
+#ifdef RQHIP_EXPERIMENTS
+            static const bool occ4p = [] { const char* e = std::getenv("RQHIP_APPLY_PAIROCC"); return e && e[0] == '4'; }();
+            if (occ4p) {
+                hipLaunchKernelGGL((k_apply<8, CPL, 2, OCC, true>), g, dim3(64), lds + 40 * 8, st, a, nu, np, mc);
+                return;
+            }
+#endif
+            hipLaunchKernelGGL((k_apply<8, CPL, 2, 3, true>), g, dim3(64), lds + 40 * 8, st, a, nu, np, mc);
             return;
         }
     }
