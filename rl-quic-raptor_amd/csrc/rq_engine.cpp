@@ -1476,8 +1476,13 @@ int rq_launch_time(double* ms_total, uint32_t* n_launches, int reset) {
 int rq_shutdown(void) {
     std::lock_guard<std::mutex> lk(g_ctx_mu);
     for (auto& kv : g_ctx) {
-        std::lock_guard<std::mutex> l2(kv.second->mu);
-        std::unique_ptr<DevCtx> c = std::move(kv.second);
+        std::unique_ptr<DevCtx> c;
+        {
+            // wait for a call in flight on the context, then take it out of the map; the lock is
+            // released before the context (and its mutex) is destroyed, never after
+            std::lock_guard<std::mutex> l2(kv.second->mu);
+            c = std::move(kv.second);
+        }
         c.reset();  // ~DevCtx: device sync, then every buffer, module, stream and event of the device
     }
     g_ctx.clear();
