@@ -159,7 +159,8 @@ int rq_stream_release(void* stream);
 /* Releases every device resource of the library (workspaces, compiled programs, internal streams and
  * events, staging) after synchronising each device.  Optional: nothing is released at process exit
  * (static teardown may run after the HIP runtime's), so a process that wants a clean HIP teardown
- * calls this before exiting.  Any later call re-creates what it needs. */
+ * calls this before exiting.  Any later call re-creates what it needs.  It waits for a call already
+ * holding a device's context, but no other library call may start on any thread until it returns. */
 int rq_shutdown(void);
 
 /* Measurement (bench.py's roofline): while timing is on for the current device, every column-program
