@@ -122,16 +122,18 @@ def encode_position():
 
 def encode_position2():
     """[encode, decode] x 12 with the bench's buffers, with alternating outputs, and with the encode
-    reading the decode's data buffer (run under a kernel trace)."""
+    reading the decode's data buffer (run under a kernel trace); PROBE_INTERLEAVE=1 rotates the three
+    modes step by step instead."""
     torch, src, rep, data, db, esis, s, recv = _config3()
     rep2 = torch.empty_like(rep)
-    for mode in range(3):
-        for i in range(12):
-            a = data if mode == 2 else src
-            o = (rep2 if i % 2 else rep) if mode == 1 else rep
-            rqhip.encode_batch(a, K3, T3, esis, o, stream=s)
-            db.run_async(data, recv, stream=s)
-        torch.cuda.synchronize()
+    interleave = os.environ.get("PROBE_INTERLEAVE") == "1"  # modes rotate per step (no clock drift)
+    order = [i % 3 for i in range(36)] if interleave else [m for m in range(3) for _ in range(12)]
+    for i, mode in enumerate(order):
+        a = data if mode == 2 else src
+        o = (rep2 if i % 2 else rep) if mode == 1 else rep
+        rqhip.encode_batch(a, K3, T3, esis, o, stream=s)
+        db.run_async(data, recv, stream=s)
+    torch.cuda.synchronize()
     print("done")
 
 
