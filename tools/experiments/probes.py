@@ -4,6 +4,8 @@
   python tools/experiments/probes.py host_enqueue    cost of the bench's timing events and host enqueue
   python tools/experiments/probes.py encode_position encode launch by position in the step / buffer
   python tools/experiments/probes.py encode_position2 encode launch in three step shapes
+  python tools/experiments/probes.py out_offset      encode launch by the output buffer's placement
+  python tools/experiments/probes.py launch_order    column-program launch after an apply vs after itself
 
 Set RQHIP_LIB to probe another library build."""
 import os
@@ -128,17 +130,63 @@ def encode_position2():
     rep2 = torch.empty_like(rep)
     interleave = os.environ.get("PROBE_INTERLEAVE") == "1"  # modes rotate per step (no clock drift)
     order = [i % 3 for i in range(36)] if interleave else [m for m in range(3) for _ in range(12)]
+    idle = os.environ.get("PROBE_IDLE") == "1"  # mode 1 instead: the bench's buffers, 2 ms idle before the encode
     for i, mode in enumerate(order):
+        if idle and mode == 1:
+            torch.cuda.synchronize()
+            time.sleep(0.002)
         a = data if mode == 2 else src
-        o = (rep2 if i % 2 else rep) if mode == 1 else rep
+        o = (rep2 if i % 2 else rep) if mode == 1 and not idle else rep
         rqhip.encode_batch(a, K3, T3, esis, o, stream=s)
         db.run_async(data, recv, stream=s)
     torch.cuda.synchronize()
     print("done")
 
 
+def out_offset():
+    """[encode, decode] steps with the encode's output buffer placed at byte offsets 0 / 256 / 4 KiB /
+    64 KiB / 1 MiB / 2 MiB + 4 KiB into one allocation, offsets rotating step by step (run under a
+    kernel trace): does the output's placement relative to the source change the launch?"""
+    torch, src, rep, data, db, esis, s, recv = _config3()
+    offs = [0, 256, 4096, 65536, 1 << 20, (2 << 20) + 4096]
+    n = rep.numel()
+    big = torch.empty(n + max(offs), dtype=torch.uint8, device=src.device)
+    print("src %#x data %#x rep %#x big %#x" % (src.data_ptr(), data.data_ptr(), rep.data_ptr(), big.data_ptr()))
+    outs = [big[o:o + n].view(rep.shape) for o in offs]
+    for i in range(6 * 8):
+        rqhip.encode_batch(src, K3, T3, esis, outs[i % 6], stream=s)
+        db.run_async(data, recv, stream=s)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[(6 * 8 - 1) % 6], rep)  # the views overlap: only the last one written is whole
+    print("done")
+
+
+def launch_order():
+    """Alternating steps A = [encode(src -> rep), decode, decode] and B = [encode(src -> rep),
+    encode(src -> rep2), decode], 12 of each (run under a kernel trace): the column program's time
+    after an apply against after another column-program launch, for both the encode and the syndrome."""
+    torch, src, rep, data, db, esis, s, recv = _config3()
+    rep2 = torch.empty_like(rep)
+    if os.environ.get("PROBE_WARM") == "1":  # A becomes [256 MiB device copy, encode, decode, decode]
+        wa = torch.empty(256 << 20, dtype=torch.uint8, device=src.device)
+        wb = torch.empty_like(wa)
+    for i in range(24):
+        if os.environ.get("PROBE_WARM") == "1" and i % 2 == 0:
+            with torch.cuda.stream(s):
+                wb.copy_(wa)
+        rqhip.encode_batch(src, K3, T3, esis, rep, stream=s)
+        if i % 2:
+            rqhip.encode_batch(src, K3, T3, esis, rep2, stream=s)
+            db.run_async(data, recv, stream=s)
+        else:
+            db.run_async(data, recv, stream=s)
+            db.run_async(data, recv, stream=s)
+    torch.cuda.synchronize()
+    print("done")
+
+
 if __name__ == "__main__":
-    cmds = {f.__name__: f for f in (perobj, host_enqueue, encode_position, encode_position2)}
+    cmds = {f.__name__: f for f in (perobj, host_enqueue, encode_position, encode_position2, out_offset, launch_order)}
     if len(sys.argv) != 2 or sys.argv[1] not in cmds:
         raise SystemExit("usage: probes.py {%s}" % "|".join(cmds))
     cmds[sys.argv[1]]()
