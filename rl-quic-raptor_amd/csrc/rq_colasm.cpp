@@ -764,6 +764,33 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
         std::snprintf(buf, sizeof buf, "s_mov_b32 s%u, %u", 56 + j, 4096u * (j + 1));
         line(buf);
     }
+    // Code warm-up (W = 1): the program is ~180 KB of straight-line code that every wave starts at
+    // once, and when the previous kernel was not a column program its lines are in neither L2 nor the
+    // memory-side cache, so round 1's instruction fetches go to HBM one after another (12-15 us per
+    // launch after a decode's apply, ~30 us after a large copy: profiles/r03_dense/r03pos).  Each wave
+    // reads four 8 KiB strides of its own code (one dword per 128-B line; slice (wg / 8) % 32 within
+    // its XCD), so the XCD's waves pull the whole program into their L2 in parallel, then wait once.
+    // Bounds-checked buffer loads (num_records = code length): nothing beyond the code is read.
+    static const bool code_pf = [] { const char* e = knob("RQHIP_CODEPF"); return !e || e[0] != '0'; }();
+    if (W == 1 && code_pf && !(diag & 4) && mp.n_vgpr >= 12) {  // v5, v6, v8..v11 are program registers
+        line("s_getpc_b64 s[44:45]");
+        s += ".Lcpf:\n";
+        line(("s_sub_u32 s44, s44, .Lcpf-" + kname).c_str());
+        line("s_subb_u32 s45, s45, 0");
+        line("s_and_b32 s45, s45, 0xffff");
+        line(("s_mov_b32 s46, .Lfunc_end-" + kname).c_str());
+        line("s_mov_b32 s47, 0x20000");
+        line("s_lshr_b32 s43, s2, 3");
+        line("s_and_b32 s43, s43, 31");
+        line("s_lshl_b32 s43, s43, 13");
+        line("v_lshlrev_b32_e32 v5, 7, v0");
+        line("v_add_u32_e32 v5, s43, v5");
+        for (uint32_t k = 0; k < 4; ++k) {
+            std::snprintf(buf, sizeof buf, "v_add_u32_e32 v6, 0x%x, v5", k * 32u * 8192u); line(buf);
+            std::snprintf(buf, sizeof buf, "buffer_load_dword v%u, v6, s[44:47], 0 offen", 8 + k); line(buf);
+        }
+        line("s_waitcnt vmcnt(0)");
+    }
     // experiments: RQHIP_STAGGER=n delays the odd workgroups' start by n x 127 x 64 cycles (do the
     // first rounds' coinciding load bursts cost time?)
     static const uint32_t stagger = [] { const char* e = knob("RQHIP_STAGGER"); return e ? (uint32_t)std::atoi(e) : 0u; }();
