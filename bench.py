@@ -71,7 +71,7 @@ def rank_env(world, rank, port):
     """Environment of rank `rank` of a `world`-rank run on this node (what torch.distributed.run sets)."""
     env = dict(os.environ)
     env.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
-               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RQHIP_BENCH_SPAWNED="1")
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     return env
 
@@ -91,9 +91,12 @@ def launch_plan(args, world):
 def spawn_ranks(args):
     """`--gpus N` without a launcher: start N rank processes of this script (one per GPU, rank r on GPU r)
     before this process touches the GPU, and exit with the first non-zero rank status.  Rank 0 prints the
-    JSON line.  (Under `torch.distributed.run` WORLD_SIZE is already set and no process is spawned.)"""
+    JSON line.  (Under `torch.distributed.run` WORLD_SIZE is already set and no process is spawned.)
+    The parent builds librqhip.so first if it is missing (rqhip.ensure_built: no GPU call), so the ranks
+    never race one build or load a half-written library."""
     import socket
     import subprocess
+    rqhip.ensure_built()
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
@@ -164,18 +167,40 @@ def cpu_run(K, T, N, n_erase, n_blocks, threads, seed):
     return t_enc, t_dec
 
 
+def host_cores():
+    """Threads the CPU baseline may use on this host, and where that number comes from: the smallest of
+    the process's CPU affinity, its cgroup CPU quota and OMP_NUM_THREADS (the GPU box sets 16 for its
+    share of a larger machine), at most 16."""
+    lim = {"affinity": len(os.sched_getaffinity(0))}
+    try:  # cgroup v2: "quota period" or "max period"
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            lim["cgroup_quota"] = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    try:
+        if os.environ.get("OMP_NUM_THREADS"):
+            lim["OMP_NUM_THREADS"] = max(1, int(os.environ["OMP_NUM_THREADS"]))
+    except ValueError:
+        pass
+    lim["cap"] = 16
+    src = min(lim, key=lambda k: lim[k])
+    return lim[src], "%s (%s)" % (src, ", ".join("%s %d" % kv for kv in lim.items()))
+
+
 def cpu_baseline(K, T, N, n_erase, n_blocks):
     """CPU baseline on the box's host cores: librqcpu.so, the C++ port of this
     engine's algorithm (the same column program evaluated in 64-byte strips; syndrome decode with
     AVX2 split-nibble GF(256) mul-adds, the reference's asmSSSE3MulAdd technique), on a bounded
-    sample of the same workload: all cores of the box's share (16 threads, one block per thread at a
-    time) as the reported value, and 1 thread beside it.  The oracle is only the checker (tests)."""
-    threads = max(1, min(16, os.cpu_count() or 1))  # the GPU box's CPU share is 16 cores
+    sample of the same workload: all cores of the process's share (host_cores, one block per thread at
+    a time) as the reported value, and 1 thread beside it.  The oracle is only the checker (tests)."""
+    threads, cores_src = host_cores()
     te1, td1 = cpu_run(K, T, N, n_erase, max(8, n_blocks // 8), 1, 4242)
     nb1 = max(8, n_blocks // 8)
     teN, tdN = cpu_run(K, T, N, n_erase, n_blocks, threads, 9000)
     gb = lambda nb, t: round(nb * K * T / t / 1e9, 4)
-    return {"value": gb(n_blocks, teN + tdN), "unit": "GB/s", "cores": threads, "kind": "port",
+    return {"value": gb(n_blocks, teN + tdN), "unit": "GB/s", "cores": threads, "cores_source": cores_src,
+            "kind": "port",
             "sample": "%d blocks K=%d T=%d N=%d, %d of N erased, %d threads on '%s' (os.cpu_count %d): "
                       "librqcpu.so (C++ port of this engine's column-program encode + syndrome decode, bit-exact "
                       "to the oracle), encode %.3f s, decode %.3f s" % (n_blocks, K, T, N, n_erase, threads, cpu_model(),
@@ -190,7 +215,7 @@ def cpu_baseline_encode(K, T, esis, n_blocks):
     """Config 2's CPU baseline: librqcpu.so encode (the same column program on host cores) of a sample of
     the same workload, 16 threads (the GPU box's CPU share) and 1 thread."""
     import rqcpu
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads, cores_src = host_cores()
     rng = np.random.default_rng(4343)
     src = rng.integers(0, 256, (n_blocks, K * T), dtype=np.uint8)
     rqcpu.encode(src[:1], K, T, esis)  # program compile outside the timed region, as on the GPU
@@ -202,7 +227,7 @@ def cpu_baseline_encode(K, T, esis, n_blocks):
     rqcpu.encode(src[:n1], K, T, esis, 1)
     t1 = time.perf_counter() - t0
     gb = lambda nb, t: round(nb * K * T / t / 1e9, 4)
-    return {"value": gb(n_blocks, tN), "unit": "GB/s", "cores": threads, "kind": "port",
+    return {"value": gb(n_blocks, tN), "unit": "GB/s", "cores": threads, "cores_source": cores_src, "kind": "port",
             "sample": "%d blocks K=%d T=%d, %d repairs, %d threads on '%s': librqcpu.so encode (the engine's column "
                       "program on host cores, bit-exact to the oracle), %.3f s" % (n_blocks, K, T, len(esis), threads,
                                                                                  cpu_model(), tN),
@@ -213,7 +238,7 @@ def cpu_baseline_mixed(shapes, frac_div):
     """Config 5's CPU baseline: librqcpu.so encode + decode of a sample of every shape of the stream (1 /
     frac_div of its blocks, at least 2), 16 threads; every decode checked against the source."""
     import rqcpu
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads, cores_src = host_cores()
     t_all, nbytes = 0.0, 0
     for sh in shapes:
         K, T, B = sh["K"], sh["T"], max(2, sh["B"] // frac_div)
@@ -234,7 +259,8 @@ def cpu_baseline_mixed(shapes, frac_div):
         ok = st == 1
         assert np.array_equal(data[ok], src[ok]), "CPU baseline decode mismatch"
         nbytes += B * K * T
-    return {"value": round(nbytes / t_all / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": "port",
+    return {"value": round(nbytes / t_all / 1e9, 4), "unit": "GB/s", "cores": threads, "cores_source": cores_src,
+            "kind": "port",
             "sample": "1/%d of every shape's blocks (>= 2), encode + decode from host memory, %d threads on '%s': "
                       "librqcpu.so (bit-exact to the oracle)" % (frac_div, threads, cpu_model())}
 
@@ -295,6 +321,13 @@ def dist_setup(args):
         dist = tdist
         print("bench.py: rank %d of %d on GPU %d (%s)" % (rank, world, gpu, args.dist_backend), file=sys.stderr,
               flush=True)
+        # every rank owns a distinct GPU under RCCL (gloo may share one GPU in a rehearsal)
+        owners = [None] * world
+        tdist.all_gather_object(owners, (rank, gpu, torch.cuda.device_count()))
+        if args.dist_backend == "nccl":
+            gpus = [o[1] for o in owners]
+            if len(set(gpus)) != world or any(o[2] < world for o in owners):
+                raise SystemExit("bench.py: ranks do not own distinct GPUs: %s" % owners)
     rqhip.lib().rq_set_device(gpu)
     coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
     return world, rank, dist, dev, coll_dev
@@ -337,10 +370,16 @@ def run_config2(args):
             rqhip.launch_timing(False)
             ev[s][1].record(stream)
     torch.cuda.synchronize()
+    t_rank = time.perf_counter() - t0
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     dt = rqshard.max_over_ranks(time.perf_counter() - t0, dist, coll_dev)
+    rank_ms = [t / args.steps * 1e3 for t in rqshard.all_over_ranks(t_rank, dist, coll_dev)]
+    if not args.no_verify:  # the timed launches' output, checked after the loop
+        import rqcpu
+        assert np.array_equal(rep[-8:].cpu().numpy(), rqcpu.encode(src[-8:].cpu().numpy(), K, T, esis)), \
+            "config 2 repairs differ from the CPU port after the timed loop"
     enc_ms = float(np.mean([a.elapsed_time(b) for a, b in ev.values()]))
     kern_ms, n_launch = rqhip.launch_time(reset=True)
     total = rqshard.sum_over_ranks(B, dist, coll_dev)
@@ -355,7 +394,8 @@ def run_config2(args):
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (seeded torch.randint payload)",
             "config": {"workload": "encode-only K=%d T=%d, %d repairs per block" % (K, T, R), "blocks_per_gpu": B,
-                       "verified_blocks_vs_cpu_port": 0 if args.no_verify else 8},
+                       "verified_blocks_vs_cpu_port": 0 if args.no_verify else 16,
+                       "rank_ms_per_step": {"min": round(min(rank_ms), 4), "max": round(max(rank_ms), 4)}},
             "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic, "traffic_source": traffic_src, "algorithmic_bytes_per_launch": B * K * T,
@@ -468,10 +508,21 @@ def main():
     if args.gpus < 1:
         raise SystemExit("bench.py: --gpus must be >= 1")
     if args.plan_only:
+        # a rehearsal of the launch without any GPU call: the parent builds the library if it is missing,
+        # then (no launcher) starts the N ranks, each of which only checks that the library is there
+        if os.environ.get("RQHIP_BENCH_SPAWNED") == "1":
+            built = rqhip.ensure_built()
+            print("bench.py --plan-only: rank %s sees %s (built here: %s)" % (os.environ.get("RANK"), rqhip.LIB_PATH, built),
+                  file=sys.stderr, flush=True)
+            return 0
         world = args.gpus
-        print(json.dumps({"world": world, "launcher": "spawn" if "WORLD_SIZE" not in os.environ else "external",
-                          "scaling": "strong" if args.total_blocks else "weak", "ranks": launch_plan(args, world)}))
-        return 0
+        launcher = "spawn" if "WORLD_SIZE" not in os.environ else "external"
+        built = rqhip.ensure_built()
+        rc = spawn_ranks(args) if launcher == "spawn" and world > 1 else 0
+        print(json.dumps({"world": world, "launcher": launcher, "scaling": "strong" if args.total_blocks else "weak",
+                          "ranks": launch_plan(args, world), "library": str(rqhip.LIB_PATH), "built_by_parent": built,
+                          "ranks_rc": rc}))
+        return rc
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return spawn_ranks(args)
     if args.config == 2:
@@ -538,12 +589,23 @@ def main():
         if samp:
             ev[s][2].record(stream)
     torch.cuda.synchronize()
+    t_rank = time.perf_counter() - t0  # this rank's own time, before the closing barrier
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     dt = rqshard.max_over_ranks(time.perf_counter() - t0, dist, coll_dev)
+    rank_ms = [t / args.steps * 1e3 for t in rqshard.all_over_ranks(t_rank, dist, coll_dev)]
     if not args.no_verify:
         assert np.array_equal(st_async, st), "async decode statuses differ"
+        # the timed decodes ran on rows already recovered (zero syndromes; the work is data-independent):
+        # poison the erased rows again and decode once more, checking bytes as well as statuses
+        rqhip.encode_batch(src, K, T, esis, rep, stream=stream)
+        data.view(B, K, T)[eb, ei] = 0x5A
+        st_post = db.run(data, recv, stream=stream)
+        torch.cuda.synchronize()
+        assert np.array_equal(st_post, st), "post-timing decode statuses differ"
+        good = torch.tensor(st_post == 1, device=dev)
+        assert torch.equal(data[good], src[good]), "post-timing decode bytes differ"
     enc_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1, _ in ev.values()]))
     dec_ms = float(np.mean([e1.elapsed_time(e2) for _, e1, e2 in ev.values()]))
     kern_ms, n_launch = rqhip.launch_time(reset=True)
@@ -563,7 +625,10 @@ def main():
             "config": {"workload": "encode+decode K=%d T=%d N=%d, erase %d of %d symbols per block" % (K, T, N, n_erase, N),
                        "blocks_per_gpu": B, "total_blocks": total_blocks, "bytes_per_gpu": B * K * T,
                        "parallelism": "block-sharded x%d" % world,
-                       "decode_ok_fraction": ok_frac, "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4)},
+                       "decode_ok_fraction": ok_frac, "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4),
+                       "rank_ms_per_step": {"min": round(min(rank_ms), 4), "max": round(max(rank_ms), 4),
+                                            "per_rank": [round(x, 4) for x in rank_ms]},
+                       "post_timing_check": "skipped" if args.no_verify else "bytes+statuses"},
             "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "traffic_source": traffic_src, "algorithmic_bytes_per_launch": B * K * T,

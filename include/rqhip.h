@@ -152,15 +152,17 @@ int rq_device_count(void);
 int rq_set_device(int device);      /* selects the HIP device for subsequent calls on this thread */
 /* The library keeps per-stream device workspaces for the batched device-resident calls (descriptors,
  * syndromes, scratch).  At most 8 caller streams per device keep one: beyond that the least recently
- * used is released (after a device synchronisation).  rq_stream_release frees the workspace of
- * `stream` (a hipStream_t; NULL = the default stream) on the current device now -- call it when a
- * stream is retired.  No reference counterpart (the Go library has no device state). */
+ * used is retired, and freed once the work of its last call has completed (an event recorded on its
+ * stream; no device synchronisation).  rq_stream_release retires the workspace of `stream` (a
+ * hipStream_t; NULL = the default stream) on the current device the same way -- call it when a stream
+ * is retired.  No reference counterpart (the Go library has no device state). */
 int rq_stream_release(void* stream);
 /* Releases every device resource of the library (workspaces, compiled programs, internal streams and
  * events, staging) after synchronising each device.  Optional: nothing is released at process exit
  * (static teardown may run after the HIP runtime's), so a process that wants a clean HIP teardown
- * calls this before exiting.  Any later call re-creates what it needs.  It waits for a call already
- * holding a device's context, but no other library call may start on any thread until it returns. */
+ * calls this before exiting.  Any later call re-creates what it needs.  Safe beside concurrent calls:
+ * each call holds its device context until it returns, and a context taken out by rq_shutdown is
+ * destroyed when the last such call returns (in that call's thread). */
 int rq_shutdown(void);
 
 /* Measurement (bench.py's roofline): while timing is on for the current device, every column-program

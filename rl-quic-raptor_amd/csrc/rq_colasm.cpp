@@ -824,7 +824,12 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
     if (n_groups) line("s_load_dwordx16 s[64:79], s[50:51], 0x0");
     uint32_t src_j = 0;
     int sr = 0;
-    auto srot = [&]() { sr = (sr + 1) & 7; return 40 + sr; };
+    // s40..s47 rotate as short-lived SALU temporaries; at W > 1, s41 holds the wave's LDS base for the
+    // whole kernel (MI_DMA's m0), so the rotation skips it
+    auto srot = [&]() {
+        do sr = (sr + 1) & 7; while (W > 1 && sr == 1);
+        return 40 + sr;
+    };
     auto scr_soff = [&](uint32_t slot) -> std::string {
         const uint32_t j = slot / 16;
         if (j == 0) return "0";

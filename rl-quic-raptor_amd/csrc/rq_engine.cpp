@@ -137,7 +137,21 @@ struct Workspace {
 
     uint32_t flip = 0;
     uint64_t last_use = 0;          // LRU clock (DevCtx::wsp)
+    // recorded on the caller's stream after every call's last command that touches this workspace:
+    // an evicted or released workspace is freed once it has completed (DevCtx::reap), so eviction
+    // never synchronises the device while the context lock is held
+    hipEvent_t last = nullptr;
+    int mark(void* stream) {
+        if (!last && hipEventCreateWithFlags(&last, hipEventDisableTiming) != hipSuccess) {
+            last = nullptr;
+            return fail(RQ_ERR_DEVICE, "hipEventCreate failed");
+        }
+        if (hipEventRecord(last, (hipStream_t)stream) != hipSuccess) return fail(RQ_ERR_DEVICE, "hipEventRecord failed");
+        return RQ_OK;
+    }
+    bool idle() const { return !last || hipEventQuery(last) != hipErrorNotReady; }
     ~Workspace() {
+        if (last) (void)hipEventDestroy(last);
         for (hipEvent_t& e : up)
             if (e) (void)hipEventDestroy(e);
         for (hipEvent_t& e : cpy)
@@ -182,7 +196,14 @@ struct DevCtx {
     // device synchronisation: its stream may still run kernels reading it); the library's own stage
     // streams are never evicted.  rq_stream_release() releases one explicitly.
     static constexpr size_t MAX_WS = 8;
+    std::vector<std::unique_ptr<Workspace>> dead;  // evicted / released, freed once idle
+    void reap() {
+        for (size_t i = 0; i < dead.size();)
+            if (dead[i]->idle()) { dead[i] = std::move(dead.back()); dead.pop_back(); }
+            else ++i;
+    }
     Workspace* wsp(void* stream) {
+        if (!dead.empty()) reap();
         auto& w = ws[stream];
         if (!w) {
             w.reset(new Workspace());
@@ -206,7 +227,7 @@ struct DevCtx {
                     (victim == ws.end() || it->second->last_use < victim->second->last_use))
                     victim = it;
             if (victim == ws.end()) return;
-            (void)hipDeviceSynchronize();
+            dead.push_back(std::move(victim->second));  // freed by reap() once its last call completed
             ws.erase(victim);
             --n_caller;
         }
@@ -215,6 +236,7 @@ struct DevCtx {
         (void)hipSetDevice(device);
         (void)hipDeviceSynchronize();
         ws.clear();
+        dead.clear();
         colk.clear();
         for (Stage& st : stage)
             if (st.s) (void)hipStreamDestroy(st.s);
@@ -231,8 +253,9 @@ struct DevCtx {
     void release_ws(void* stream) {
         auto it = ws.find(stream);
         if (it == ws.end()) return;
-        (void)hipDeviceSynchronize();
+        dead.push_back(std::move(it->second));
         ws.erase(it);
+        reap();
     }
 };
 
@@ -240,8 +263,16 @@ struct DevCtx {
 // at process exit the HIP runtime (or a profiler's tool library) may already be torn down, and a
 // hipFree / hipModuleUnload from __cxa_finalize then faults (profiles/r02az: SIGSEGV in
 // __cxa_finalize after rocprofv3's finalisation).  rq_shutdown() releases everything explicitly.
+// Each library call holds its context through a CtxRef (a shared_ptr): rq_shutdown only takes the
+// contexts out of the map, and a context is destroyed when the last call that fetched it returns, so
+// a call racing rq_shutdown never touches freed memory.
 std::mutex g_ctx_mu;
-std::map<int, std::unique_ptr<DevCtx>>& g_ctx = *new std::map<int, std::unique_ptr<DevCtx>>();
+std::map<int, std::shared_ptr<DevCtx>>& g_ctx = *new std::map<int, std::shared_ptr<DevCtx>>();
+struct CtxRef {
+    std::shared_ptr<DevCtx> p;
+    DevCtx* operator->() const { return p.get(); }
+    operator DevCtx*() const { return p.get(); }
+};
 
 int current_device(int* dev) {
     if (g_device < 0) {
@@ -255,7 +286,7 @@ int current_device(int* dev) {
     return RQ_OK;
 }
 
-int get_ctx(DevCtx** out) {
+int get_ctx(CtxRef* out) {
     int dev;
     int rc = current_device(&dev);
     if (rc) return rc;
@@ -263,13 +294,13 @@ int get_ctx(DevCtx** out) {
     std::lock_guard<std::mutex> lk(g_ctx_mu);
     auto& c = g_ctx[dev];
     if (!c) {
-        c.reset(new DevCtx());
+        c = std::make_shared<DevCtx>();
         c->device = dev;
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
             c->n_cu = (uint32_t)cus;
     }
-    *out = c.get();
+    out->p = c;
     return RQ_OK;
 }
 
@@ -628,7 +659,7 @@ int launch_col(DevCtx* ctx, ColKernel* k, uint32_t T, uint32_t n_blocks, const v
         }
         HIP_TRY(hipModuleLaunchKernel(k->fn, wgs, 1, 1, 64 * Wg, 1, 1, 0, (hipStream_t)stream, nullptr, cfg));
     }
-    return RQ_OK;
+    return w->mark(stream);
 }
 
 // Encode `n_blocks` device-resident blocks: outputs esi[0..n_esi) of every block.
@@ -844,9 +875,20 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     static const int desc_mode = [] { const char* e = knob("RQHIP_DEC_ZC"); return e ? std::atoi(e) : 2; }();
     const bool zero_copy = desc_mode != 0;  // statuses in dstatus, `up` after the last kernel
     const bool side = desc_mode == 2;
-    if (side && !w->cs) {
-        HIP_TRY(hipStreamCreateWithFlags(&w->cs, hipStreamNonBlocking));
-        for (int i = 0; i < 2; ++i) HIP_TRY(hipEventCreateWithFlags(&w->cpy[i], hipEventDisableTiming));
+    if (side && !w->cs) {  // events first: a half-built pair is destroyed, never published
+        hipEvent_t ev[2] = {nullptr, nullptr};
+        hipStream_t cs = nullptr;
+        bool ok = hipEventCreateWithFlags(&ev[0], hipEventDisableTiming) == hipSuccess &&
+                  hipEventCreateWithFlags(&ev[1], hipEventDisableTiming) == hipSuccess &&
+                  hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) == hipSuccess;
+        if (!ok) {
+            for (hipEvent_t e : ev)
+                if (e) (void)hipEventDestroy(e);
+            return fail(RQ_ERR_DEVICE, "side-stream setup failed");
+        }
+        w->cpy[0] = ev[0];
+        w->cpy[1] = ev[1];
+        w->cs = cs;
     }
     // the set's staging and (zero copy / side upload) its device copy were last read by call n - 2's
     // kernels, which precede `up[set]`
@@ -858,9 +900,24 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     std::memcpy(w->h_idx[set].p, idx.data(), idx.size() * 4);
     const uint32_t* di;
     int32_t* dst_status;
+    // An error return after the side copy is queued must still leave `up[set]` behind that copy (and
+    // whatever this call queued after it): the call that reuses the set two calls later rewrites its
+    // pinned staging once `up[set]` completes.
+    struct UpGuard {
+        Workspace* w = nullptr;
+        hipStream_t s = nullptr;
+        uint32_t set = 0;
+        bool armed = false;
+        ~UpGuard() {
+            if (!armed) return;
+            (void)hipStreamWaitEvent(s, w->cpy[set], 0);
+            (void)hipEventRecord(w->up[set], s);
+        }
+    } up_guard{w, (hipStream_t)stream, set, false};
     if (side) {
         if ((rc = w->dstatus.ensure((size_t)n_blocks * 4))) return rc;
         HIP_TRY(hipMemcpyAsync(w->idx[set].p, w->h_idx[set].p, idx.size() * 4, hipMemcpyHostToDevice, w->cs));
+        up_guard.armed = true;
         HIP_TRY(hipEventRecord(w->cpy[set], w->cs));
         di = w->idx[set].as<uint32_t>();
         dst_status = w->dstatus.as<int32_t>();  // the host-decided statuses: copied by the first solver
@@ -938,13 +995,17 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     }
     // the last kernel that reads the staging is queued: `up` (no fence) before the downloads, so the
     // stream's last command stays a copy whose completion makes its bytes visible to the host
-    if (zero_copy) HIP_TRY(hipEventRecord(w->up[set], (hipStream_t)stream));
+    if (zero_copy) {
+        HIP_TRY(hipEventRecord(w->up[set], (hipStream_t)stream));
+        up_guard.armed = false;
+    }
     if (po) HIP_TRY(hipMemcpyAsync(w->h_pack.p, w->pk.p, pack_bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
     if (async) {  // statuses land in the caller's pinned array when the stream gets here
         HIP_TRY(hipMemcpyAsync(status, dst_status, n_blocks * 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
-        return RQ_OK;
+        return w->mark(stream);
     }
     HIP_TRY(hipMemcpyAsync(w->h_status.p, dst_status, n_blocks * 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
+    if ((rc = w->mark(stream))) return rc;
     if (fin == Fin::Deferred) return RQ_OK;  // decode_collect after the caller's stream sync
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
     decode_collect(w, blk_map, eoff, T, status, po);
@@ -1107,7 +1168,7 @@ int copy_2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t wid
 // only after its previous chunk finished, and `kdone` keeps the stages' kernels in chunk order.
 int encode_host_shard(int dev, const rq_encode_desc& d, const Params& p, uint32_t b0, uint32_t b1) {
     g_device = dev;
-    DevCtx* ctx;
+    CtxRef ctx;
     int rc = get_ctx(&ctx);
     if (rc) return rc;
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -1187,7 +1248,7 @@ int upload_runs(uint8_t* dst, const P* src, const uint64_t* bytes, uint32_t n, h
 int decode_host_shard(int dev, const HostDecode& d, const Params& p, uint32_t b0, uint32_t b1,
                       const std::vector<uint64_t>& eoff, const std::vector<uint64_t>& roff) {
     g_device = dev;
-    DevCtx* ctx;
+    CtxRef ctx;
     int rc = get_ctx(&ctx);
     if (rc) return rc;
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -1436,7 +1497,7 @@ int rq_debug_tuple(uint32_t K, uint32_t X, uint32_t out[6]) {
 }
 
 int rq_stream_release(void* stream) {
-    DevCtx* ctx;
+    CtxRef ctx;
     int rc = get_ctx(&ctx);
     if (rc) return rc;
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -1446,7 +1507,7 @@ int rq_stream_release(void* stream) {
 }
 
 int rq_launch_timing(int enable) {
-    DevCtx* ctx;
+    CtxRef ctx;
     int rc = get_ctx(&ctx);
     if (rc) return rc;
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -1456,7 +1517,7 @@ int rq_launch_timing(int enable) {
 
 int rq_launch_time(double* ms_total, uint32_t* n_launches, int reset) {
     if (!ms_total || !n_launches) return fail(RQ_ERR_BAD_ARG, "null output");
-    DevCtx* ctx;
+    CtxRef ctx;
     int rc = get_ctx(&ctx);
     if (rc) return rc;
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -1474,18 +1535,15 @@ int rq_launch_time(double* ms_total, uint32_t* n_launches, int reset) {
 }
 
 int rq_shutdown(void) {
-    std::lock_guard<std::mutex> lk(g_ctx_mu);
-    for (auto& kv : g_ctx) {
-        std::unique_ptr<DevCtx> c;
-        {
-            // wait for a call in flight on the context, then take it out of the map; the lock is
-            // released before the context (and its mutex) is destroyed, never after
-            std::lock_guard<std::mutex> l2(kv.second->mu);
-            c = std::move(kv.second);
-        }
-        c.reset();  // ~DevCtx: device sync, then every buffer, module, stream and event of the device
+    std::vector<std::shared_ptr<DevCtx>> gone;
+    {
+        std::lock_guard<std::mutex> lk(g_ctx_mu);
+        for (auto& kv : g_ctx) gone.push_back(std::move(kv.second));
+        g_ctx.clear();
     }
-    g_ctx.clear();
+    // ~DevCtx (device sync, then every buffer, module, stream and event of the device) runs here, or
+    // in a concurrent call that still holds the context, when that call returns
+    gone.clear();
     return RQ_OK;
 }
 
@@ -1621,7 +1679,7 @@ int rq_encode_batch(const rq_encode_desc* d) {
     Params p;
     int rc = params_for_K(d->K, &p);
     if (rc) return fail(rc, "k is too big");
-    DevCtx* ctx;
+    CtxRef ctx;
     if ((rc = get_ctx(&ctx))) return rc;
     std::lock_guard<std::mutex> lk(ctx->mu);
     return encode_locked(ctx, p, d->T, d->n_blocks, d->src, d->src_stride, d->esi, d->n_esi, d->out, d->out_stride,
@@ -1635,7 +1693,7 @@ int rq_decode_batch(const rq_decode_desc* d) {
     Params p;
     int rc = params_for_K(d->K, &p);
     if (rc) return fail(rc, "k is too big");
-    DevCtx* ctx;
+    CtxRef ctx;
     if ((rc = get_ctx(&ctx))) return rc;
     std::lock_guard<std::mutex> lk(ctx->mu);
     return decode_locked(ctx, p, d->T, d->n_blocks, d->data, d->data_stride, d->n_erased, d->erased, d->n_repair,
@@ -1654,7 +1712,7 @@ int rq_decode_batch_async(const rq_decode_desc* d) {
     Params p;
     int rc = params_for_K(d->K, &p);
     if (rc) return fail(rc, "k is too big");
-    DevCtx* ctx;
+    CtxRef ctx;
     if ((rc = get_ctx(&ctx))) return rc;
     std::lock_guard<std::mutex> lk(ctx->mu);
     return decode_locked(ctx, p, d->T, d->n_blocks, d->data, d->data_stride, d->n_erased, d->erased, d->n_repair,
@@ -1784,7 +1842,7 @@ rq_enc* rq_encoder_create(const uint8_t* data, size_t len, uint32_t T, int* err)
         const size_t n = off >= len ? 0 : std::min<size_t>(T, len - off);
         if (n) std::memcpy(&e->src[(size_t)i * e->Tp], data + off, n);
     }
-    DevCtx* ctx;
+    CtxRef ctx;
     if ((rc = get_ctx(&ctx))) { *err = rc; return nullptr; }
     std::lock_guard<std::mutex> lk(ctx->mu);
     hipStream_t st;
@@ -1838,7 +1896,7 @@ int rq_encoder_symbols(rq_enc* e, uint32_t first, uint32_t count, uint8_t* out) 
         else rep.push_back((uint32_t)esi);
     }
     if (rep.empty()) return RQ_OK;
-    DevCtx* ctx;
+    CtxRef ctx;
     int rc = get_ctx(&ctx);
     if (rc) return rc;
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -1918,7 +1976,7 @@ int rq_decoder_decode(rq_dec* d, uint8_t* out, int* ok) {
         std::vector<uint32_t> erased, resi;
         for (uint32_t i = 0; i < K; ++i)
             if (!d->have[i]) erased.push_back(i);
-        DevCtx* ctx;
+        CtxRef ctx;
         int rc = get_ctx(&ctx);
         if (rc) return rc;
         std::lock_guard<std::mutex> lk(ctx->mu);

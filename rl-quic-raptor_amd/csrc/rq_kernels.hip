@@ -351,6 +351,7 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pm(SolveArgs a) {
     // LUT: per pivot value f (!= 0), log f | log(1 ^ 1/f) << 8 | (1 ^ 1/f != 0) << 16: one lookup per
     // step instead of three dependent ones (lg[f_p], ex[255 - lg f_p], lg[c_p])
     __shared__ uint32_t pinfo[LUT ? 256 : 1];
+    __shared__ uint8_t fcol[2][NROWS];  // column k of every row by step parity (see k_solve_pq)
     const uint32_t b = a.blk_map[blockIdx.x];
     const uint32_t tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
     if (a.status_init)  // the host-decided statuses (disjoint from the solver's blocks, ST_PENDING)
@@ -388,6 +389,8 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pm(SolveArgs a) {
             pinfo[x] = lx | (cp ? (uint32_t)lg[cp] << 8 | 1u << 16 : 0u);
         }
     __syncthreads();
+    for (uint32_t r = tid; r < NROWS; r += NT) fcol[0][r] = (uint8_t)(rows[r * SW] & 0xFFu);
+    __syncthreads();
     const uint32_t q1 = (e + nrow + 15) >> 4;  // quads holding live columns
     bool used[RPL];
 #pragma unroll
@@ -398,7 +401,7 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pm(SolveArgs a) {
         uint32_t p = 0xFFFFFFFFu;
 #pragma unroll
         for (int q = RPL - 1; q >= 0; --q) {
-            f[q] = (rows[(lane + 64 * q) * SW + (k >> 2)] >> ((k & 3) * 8)) & 0xFFu;
+            f[q] = fcol[k & 1][lane + 64 * q];
             const uint64_t bal = __ballot(f[q] != 0 && !used[q]);
             if (bal) p = 64 * q + (uint32_t)__ffsll((unsigned long long)bal) - 1;
         }
@@ -454,20 +457,27 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pm(SolveArgs a) {
         }
         // columns < k are zero in the pivot row (all are earlier pivot columns): start at quad k/16
         const uint4* prow = reinterpret_cast<const uint4*>(rows + p * SW);
+        const uint32_t kn = k + 1;
         for (uint32_t w = (k >> 4) + g; w < q1; w += NW) {
             const uint4 P = prow[w];
             const uint32_t px = __builtin_amdgcn_readfirstlane(P.x), py = __builtin_amdgcn_readfirstlane(P.y);
             const uint32_t pz = __builtin_amdgcn_readfirstlane(P.z), pw = __builtin_amdgcn_readfirstlane(P.w);
 #pragma unroll
             for (int q = 0; q < RPL; ++q) {
-                if (!act[q]) continue;
                 uint4* my4 = reinterpret_cast<uint4*>(rows + (lane + 64 * q) * SW);
                 uint4 r = my4[w];
-                r.x ^= perm_mul(A[q], B[q], px);
-                r.y ^= perm_mul(A[q], B[q], py);
-                r.z ^= perm_mul(A[q], B[q], pz);
-                r.w ^= perm_mul(A[q], B[q], pw);
-                my4[w] = r;
+                if (act[q]) {
+                    r.x ^= perm_mul(A[q], B[q], px);
+                    r.y ^= perm_mul(A[q], B[q], py);
+                    r.z ^= perm_mul(A[q], B[q], pz);
+                    r.w ^= perm_mul(A[q], B[q], pw);
+                    my4[w] = r;
+                }
+                if (kn < e && w == (kn >> 4)) {  // wave-uniform: this wave owns column k + 1
+                    const uint32_t d = (kn >> 2) & 3u;
+                    const uint32_t dw = d == 0 ? r.x : d == 1 ? r.y : d == 2 ? r.z : r.w;
+                    fcol[kn & 1][lane + 64 * q] = (uint8_t)(dw >> ((kn & 3u) * 8));
+                }
             }
         }
         __syncthreads();
@@ -503,6 +513,11 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
     __shared__ __attribute__((aligned(16))) uint4 tlA[510];
     __shared__ uint32_t tlB[510];
     __shared__ uint32_t pinfo[256];
+    // column k of every row, double-buffered by step parity: step k reads fcol[k & 1]; the wave that
+    // updates the quad holding column k + 1 writes fcol[(k + 1) & 1] from its registers.  Reading
+    // column k from `rows` instead would race with wave 0, which rewrites quad k / 16 in the same step
+    // (a late wave then sees column k already eliminated: a wrong X with status 1).
+    __shared__ uint8_t fcol[2][NROWS];
     const uint32_t b = a.blk_map[blockIdx.x];
     const uint32_t tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
     if (a.status_init)
@@ -547,6 +562,8 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
         pinfo[x] = v;
     }
     __syncthreads();
+    for (uint32_t r = tid; r < NROWS; r += NT) fcol[0][r] = (uint8_t)(rows[r * SW] & 0xFFu);
+    __syncthreads();
     const uint32_t q1 = (e + nrow + 15) >> 4;  // quads holding live columns
     bool used[RPL];
 #pragma unroll
@@ -566,7 +583,7 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
                 R[q][j] = reinterpret_cast<const uint4*>(rows + (lane + 64 * q) * SW)[min(w0 + NW * j, 8u * RPL)];
         uint32_t f[RPL], pif[RPL];
 #pragma unroll
-        for (int q = 0; q < RPL; ++q) f[q] = (rows[(lane + 64 * q) * SW + (k >> 2)] >> ((k & 3) * 8)) & 0xFFu;
+        for (int q = 0; q < RPL; ++q) f[q] = fcol[k & 1][lane + 64 * q];
         // (2) pinfo of every row's coefficient, beside the ballot
 #pragma unroll
         for (int q = 0; q < RPL; ++q) pif[q] = pinfo[f[q]];
@@ -606,6 +623,7 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
             B[q] = tlB[l];
         }
         // columns < k are zero in the pivot row (all are earlier pivot columns): quads from k/16
+        const uint32_t kn = k + 1;  // the column the next step reads
 #pragma unroll
         for (int j = 0; j < (int)QW; ++j) {
             const uint32_t w = w0 + NW * j;
@@ -620,6 +638,12 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
                 r.z ^= perm_mul(A[q], B[q], pz);
                 r.w ^= perm_mul(A[q], B[q], pw);
                 if (act[q]) reinterpret_cast<uint4*>(rows + (lane + 64 * q) * SW)[w] = r;
+                if (kn < ksteps && w == (kn >> 4)) {  // wave-uniform: this wave owns column k + 1
+                    const uint4 v = act[q] ? r : R[q][j];
+                    const uint32_t d = (kn >> 2) & 3u;
+                    const uint32_t dw = d == 0 ? v.x : d == 1 ? v.y : d == 2 ? v.z : v.w;
+                    fcol[kn & 1][lane + 64 * q] = (uint8_t)(dw >> ((kn & 3u) * 8));
+                }
             }
         }
         __syncthreads();

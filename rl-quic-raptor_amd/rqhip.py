@@ -77,21 +77,45 @@ class BlockIO(ctypes.Structure):
 
 
 def build():
-    subprocess.run(["make", "-s", "-C", str(_HERE), "-j8"], check=True)
+    # RQHIP_BUILD_CMD replaces the make invocation (a test hook: tests/test_multi_rank.py counts builds)
+    cmd = os.environ.get("RQHIP_BUILD_CMD")
+    if cmd:
+        subprocess.run(cmd, shell=True, check=True)
+    else:
+        subprocess.run(["make", "-s", "-C", str(_HERE), "-j8"], check=True)
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        if not LIB_PATH.exists():
-            # build on demand (hipcc cross-compiles gfx950 without a device); a failed build
-            # raises -- there is no CPU fallback behind this library
+def ensure_built():
+    """Build librqhip.so if it is missing, under an exclusive file lock, without loading it (no GPU call).
+    Returns True if this process ran the build.  Several processes that start at once (bench.py's ranks)
+    then run one build between them, and none of them can dlopen a half-written library: the others wait
+    on the lock and find the finished file."""
+    if LIB_PATH.exists():
+        return False
+    import fcntl
+    LIB_PATH.parent.mkdir(parents=True, exist_ok=True)
+    with open(str(LIB_PATH) + ".lock", "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        try:
+            if LIB_PATH.exists():
+                return False
+            # hipcc cross-compiles gfx950 without a device; a failed build raises -- there is no CPU
+            # fallback behind this library
             try:
                 build()
             except (OSError, subprocess.CalledProcessError) as ex:
                 raise RaptorQError(RQ_ERR_DEVICE, "librqhip.so could not be built: %s" % ex) from ex
             if not LIB_PATH.exists():
                 raise RaptorQError(RQ_ERR_DEVICE, "librqhip.so not built (run `make -C rl-quic-raptor_amd`)")
+            return True
+        finally:
+            fcntl.flock(lk, fcntl.LOCK_UN)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        ensure_built()
         # One HIP runtime per process: PyTorch-ROCm bundles its own libamdhip64.so.7 (same soname as
         # /opt/rocm's).  Loaded first, torch's copy also serves librqhip.so's NEEDED entry; loaded after
         # librqhip.so, a second runtime initialises the device beside the first and the library's

@@ -37,3 +37,13 @@ def sum_over_ranks(x, dist=None, device=None):
     t = torch.tensor([int(x)], dtype=torch.int64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return int(t.item())
+
+
+def all_over_ranks(x, dist=None, device=None):
+    """Every rank's value of a float, in rank order (per-rank timings in the bench line)."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return [float(x)]
+    import torch
+    out = [torch.zeros(1, dtype=torch.float64, device=device) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, torch.tensor([float(x)], dtype=torch.float64, device=device))
+    return [float(t.item()) for t in out]

@@ -16,3 +16,15 @@ def oracle_repairs(args):
     from oracle import oracle as O
     enc = O.OracleEncoder(data, T)
     return np.stack([enc.gen_symbol(e) for e in esis])
+
+
+def oracle_decode(args):
+    """The oracle decoder on one block: (K, T, {esi: row bytes} of the received symbols) -> (ok, payload)."""
+    K, T, recv = args
+    if str(ROOT) not in sys.path:
+        sys.path.insert(0, str(ROOT))
+    from oracle import oracle as O
+    dec = O.OracleDecoder(K * T, T)
+    for esi, row in recv.items():
+        dec.add_symbol(esi, row)
+    return dec.decode()

@@ -124,3 +124,54 @@ def test_config4_shard_on_one_gpu(gpu, rq, rank):
     assert np.array_equal(out[[0, count - 1]].cpu().numpy(), ref)
     data, st, *_ = _erase_decode(rq, gpu, src, out, K, T, N, n_erase, 40 + rank)
     assert (st == 1).all() and torch.equal(data, src)
+
+
+def _oracle_map(fn, jobs):
+    import multiprocessing as mp
+    sys.path.insert(0, str(ROOT / "tests"))
+    import _oracle_pool
+    with mp.get_context("spawn").Pool(min(8, THREADS)) as pool:
+        return pool.map(getattr(_oracle_pool, fn), jobs)
+
+
+def test_config2_encode_sample_matches_oracle(gpu, rq):
+    """Config 2's full launch (1 024 blocks K=256 T=1200, 26 repairs) against the independent C
+    restatement: 32 blocks spread over the batch (every 33rd, and the last), every repair byte."""
+    K, T, R, nb = 256, 1200, 26, 1024
+    esis = list(range(K, K + R))
+    src = _src(gpu, nb, K, T, 22)
+    out = _encode(rq, gpu, src, K, T, esis).view(nb, R, T).cpu().numpy()
+    src_h = src.cpu().numpy()
+    sample = sorted(set(list(range(0, nb, 33)) + [nb - 1]))
+    assert len(sample) == 32
+    refs = _oracle_map("oracle_repairs", [(src_h[b].tobytes(), T, esis) for b in sample])
+    for b, ref in zip(sample, refs):
+        assert np.array_equal(out[b], ref), "block %d" % b
+
+
+def test_k2048_t1200_matches_oracle(gpu, rq):
+    """Config 5's largest shape (K=2048, T=1200, N = K + K/10 + 8, 5 % of N erased) through the
+    device-resident path, against the oracle: the repairs of 8 of 32 blocks byte for byte, and the
+    decodes of 2 blocks (ok flag and payload) with the oracle decoder on the same received symbols;
+    every block decodes back to its source."""
+    K, T, nb = 2048, 1200, 32
+    N = K + K // 10 + 8
+    n_erase = round(0.05 * N)
+    esis = list(range(K, N))
+    src = _src(gpu, nb, K, T, 2048)
+    out = _encode(rq, gpu, src, K, T, esis)
+    src_h = src.cpu().numpy()
+    out_h = out.view(nb, N - K, T).cpu().numpy()
+    sample = [0, 5, 9, 14, 18, 23, 27, 31]
+    refs = _oracle_map("oracle_repairs", [(src_h[b].tobytes(), T, esis) for b in sample])
+    for b, ref in zip(sample, refs):
+        assert np.array_equal(out_h[b], ref), "block %d" % b
+    data, st, er, rl, _ = _erase_decode(rq, gpu, src, out, K, T, N, n_erase, 77)
+    assert (st == 1).all() and torch.equal(data, src)
+    jobs = []
+    for b in (3, 30):
+        recv = {i: src_h[b, i * T:(i + 1) * T].tobytes() for i in range(K) if i not in set(er[b])}
+        recv.update({e: out_h[b, e - K].tobytes() for e in rl[b]})
+        jobs.append((K, T, recv))
+    for b, (ok, payload) in zip((3, 30), _oracle_map("oracle_decode", jobs)):
+        assert ok and payload == src_h[b].tobytes(), "block %d" % b

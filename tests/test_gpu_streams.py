@@ -122,3 +122,39 @@ def test_launch_timing(gpu, rq):
     assert n == 3 and 0 < ms <= a.elapsed_time(b) * 1.01, (ms, n, a.elapsed_time(b))
     assert torch.equal(rep, ref)
     assert rq.launch_time(reset=True) == (0.0, 0)
+
+
+def test_shutdown_with_concurrent_caller(gpu, rq):
+    """rq_shutdown while another thread is inside library calls: each call holds its context (a
+    shared_ptr, rq_engine.cpp CtxRef), so the context is destroyed only when the last call using it
+    returns, and calls after the shutdown build a fresh one.  Every encode still returns the reference
+    bytes; nothing faults."""
+    import threading
+    src, _, _ = _case(gpu, rq, 31)
+    esis = list(range(K, N))
+    ref = torch.empty((NB, (N - K) * T), dtype=torch.uint8, device=gpu)
+    rq.encode_batch(src, K, T, esis, ref)
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    outs = [torch.empty_like(ref) for _ in range(24)]
+    errors = []
+
+    def worker():
+        try:
+            for o in outs:
+                rq.encode_batch(src, K, T, esis, o, stream=s)
+                s.synchronize()
+        except Exception as ex:  # noqa: BLE001 -- reported by the main thread
+            errors.append(repr(ex))
+
+    th = threading.Thread(target=worker)
+    th.start()
+    import time
+    for _ in range(3):
+        time.sleep(0.05)
+        assert rq.lib().rq_shutdown() == 0
+    th.join(timeout=120)
+    assert not th.is_alive() and not errors, errors
+    torch.cuda.synchronize()
+    for i, o in enumerate(outs):
+        assert torch.equal(o, ref), i

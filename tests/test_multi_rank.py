@@ -124,3 +124,43 @@ def test_bench_rank_env_and_external_launcher():
     # under torch.distributed.run the environment already names the world: no spawning
     plan = _bench("--gpus", "2", "--plan-only", env={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
     assert plan["launcher"] == "external"
+
+
+def test_bench_spawn_builds_once(tmp_path):
+    """`--gpus 4 --plan-only` with the library absent: the parent builds it once (under the lock of
+    rqhip.ensure_built), the four spawned ranks only find it -- no rank races a build or loads a
+    half-written file.  RQHIP_BUILD_CMD stands in for make and counts the builds."""
+    lib = tmp_path / "build" / "librqhip.so"
+    count = tmp_path / "builds.txt"
+    cmd = "echo build >> %s && sleep 1 && mkdir -p %s && echo fake > %s.tmp && mv %s.tmp %s" % (
+        count, lib.parent, lib, lib, lib)
+    plan = _bench("--gpus", "4", "--plan-only", env={"RQHIP_LIB": str(lib), "RQHIP_BUILD_CMD": cmd})
+    assert plan["world"] == 4 and plan["launcher"] == "spawn" and plan["ranks_rc"] == 0
+    assert plan["built_by_parent"] is True and plan["library"] == str(lib)
+    assert count.read_text().split() == ["build"]
+    # a second rehearsal finds the library and builds nothing
+    plan = _bench("--gpus", "2", "--plan-only", env={"RQHIP_LIB": str(lib), "RQHIP_BUILD_CMD": cmd})
+    assert plan["built_by_parent"] is False and count.read_text().split() == ["build"]
+
+
+def test_ensure_built_concurrent(tmp_path):
+    """Eight processes call rqhip.ensure_built at once on an absent library: exactly one builds."""
+    import subprocess
+    lib = tmp_path / "librqhip.so"
+    count = tmp_path / "builds.txt"
+    cmd = "echo build >> %s && sleep 1 && echo fake > %s.tmp && mv %s.tmp %s" % (count, lib, lib, lib)
+    env = dict(os.environ, RQHIP_LIB=str(lib), RQHIP_BUILD_CMD=cmd)
+    code = "import sys; sys.path.insert(0, %r); import rqhip; print(int(rqhip.ensure_built()))" % str(ROOT / "rl-quic-raptor_amd")
+    procs = [subprocess.Popen([sys.executable, "-c", code], env=env, stdout=subprocess.PIPE, text=True) for _ in range(8)]
+    outs = [p.communicate(timeout=120)[0].strip() for p in procs]
+    assert all(p.returncode == 0 for p in procs)
+    assert sorted(outs) == ["0"] * 7 + ["1"]
+    assert count.read_text().split() == ["build"]
+
+
+def test_host_cores_stated():
+    sys.path.insert(0, str(ROOT))
+    import bench
+    n, src = bench.host_cores()
+    assert 1 <= n <= 16 and n <= len(os.sched_getaffinity(0))
+    assert "affinity" in src
