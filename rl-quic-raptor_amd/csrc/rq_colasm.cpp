@@ -6,6 +6,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <queue>
 #include <set>
 
@@ -404,6 +405,47 @@ struct Allocator {
                     }
                     break;
                 }
+                case IR_SEND: {  // pair programs, wave A: value -> ring slot (ds_write_b32; VGPR or AGPR data)
+                    const uint32_t v = n.a;
+                    int r = reg[v];
+                    if (r < 0) {
+                        if (!has_copy(v)) { fail("colasm: send of a lost value"); break; }
+                        r = take_vgpr();
+                        reload_into(v, r);
+                        mp->st.sync_reload++;
+                    }
+                    if (inflight[r]) wait_seq(inflight[r]);
+                    if (linflight[r]) wait_lseq(linflight[r]);
+                    issue_lgkm();
+                    emit(MI_RST, -1, r, -1, -1, n.imm);
+                    mp->st.rst++;
+                    uptr[v]++;
+                    if (nu(v) == INF) kill(v);
+                    break;
+                }
+                case IR_RECV: {  // pair programs, wave B: ring slot -> register (ds_read_b32)
+                    if (uses[i].empty()) break;
+                    int r = -1;
+                    if (uses[i][0] > i + o.lds_horizon) r = take_any(uses[i][0]);  // used much later: any register
+                    if (r < 0) r = take_vgpr();
+                    const uint64_t q = issue_lgkm();
+                    emit(MI_RLD, r, -1, -1, -1, n.imm);
+                    mp->st.rld++;
+                    linflight[r] = q;
+                    pend_lds.push_back({q, r});
+                    owner[r] = (int32_t)i; reg[i] = (int16_t)r;
+                    break;
+                }
+                case IR_BAR: {  // pair programs: the transfer's LDS operations complete, then the barrier
+                    if (lseq > lretired) {
+                        emit(MI_WAITL, -1, -1, -1, -1, 0);
+                        mp->st.waitl++;
+                        retire_l(lseq);
+                    }
+                    emit(MI_BAR, -1, -1, -1, -1, n.imm);
+                    mp->st.bar++;
+                    break;
+                }
                 case IR_STORE: {
                     const uint32_t v = n.a;
                     int r = reg[v];
@@ -629,15 +671,24 @@ std::vector<uint32_t> colprog_src_rows(const MProg& mp) {
     return rows;
 }
 
-std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
+// Scratch slot s sits at soffset 4096 * (s / 16) + offset (s % 16) * 256: soffset 0 or one of
+// SCR_BASES SGPRs s56.. loaded once by the prologue; slots beyond them (very large K) form their
+// soffset with an s_mov.
+static uint32_t scratch_bases(const MProg& mp) {
+    return std::min<uint32_t>(SCR_BASES, mp.n_slots > 16 ? (mp.n_slots - 1) / 16 : 0);
+}
+
+// The per-item instruction stream of an allocated program (the body of the persistent loop): the
+// source row-offset window (A / single-wave programs), scratch soffsets, and every MInst.  Shared by
+// the single-wave kernel (emit_colprog_asm) and both waves of a pair kernel (emit_pair_asm).  W: waves
+// per workgroup of the single-wave layout (MI_DMA's per-wave LDS base in s41 when W > 1).
+static void emit_colprog_body(const MProg& mp, uint32_t W, std::string& s) {
     static const Policy pol;
     static const uint32_t diag = diag_mask();
+    static const uint32_t wgbar = [] { const char* e = knob("RQHIP_WGBAR"); return e ? (uint32_t)std::atoi(e) : 0u; }();
     const Reserved rv(mp.n_vgpr);
     const int V_T1 = rv.t1, V_T2 = rv.t2, V_SCROFF = rv.scroff, V_OUTOFF = rv.outoff, V_SRCOFF = rv.srcoff;
-    const uint32_t acc_off = (mp.n_vgpr + N_RESERVED + 3) & ~3u;        // first AGPR in the unified file
-    const uint32_t n_regs = (acc_off + std::max<uint32_t>(mp.n_agpr, 1) + 7) & ~7u;
-    std::string s;
-    s.reserve(mp.ins.size() * 48 + 8192);
+    const uint32_t n_bases = scratch_bases(mp);
     char buf[256];
     auto R = [&](int r) {
         static thread_local char b[2][16];
@@ -647,173 +698,12 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
         return b[k];
     };
     auto line = [&](const char* t) { s += '\t'; s += t; s += '\n'; };
-    s += "\t.amdgcn_target \"amdgcn-amd-amdhsa--gfx950\"\n\t.amdhsa_code_object_version 6\n\t.text\n";
-    s += "\t.globl " + kname + "\n\t.p2align 8\n\t.type " + kname + ",@function\n" + kname + ":\n";
-    // Persistent loop: the grid holds as many waves as can be resident (the host sets n_wg = s49);
-    // wave w processes items w, w + n_wg, ... < n_items (s48), so its scratch lines are reused by
-    // its own next item instead of a fresh wave's, and the scratch footprint stays at the
-    // resident set.  One item = 64 dword columns (the lane -> (block, column) map below).
-    const char* pro_once[] = {
-        "s_load_dwordx8 s[4:11], s[0:1], 0x0",
-        "s_load_dwordx8 s[12:19], s[0:1], 0x20",
-        "s_load_dwordx4 s[48:51], s[0:1], 0x40",
-        "s_waitcnt lgkmcnt(0)",
-        "v_lshlrev_b32_e32 V_SCROFF, 2, v0",
-        "v_add_u32_e32 V_LDS2, 0x10000, V_SCROFF",
-        "s_mov_b32 s24, s4",
-        "s_and_b32 s25, s5, 0xffff",
-        "s_mov_b32 s26, -1",
-        "s_mov_b32 s27, 0x20000",
-        "s_mov_b32 s28, s6",
-        "s_and_b32 s29, s7, 0xffff",
-        "s_mov_b32 s30, -1",
-        "s_mov_b32 s31, 0x20000",
-        "s_mul_i32 s32, s2, s16",
-        "s_mul_hi_u32 s33, s2, s16",
-        "s_add_u32 s32, s8, s32",
-        "s_addc_u32 s33, s9, s33",
-        "s_and_b32 s33, s33, 0xffff",
-        "s_mov_b32 s34, -1",
-        "s_mov_b32 s35, 0x20000",
-        "s_mov_b32 s36, 0x090b080a",
-        "s_mov_b32 s37, 0xfefefefe",
-        "s_mov_b32 s38, 0x1d1d1d1d",
-        "s_mov_b32 s52, s2",
+    // LDS slot sl (256 B per lane row) of this program: offset (sl & 255) * 256 from V_SCROFF (the lane's
+    // 4 B) or from V_LDS2 = V_SCROFF + 64 KiB (the ds offset field is 16 bits)
+    auto lds_at = [&](uint32_t sl, int* vbase) {
+        *vbase = sl < 256 ? V_SCROFF : rv.lds2;
+        return (sl & 255u) * 256u;
     };
-    const char* pro_iter[] = {
-        // (the program is longer than a 16-bit branch reaches: exit in place, loop back by s_setpc)
-        "s_cmp_lt_u32 s52, s48",
-        "s_cbranch_scc1 .Lbody",
-        "s_endpgm",
-        ".Lbody:",
-        "s_mov_b64 exec, -1",
-        // XCD-aware item order: workgroups are dealt to the 8 XCDs round-robin, so logical item
-        // L = (w % 8) * q + w / 8 (for w < 8q; s17 = q, s18 = 8q, both 0 = identity) keeps the
-        // items of one block, which share the 128-B lines at their 256-B segment edges, on one L2.
-        "s_and_b32 s39, s52, 7",
-        "s_mul_i32 s39, s39, s17",
-        "s_lshr_b32 s40, s52, 3",
-        "s_add_u32 s39, s39, s40",
-        "s_cmp_lt_u32 s52, s18",
-        "s_cselect_b32 s39, s39, s52",
-        "s_lshl_b32 s20, s39, 6",
-        "v_lshrrev_b32_e32 v0, 2, V_SCROFF",
-        "v_add_u32_e32 v1, s20, v0",
-        "v_cmp_gt_u32_e64 s[22:23], s13, v1",
-        "s_and_b64 exec, exec, s[22:23]",
-        "v_mul_hi_u32 v2, v1, s14",
-        "v_lshrrev_b32_e32 v2, s15, v2",
-        "s_lshr_b32 s21, s12, 2",
-        "v_mul_lo_u32 v3, v2, s21",
-        "v_sub_u32_e32 v3, v1, v3",
-        "v_lshlrev_b32_e32 v3, 2, v3",
-        "v_mul_lo_u32 v4, v2, s10",
-        "v_add_u32_e32 V_SRCOFF, v4, v3",
-        "v_mul_lo_u32 v4, v2, s11",
-        "v_add_u32_e32 V_OUTOFF, v4, v3",
-    };
-    auto put = [&](const char* p) {
-        std::string l(p);
-        const std::pair<const char*, int> names[] = {
-            {"V_SRCOFF", V_SRCOFF}, {"V_OUTOFF", V_OUTOFF}, {"V_SCROFF", V_SCROFF}, {"V_LDS2", rv.lds2}};
-        for (const auto& nm : names)
-            for (size_t at = l.find(nm.first); at != std::string::npos; at = l.find(nm.first))
-                l.replace(at, std::strlen(nm.first), "v" + std::to_string(nm.second));
-        line(l.c_str());
-    };
-    const uint32_t W = std::max<uint32_t>(1, mp.wg_waves);
-    static const uint32_t wgbar = [] { const char* e = knob("RQHIP_WGBAR"); return e ? (uint32_t)std::atoi(e) : 0u; }();
-    const uint32_t LB = mp.n_lds_slots * 256u;  // LDS bytes per wave
-    if (W == 1) {
-        for (const char* p : pro_once) put(p);
-    } else {
-        // W waves per workgroup (one per SIMD of a CU) take W consecutive items, i.e. the W x 256-B
-        // pieces of the same source rows (1 KiB at W = 4), which then reach the memory system close
-        // together.  Wave w of the workgroup: LDS slots at w * LB (folded into V_SCROFF, the lane's
-        // LDS / scratch voffset), scratch of global wave (wg * W + w), its base moved back by w * LB
-        // because V_SCROFF carries that LDS offset too.
-        for (const char* p : pro_once) {
-            const std::string l(p);
-            if (l.rfind("v_lshlrev_b32_e32 V_SCROFF", 0) == 0 || l.rfind("v_add_u32_e32 V_LDS2", 0) == 0 ||
-                l.rfind("s_mul_i32 s32", 0) == 0 || l.rfind("s_mul_hi_u32 s33", 0) == 0)
-                continue;
-            if (l.rfind("s_add_u32 s32, s8, s32", 0) == 0) {
-                put("v_lshrrev_b32_e32 v1, 6, v0");
-                line("s_nop 4");  // VALU write -> v_readfirstlane of it (a missing wait state read v1 stale)
-                line("v_readfirstlane_b32 s53, v1");
-                put("v_and_b32_e32 v0, 63, v0");
-                put("v_lshlrev_b32_e32 V_SCROFF, 2, v0");
-                std::snprintf(buf, sizeof buf, "s_mul_i32 s41, s53, %u", LB); line(buf);
-                put("v_add_u32_e32 V_SCROFF, s41, V_SCROFF");
-                put("v_add_u32_e32 V_LDS2, 0x10000, V_SCROFF");
-                std::snprintf(buf, sizeof buf, "s_mul_i32 s42, s2, %u", W); line(buf);
-                line("s_add_u32 s42, s42, s53");
-                line("s_mul_i32 s32, s42, s16");
-                line("s_mul_hi_u32 s33, s42, s16");
-                line("s_sub_u32 s32, s32, s41");
-                line("s_subb_u32 s33, s33, 0");
-            }
-            put(p);
-        }
-    }
-    // Scratch slot s sits at soffset 4096 * (s / 16) + offset (s % 16) * 256: soffset 0 or one of
-    // SCR_BASES SGPRs s56.. loaded once, so a spill or reload carries no SALU; slots beyond them
-    // (very large K) form their soffset with an s_mov.
-    const uint32_t n_bases = std::min<uint32_t>(SCR_BASES, mp.n_slots > 16 ? (mp.n_slots - 1) / 16 : 0);
-    for (uint32_t j = 0; j < n_bases; ++j) {
-        std::snprintf(buf, sizeof buf, "s_mov_b32 s%u, %u", 56 + j, 4096u * (j + 1));
-        line(buf);
-    }
-    // Code warm-up (W = 1): the program is ~180 KB of straight-line code that every wave starts at
-    // once, and when the previous kernel was not a column program its lines are in neither L2 nor the
-    // memory-side cache, so round 1's instruction fetches go to HBM one after another (12-15 us per
-    // launch after a decode's apply, ~30 us after a large copy: profiles/r03_dense/r03pos).  Each wave
-    // reads four 8 KiB strides of its own code (one dword per 128-B line; slice (wg / 8) % 32 within
-    // its XCD), so the XCD's waves pull the whole program into their L2 in parallel, then wait once.
-    // Bounds-checked buffer loads (num_records = code length): nothing beyond the code is read.
-    static const bool code_pf = [] { const char* e = knob("RQHIP_CODEPF"); return !e || e[0] != '0'; }();
-    if (W == 1 && code_pf && !(diag & 4) && mp.n_vgpr >= 12) {  // v5, v6, v8..v11 are program registers
-        line("s_getpc_b64 s[44:45]");
-        s += ".Lcpf:\n";
-        line(("s_sub_u32 s44, s44, .Lcpf-" + kname).c_str());
-        line("s_subb_u32 s45, s45, 0");
-        line("s_and_b32 s45, s45, 0xffff");
-        line(("s_mov_b32 s46, .Lfunc_end-" + kname).c_str());
-        line("s_mov_b32 s47, 0x20000");
-        line("s_lshr_b32 s43, s2, 3");
-        line("s_and_b32 s43, s43, 31");
-        line("s_lshl_b32 s43, s43, 13");
-        line("v_lshlrev_b32_e32 v5, 7, v0");
-        line("v_add_u32_e32 v5, s43, v5");
-        for (uint32_t k = 0; k < 4; ++k) {
-            std::snprintf(buf, sizeof buf, "v_add_u32_e32 v6, 0x%x, v5", k * 32u * 8192u); line(buf);
-            std::snprintf(buf, sizeof buf, "buffer_load_dword v%u, v6, s[44:47], 0 offen", 8 + k); line(buf);
-        }
-        line("s_waitcnt vmcnt(0)");
-    }
-    // experiments: RQHIP_STAGGER=n delays the odd workgroups' start by n x 127 x 64 cycles (do the
-    // first rounds' coinciding load bursts cost time?)
-    static const uint32_t stagger = [] { const char* e = knob("RQHIP_STAGGER"); return e ? (uint32_t)std::atoi(e) : 0u; }();
-    if (stagger) {
-        line("s_bitcmp1_b32 s2, 0");
-        line("s_cbranch_scc0 .Lnostagger");
-        for (uint32_t i = 0; i < stagger; ++i) line("s_sleep 127");
-        s += ".Lnostagger:\n";
-    }
-    s += ".Lloop:\n";
-    for (const char* p : pro_iter) {
-        const std::string l(p);
-        if (W > 1 && l.rfind("s_lshl_b32 s20, s39, 6", 0) == 0) {  // item = iteration * W + wave
-            std::snprintf(buf, sizeof buf, "s_mul_i32 s39, s39, %u", W); line(buf);
-            line("s_add_u32 s39, s39, s53");
-        }
-        if (W > 1 && l.rfind("v_lshrrev_b32_e32 v0, 2, V_SCROFF", 0) == 0) {  // lane id (V_SCROFF has w * LB)
-            line("v_mbcnt_lo_u32_b32 v0, -1, 0");
-            line("v_mbcnt_hi_u32_b32 v0, -1, v0");
-            continue;
-        }
-        put(p);
-    }
     // Source row j of the program (in issue order) is read at soffset row_off[j] = row * T, a
     // host-built table (colprog_src_rows) streamed into SGPRs 16 entries at a time by s_load_dwordx16,
     // one group ahead: a source load carries no SALU of its own, only one s_load and one
@@ -890,8 +780,9 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
                 if (diag & 4) break;
                 const int q = srot();
                 std::snprintf(buf, sizeof buf, "s_mul_i32 s%d, s12, %u", q, m.imm); line(buf);
-                if (W > 1) std::snprintf(buf, sizeof buf, "s_add_u32 m0, s41, %u", (uint32_t)m.d * 256u);
-                else std::snprintf(buf, sizeof buf, "s_mov_b32 m0, %u", (uint32_t)m.d * 256u);
+                const uint32_t dsl = (uint32_t)m.d + mp.lds_base;
+                if (W > 1) std::snprintf(buf, sizeof buf, "s_add_u32 m0, s41, %u", dsl * 256u);
+                else std::snprintf(buf, sizeof buf, "s_mov_b32 m0, %u", dsl * 256u);
                 line(buf);
                 line("s_nop 0");
                 std::snprintf(buf, sizeof buf, "buffer_load_dword v%d, s[24:27], s%d offen%s lds", V_SRCOFF, q, pol.src.c_str());
@@ -931,21 +822,210 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
             case MI_NOP:
                 std::snprintf(buf, sizeof buf, "s_nop %u", m.imm); line(buf); break;
             case MI_LDST:
-                if (diag & 2) break;
-                std::snprintf(buf, sizeof buf, "ds_write_b32 v%d, %s offset:%u", m.imm < 256 ? V_SCROFF : rv.lds2, R(m.a),
-                              (m.imm & 255u) * 256u);
+            case MI_RST: {  // spill slots sit after the ring (lds_base); ring slots from 0
+                if (diag & 2 && m.op == MI_LDST) break;
+                int vb;
+                const uint32_t off = lds_at(m.op == MI_RST ? m.imm : m.imm + mp.lds_base, &vb);
+                std::snprintf(buf, sizeof buf, "ds_write_b32 v%d, %s offset:%u", vb, R(m.a), off);
                 line(buf);
                 break;
+            }
             case MI_LDLD:
-                if (diag & 2) break;
-                std::snprintf(buf, sizeof buf, "ds_read_b32 %s, v%d offset:%u", R(m.d), m.imm < 256 ? V_SCROFF : rv.lds2,
-                              (m.imm & 255u) * 256u);
+            case MI_RLD: {
+                if (diag & 2 && m.op == MI_LDLD) break;
+                int vb;
+                const uint32_t off = lds_at(m.op == MI_RLD ? m.imm : m.imm + mp.lds_base, &vb);
+                std::snprintf(buf, sizeof buf, "ds_read_b32 %s, v%d offset:%u", R(m.d), vb, off);
                 line(buf);
+                break;
+            }
+            case MI_BAR:
+                line("s_barrier");
                 break;
             case MI_WAITL:
                 std::snprintf(buf, sizeof buf, "s_waitcnt lgkmcnt(%u)", m.imm); line(buf); break;
         }
     }
+}
+
+std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
+    static const Policy pol;
+    static const uint32_t diag = diag_mask();
+    const Reserved rv(mp.n_vgpr);
+    const int V_SCROFF = rv.scroff, V_OUTOFF = rv.outoff, V_SRCOFF = rv.srcoff;
+    const uint32_t acc_off = (mp.n_vgpr + N_RESERVED + 3) & ~3u;        // first AGPR in the unified file
+    const uint32_t n_regs = (acc_off + std::max<uint32_t>(mp.n_agpr, 1) + 7) & ~7u;
+    std::string s;
+    s.reserve(mp.ins.size() * 48 + 8192);
+    char buf[256];
+    auto line = [&](const char* t) { s += '\t'; s += t; s += '\n'; };
+    s += "\t.amdgcn_target \"amdgcn-amd-amdhsa--gfx950\"\n\t.amdhsa_code_object_version 6\n\t.text\n";
+    s += "\t.globl " + kname + "\n\t.p2align 8\n\t.type " + kname + ",@function\n" + kname + ":\n";
+    // Persistent loop: the grid holds as many waves as can be resident (the host sets n_wg = s49);
+    // wave w processes items w, w + n_wg, ... < n_items (s48), so its scratch lines are reused by
+    // its own next item instead of a fresh wave's, and the scratch footprint stays at the
+    // resident set.  One item = 64 dword columns (the lane -> (block, column) map below).
+    const char* pro_once[] = {
+        "s_load_dwordx8 s[4:11], s[0:1], 0x0",
+        "s_load_dwordx8 s[12:19], s[0:1], 0x20",
+        "s_load_dwordx4 s[48:51], s[0:1], 0x40",
+        "s_waitcnt lgkmcnt(0)",
+        "v_lshlrev_b32_e32 V_SCROFF, 2, v0",
+        "v_add_u32_e32 V_LDS2, 0x10000, V_SCROFF",
+        "s_mov_b32 s24, s4",
+        "s_and_b32 s25, s5, 0xffff",
+        "s_mov_b32 s26, -1",
+        "s_mov_b32 s27, 0x20000",
+        "s_mov_b32 s28, s6",
+        "s_and_b32 s29, s7, 0xffff",
+        "s_mov_b32 s30, -1",
+        "s_mov_b32 s31, 0x20000",
+        "s_mul_i32 s32, s2, s16",
+        "s_mul_hi_u32 s33, s2, s16",
+        "s_add_u32 s32, s8, s32",
+        "s_addc_u32 s33, s9, s33",
+        "s_and_b32 s33, s33, 0xffff",
+        "s_mov_b32 s34, -1",
+        "s_mov_b32 s35, 0x20000",
+        "s_mov_b32 s36, 0x090b080a",
+        "s_mov_b32 s37, 0xfefefefe",
+        "s_mov_b32 s38, 0x1d1d1d1d",
+        "s_mov_b32 s52, s2",
+    };
+    const char* pro_iter[] = {
+        // (the program is longer than a 16-bit branch reaches: exit in place, loop back by s_setpc)
+        "s_cmp_lt_u32 s52, s48",
+        "s_cbranch_scc1 .Lbody",
+        "s_endpgm",
+        ".Lbody:",
+        "s_mov_b64 exec, -1",
+        // XCD-aware item order: workgroups are dealt to the 8 XCDs round-robin, so logical item
+        // L = (w % 8) * q + w / 8 (for w < 8q; s17 = q, s18 = 8q, both 0 = identity) keeps the
+        // items of one block, which share the 128-B lines at their 256-B segment edges, on one L2.
+        "s_and_b32 s39, s52, 7",
+        "s_mul_i32 s39, s39, s17",
+        "s_lshr_b32 s40, s52, 3",
+        "s_add_u32 s39, s39, s40",
+        "s_cmp_lt_u32 s52, s18",
+        "s_cselect_b32 s39, s39, s52",
+        "s_lshl_b32 s20, s39, 6",
+        "v_lshrrev_b32_e32 v0, 2, V_SCROFF",
+        "v_add_u32_e32 v1, s20, v0",
+        "v_cmp_gt_u32_e64 s[22:23], s13, v1",
+        "s_and_b64 exec, exec, s[22:23]",
+        "v_mul_hi_u32 v2, v1, s14",
+        "v_lshrrev_b32_e32 v2, s15, v2",
+        "s_lshr_b32 s21, s12, 2",
+        "v_mul_lo_u32 v3, v2, s21",
+        "v_sub_u32_e32 v3, v1, v3",
+        "v_lshlrev_b32_e32 v3, 2, v3",
+        "v_mul_lo_u32 v4, v2, s10",
+        "v_add_u32_e32 V_SRCOFF, v4, v3",
+        "v_mul_lo_u32 v4, v2, s11",
+        "v_add_u32_e32 V_OUTOFF, v4, v3",
+    };
+    auto put = [&](const char* p) {
+        std::string l(p);
+        const std::pair<const char*, int> names[] = {
+            {"V_SRCOFF", V_SRCOFF}, {"V_OUTOFF", V_OUTOFF}, {"V_SCROFF", V_SCROFF}, {"V_LDS2", rv.lds2}};
+        for (const auto& nm : names)
+            for (size_t at = l.find(nm.first); at != std::string::npos; at = l.find(nm.first))
+                l.replace(at, std::strlen(nm.first), "v" + std::to_string(nm.second));
+        line(l.c_str());
+    };
+    const uint32_t W = std::max<uint32_t>(1, mp.wg_waves);
+    const uint32_t LB = mp.n_lds_slots * 256u;  // LDS bytes per wave
+    if (W == 1) {
+        for (const char* p : pro_once) put(p);
+    } else {
+        // W waves per workgroup (one per SIMD of a CU) take W consecutive items, i.e. the W x 256-B
+        // pieces of the same source rows (1 KiB at W = 4), which then reach the memory system close
+        // together.  Wave w of the workgroup: LDS slots at w * LB (folded into V_SCROFF, the lane's
+        // LDS / scratch voffset), scratch of global wave (wg * W + w), its base moved back by w * LB
+        // because V_SCROFF carries that LDS offset too.
+        for (const char* p : pro_once) {
+            const std::string l(p);
+            if (l.rfind("v_lshlrev_b32_e32 V_SCROFF", 0) == 0 || l.rfind("v_add_u32_e32 V_LDS2", 0) == 0 ||
+                l.rfind("s_mul_i32 s32", 0) == 0 || l.rfind("s_mul_hi_u32 s33", 0) == 0)
+                continue;
+            if (l.rfind("s_add_u32 s32, s8, s32", 0) == 0) {
+                put("v_lshrrev_b32_e32 v1, 6, v0");
+                line("s_nop 4");  // VALU write -> v_readfirstlane of it (a missing wait state read v1 stale)
+                line("v_readfirstlane_b32 s53, v1");
+                put("v_and_b32_e32 v0, 63, v0");
+                put("v_lshlrev_b32_e32 V_SCROFF, 2, v0");
+                std::snprintf(buf, sizeof buf, "s_mul_i32 s41, s53, %u", LB); line(buf);
+                put("v_add_u32_e32 V_SCROFF, s41, V_SCROFF");
+                put("v_add_u32_e32 V_LDS2, 0x10000, V_SCROFF");
+                std::snprintf(buf, sizeof buf, "s_mul_i32 s42, s2, %u", W); line(buf);
+                line("s_add_u32 s42, s42, s53");
+                line("s_mul_i32 s32, s42, s16");
+                line("s_mul_hi_u32 s33, s42, s16");
+                line("s_sub_u32 s32, s32, s41");
+                line("s_subb_u32 s33, s33, 0");
+            }
+            put(p);
+        }
+    }
+    // Scratch slot s sits at soffset 4096 * (s / 16) + offset (s % 16) * 256: soffset 0 or one of
+    // SCR_BASES SGPRs s56.. loaded once, so a spill or reload carries no SALU; slots beyond them
+    // (very large K) form their soffset with an s_mov.
+    const uint32_t n_bases = scratch_bases(mp);
+    for (uint32_t j = 0; j < n_bases; ++j) {
+        std::snprintf(buf, sizeof buf, "s_mov_b32 s%u, %u", 56 + j, 4096u * (j + 1));
+        line(buf);
+    }
+    // Code warm-up (W = 1): the program is ~180 KB of straight-line code that every wave starts at
+    // once, and when the previous kernel was not a column program its lines are in neither L2 nor the
+    // memory-side cache, so round 1's instruction fetches go to HBM one after another (12-15 us per
+    // launch after a decode's apply, ~30 us after a large copy: profiles/r03_dense/r03pos).  Each wave
+    // reads four 8 KiB strides of its own code (one dword per 128-B line; slice (wg / 8) % 32 within
+    // its XCD), so the XCD's waves pull the whole program into their L2 in parallel, then wait once.
+    // Bounds-checked buffer loads (num_records = code length): nothing beyond the code is read.
+    static const bool code_pf = [] { const char* e = knob("RQHIP_CODEPF"); return !e || e[0] != '0'; }();
+    if (W == 1 && code_pf && !(diag & 4) && mp.n_vgpr >= 12) {  // v5, v6, v8..v11 are program registers
+        line("s_getpc_b64 s[44:45]");
+        s += ".Lcpf:\n";
+        line(("s_sub_u32 s44, s44, .Lcpf-" + kname).c_str());
+        line("s_subb_u32 s45, s45, 0");
+        line("s_and_b32 s45, s45, 0xffff");
+        line(("s_mov_b32 s46, .Lfunc_end-" + kname).c_str());
+        line("s_mov_b32 s47, 0x20000");
+        line("s_lshr_b32 s43, s2, 3");
+        line("s_and_b32 s43, s43, 31");
+        line("s_lshl_b32 s43, s43, 13");
+        line("v_lshlrev_b32_e32 v5, 7, v0");
+        line("v_add_u32_e32 v5, s43, v5");
+        for (uint32_t k = 0; k < 4; ++k) {
+            std::snprintf(buf, sizeof buf, "v_add_u32_e32 v6, 0x%x, v5", k * 32u * 8192u); line(buf);
+            std::snprintf(buf, sizeof buf, "buffer_load_dword v%u, v6, s[44:47], 0 offen", 8 + k); line(buf);
+        }
+        line("s_waitcnt vmcnt(0)");
+    }
+    // experiments: RQHIP_STAGGER=n delays the odd workgroups' start by n x 127 x 64 cycles (do the
+    // first rounds' coinciding load bursts cost time?)
+    static const uint32_t stagger = [] { const char* e = knob("RQHIP_STAGGER"); return e ? (uint32_t)std::atoi(e) : 0u; }();
+    if (stagger) {
+        line("s_bitcmp1_b32 s2, 0");
+        line("s_cbranch_scc0 .Lnostagger");
+        for (uint32_t i = 0; i < stagger; ++i) line("s_sleep 127");
+        s += ".Lnostagger:\n";
+    }
+    s += ".Lloop:\n";
+    for (const char* p : pro_iter) {
+        const std::string l(p);
+        if (W > 1 && l.rfind("s_lshl_b32 s20, s39, 6", 0) == 0) {  // item = iteration * W + wave
+            std::snprintf(buf, sizeof buf, "s_mul_i32 s39, s39, %u", W); line(buf);
+            line("s_add_u32 s39, s39, s53");
+        }
+        if (W > 1 && l.rfind("v_lshrrev_b32_e32 v0, 2, V_SCROFF", 0) == 0) {  // lane id (V_SCROFF has w * LB)
+            line("v_mbcnt_lo_u32_b32 v0, -1, 0");
+            line("v_mbcnt_hi_u32_b32 v0, -1, v0");
+            continue;
+        }
+        put(p);
+    }
+    emit_colprog_body(mp, W, s);
     // Loop end: no vmcnt drain.  The item's last memory operations are its output stores (every load
     // has been consumed), and the next item's program may run while they retire: vmcnt waits in it
     // then also cover these older stores (conservative, still exact), scratch slots are reused in
@@ -989,32 +1069,42 @@ inline uint32_t xtime4(uint32_t x) {
 }
 }  // namespace
 
-bool emulate_colprog(const MProg& mp, const uint8_t* src, uint32_t T, uint8_t* out, std::string* err) {
-    const uint32_t Td = T / 4;
-    std::vector<std::vector<uint32_t>> R(512, std::vector<uint32_t>(Td, 0));
-    std::vector<std::vector<uint32_t>> scr(mp.n_slots, std::vector<uint32_t>(Td, 0));
-    std::vector<uint64_t> pend(512, 0), slot_st(mp.n_slots, 0), lpend(512, 0);
-    std::vector<std::vector<uint32_t>> lds(std::max<uint32_t>(mp.n_lds_slots, 1), std::vector<uint32_t>(Td, 0));
-    std::vector<uint64_t> lds_dma(std::max<uint32_t>(mp.n_lds_slots, 1), 0);  // pending DMA seq per slot
+namespace {
+// One wave's machine state for the emulators: registers, scratch, its LDS spill slots, the vmcnt / lgkmcnt
+// bookkeeping.  Ring stores / loads and barriers (pair programs) go to the hooks.
+struct WaveEmu {
+    const MProg& mp;
+    const uint8_t* src;
+    uint32_t T, Td;
+    uint8_t* out;
+    std::string* err;
+    std::vector<std::vector<uint32_t>> R, scr, lds;
+    std::vector<uint64_t> pend, slot_st, lpend, lds_dma;
     uint64_t seq = 0, retired = 0, lseq = 0, lretired = 0;
-    char buf[160];
-    auto bad = [&](size_t i, const char* what) {
+    std::function<bool(uint32_t, const std::vector<uint32_t>&)> ring_store;
+    std::function<bool(uint32_t, std::vector<uint32_t>*)> ring_load;
+    std::function<void()> barrier;
+    char buf[200];
+
+    WaveEmu(const MProg& m, const uint8_t* s, uint32_t t, uint8_t* o, std::string* e)
+        : mp(m), src(s), T(t), Td(t / 4), out(o), err(e), R(512, std::vector<uint32_t>(t / 4, 0)),
+          scr(m.n_slots, std::vector<uint32_t>(t / 4, 0)),
+          lds(std::max<uint32_t>(m.n_lds_slots, 1), std::vector<uint32_t>(t / 4, 0)), pend(512, 0),
+          slot_st(m.n_slots, 0), lpend(512, 0), lds_dma(std::max<uint32_t>(m.n_lds_slots, 1), 0) {}
+
+    bool bad(size_t i, const char* what) {
         std::snprintf(buf, sizeof buf, "emulate: instruction %zu: %s", i, what);
         if (err) *err = buf;
         return false;
-    };
-    for (size_t i = 0; i < mp.ins.size(); ++i) {
-        const MInst& m = mp.ins[i];
-        auto ready = [&](int r) {
-            return r < 0 || ((pend[r] == 0 || pend[r] <= retired) && (lpend[r] == 0 || lpend[r] <= lretired));
-        };
+    }
+    bool ready(int r) const {
+        return r < 0 || ((pend[r] == 0 || pend[r] <= retired) && (lpend[r] == 0 || lpend[r] <= lretired));
+    }
+    bool vmem() { return ++seq - retired <= 63; }
+
+    bool step(size_t i, const MInst& m) {
         if (!ready(m.a) || !ready(m.b) || !ready(m.c)) return bad(i, "operand read before its load completed");
         if (m.op != MI_DMA && m.d >= 0 && !ready(m.d)) return bad(i, "register overwritten while a load into it is pending");
-        auto vmem = [&]() {
-            ++seq;
-            if (seq - retired > 63) return false;
-            return true;
-        };
         switch (m.op) {
             case MI_XOR2:
                 for (uint32_t c = 0; c < Td; ++c) R[m.d][c] = R[m.a][c] ^ R[m.b][c];
@@ -1025,10 +1115,9 @@ bool emulate_colprog(const MProg& mp, const uint8_t* src, uint32_t T, uint8_t* o
             case MI_XT:
                 for (uint32_t c = 0; c < Td; ++c) R[m.d][c] = xtime4(R[m.a][c]);
                 break;
-            case MI_XTX: {
+            case MI_XTX:
                 for (uint32_t c = 0; c < Td; ++c) R[m.d][c] = xtime4(R[m.a][c]) ^ R[m.b][c];
                 break;
-            }
             case MI_ZERO:
                 std::fill(R[m.d].begin(), R[m.d].end(), 0u);
                 break;
@@ -1091,6 +1180,22 @@ bool emulate_colprog(const MProg& mp, const uint8_t* src, uint32_t T, uint8_t* o
                 if (!vmem()) return bad(i, "more than 63 vector-memory operations outstanding");
                 lds_dma[m.d] = seq;
                 break;
+            case MI_RST:
+                if (!ring_store) return bad(i, "ring store outside a pair program");
+                if (!ring_store(m.imm, R[m.a])) return bad(i, err && !err->empty() ? err->c_str() : "ring store");
+                if (++lseq - lretired > 15) return bad(i, "more than 15 LDS operations outstanding");
+                break;
+            case MI_RLD:
+                if (!ring_load) return bad(i, "ring load outside a pair program");
+                if (!ring_load(m.imm, &R[m.d])) return bad(i, err && !err->empty() ? err->c_str() : "ring load");
+                if (++lseq - lretired > 15) return bad(i, "more than 15 LDS operations outstanding");
+                lpend[m.d] = lseq;
+                break;
+            case MI_BAR:
+                if (lseq != lretired) return bad(i, "barrier with LDS operations outstanding");
+                if (!barrier) return bad(i, "barrier outside a pair program");
+                barrier();
+                break;
         }
         if ((m.op == MI_XOR2 || m.op == MI_XOR3 || m.op == MI_XT || m.op == MI_XTX || m.op == MI_ZERO) &&
             (m.d >= REG_A0 || m.a >= REG_A0 || m.b >= REG_A0 || m.c >= REG_A0))
@@ -1099,8 +1204,250 @@ bool emulate_colprog(const MProg& mp, const uint8_t* src, uint32_t T, uint8_t* o
         if ((m.op <= MI_ZERO) && (m.d >= nva || (m.a >= nva && m.a < REG_A0) || (m.b >= nva && m.b < REG_A0) ||
                                   (m.c >= nva && m.c < REG_A0)))
             return bad(i, "VALU operand in a reserved VGPR");
+        return true;
+    }
+    bool run() {
+        // each item's allocation assumes no vector-memory operation outstanding at its start (the
+        // previous item's last ones are stores; at 63 outstanding the hardware holds further issue)
+        retired = seq;
+        for (size_t i = 0; i < mp.ins.size(); ++i)
+            if (!step(i, mp.ins[i])) return false;
+        lretired = lseq;  // the loop end's lgkmcnt(0)
+        return true;
+    }
+};
+}  // namespace
+
+bool emulate_colprog(const MProg& mp, const uint8_t* src, uint32_t T, uint8_t* out, std::string* err) {
+    WaveEmu w(mp, src, T, out, err);
+    return w.run();
+}
+
+// ------------------------------------------------------------------------------------------
+// Two-wave (pair) programs.
+
+bool compile_pair(const ColIR& ir, const AllocOpts& o, uint32_t bmask, uint32_t lag, uint32_t max_xfer, uint32_t ring,
+                  PairProg* pp, std::string* err) {
+    PairIR px;
+    if (!split_pair(ir, bmask, lag, max_xfer, ring, &px, err)) return false;
+    *pp = PairProg();
+    pp->lag = lag;
+    ring = px.ring;  // the smallest ring that passed split_pair's window check
+    pp->ring = ring;
+    pp->n_xfer = px.n_xfer;
+    pp->n_cross = px.n_cross;
+    pp->bmask = bmask;
+    constexpr uint32_t WG_SLOTS = 320;  // 80 KiB of LDS per workgroup: two workgroups per CU
+    if (ring + 16 > WG_SLOTS) {
+        if (err) *err = "compile_pair: ring too large";
+        return false;
+    }
+    // B first (small live set: a few LDS slots at most), then A with the LDS that is left
+    AllocOpts ob = o;
+    ob.n_lds = std::min<uint32_t>(o.n_lds, 32);
+    ob.la_dma = 0;
+    if (!allocate_colprog(px.B, ob, &pp->B, err)) return false;
+    if (pp->B.n_slots) {
+        if (err) *err = "compile_pair: wave B needs global scratch";
+        return false;
+    }
+    AllocOpts oa = o;
+    oa.n_lds = std::min<uint32_t>(o.n_lds, WG_SLOTS - ring - pp->B.n_lds_slots);
+    oa.la_dma = 0;
+    if (!allocate_colprog(px.A, oa, &pp->A, err)) return false;
+    pp->A.lds_base = ring;
+    pp->B.lds_base = ring + pp->A.n_lds_slots;
+    pp->A.wg_waves = pp->B.wg_waves = 2;
+    return true;
+}
+
+double pair_cost(const PairProg& pp) {
+    // the two waves issue on different SIMDs: the longer one sets the item time (A's also carries
+    // the memory instructions), plus a slot per barrier for the rendezvous
+    return std::max(colprog_cost(pp.A), colprog_cost(pp.B));
+}
+
+uint32_t pair_lds_bytes(const PairProg& pp) {
+    return (pp.ring + pp.A.n_lds_slots + pp.B.n_lds_slots) * 256u;
+}
+
+bool emulate_pair(const PairProg& pp, const uint8_t* src, uint32_t T, uint8_t* out, std::string* err, uint32_t iters) {
+    const uint32_t Td = T / 4;
+    // A's ring writes: per slot, (A barrier count at the write, data)
+    std::vector<std::vector<std::pair<uint64_t, std::vector<uint32_t>>>> hist(pp.ring);
+    uint64_t a_bars = 0, b_bars = pp.lag;  // B starts with `lag` barriers
+    std::string e2;
+    WaveEmu A(pp.A, src, T, out, &e2), B(pp.B, src, T, out, &e2);
+    A.ring_store = [&](uint32_t sl, const std::vector<uint32_t>& v) {
+        if (sl >= pp.ring) { e2 = "ring slot out of range"; return false; }
+        hist[sl].push_back({a_bars, v});
+        return true;
+    };
+    A.barrier = [&]() { ++a_bars; };
+    B.barrier = [&]() { ++b_bars; };
+    B.ring_load = [&](uint32_t sl, std::vector<uint32_t>* d) {
+        if (sl >= pp.ring) { e2 = "ring slot out of range"; return false; }
+        // visible: A's writes before A's barrier b_bars (A count <= b_bars - 1); a write in A's interval
+        // b_bars runs concurrently with this read
+        const std::vector<uint32_t>* v = nullptr;
+        for (const auto& h : hist[sl]) {
+            if (h.first == b_bars) { e2 = "ring race: A writes the slot in the interval B reads it"; return false; }
+            if (h.first + 1 <= b_bars) v = &h.second;
+        }
+        if (!v) { e2 = "ring read of a slot A has not written"; return false; }
+        *d = *v;
+        return true;
+    };
+    for (uint32_t it = 0; it < iters; ++it)
+        if (!A.run()) { if (err) *err = "wave A: " + e2; return false; }
+    for (uint32_t it = 0; it < iters; ++it)
+        if (!B.run()) { if (err) *err = "wave B: " + e2; return false; }
+    (void)Td;
+    // per item the two waves execute the same number of barriers
+    if (a_bars != (uint64_t)pp.n_xfer * iters || b_bars != pp.lag + (uint64_t)pp.n_xfer * iters) {
+        if (err) *err = "emulate_pair: barrier counts differ from the transfer count";
+        return false;
     }
     return true;
+}
+
+std::string emit_pair_asm(const PairProg& pp, const std::string& kname) {
+    const MProg& A = pp.A;
+    const MProg& B = pp.B;
+    const Reserved rv(A.n_vgpr);
+    const uint32_t acc_off = (A.n_vgpr + N_RESERVED + 3) & ~3u;
+    const uint32_t n_regs = std::max(colprog_regs(A), colprog_regs(B));
+    std::string s;
+    s.reserve((A.ins.size() + B.ins.size()) * 48 + 16384);
+    char buf[256];
+    auto line = [&](const char* t) { s += '\t'; s += t; s += '\n'; };
+    auto put = [&](const char* p) {
+        std::string l(p);
+        const std::pair<const char*, int> names[] = {
+            {"V_SRCOFF", rv.srcoff}, {"V_OUTOFF", rv.outoff}, {"V_SCROFF", rv.scroff}, {"V_LDS2", rv.lds2}};
+        for (const auto& nm : names)
+            for (size_t at = l.find(nm.first); at != std::string::npos; at = l.find(nm.first))
+                l.replace(at, std::strlen(nm.first), "v" + std::to_string(nm.second));
+        line(l.c_str());
+    };
+    s += "\t.amdgcn_target \"amdgcn-amd-amdhsa--gfx950\"\n\t.amdhsa_code_object_version 6\n\t.text\n";
+    s += "\t.globl " + kname + "\n\t.p2align 8\n\t.type " + kname + ",@function\n" + kname + ":\n";
+    // Common prologue: kernel arguments, buffer resources, constants; wave 0 of the workgroup runs A,
+    // wave 1 runs B.  Workgroup g takes items g, g + n_wg, ... (s52 / s49 / s48), both waves alike.
+    const char* pro[] = {
+        "s_load_dwordx8 s[4:11], s[0:1], 0x0",
+        "s_load_dwordx8 s[12:19], s[0:1], 0x20",
+        "s_load_dwordx4 s[48:51], s[0:1], 0x40",
+        "v_lshrrev_b32_e32 v1, 6, v0",
+        "s_nop 4",
+        "v_readfirstlane_b32 s53, v1",
+        "v_and_b32_e32 v0, 63, v0",
+        "v_lshlrev_b32_e32 V_SCROFF, 2, v0",
+        "v_add_u32_e32 V_LDS2, 0x10000, V_SCROFF",
+        "s_waitcnt lgkmcnt(0)",
+        "s_mov_b32 s24, s4",
+        "s_and_b32 s25, s5, 0xffff",
+        "s_mov_b32 s26, -1",
+        "s_mov_b32 s27, 0x20000",
+        "s_mov_b32 s28, s6",
+        "s_and_b32 s29, s7, 0xffff",
+        "s_mov_b32 s30, -1",
+        "s_mov_b32 s31, 0x20000",
+        "s_mul_i32 s32, s2, s16",
+        "s_mul_hi_u32 s33, s2, s16",
+        "s_add_u32 s32, s8, s32",
+        "s_addc_u32 s33, s9, s33",
+        "s_and_b32 s33, s33, 0xffff",
+        "s_mov_b32 s34, -1",
+        "s_mov_b32 s35, 0x20000",
+        "s_mov_b32 s36, 0x090b080a",
+        "s_mov_b32 s37, 0xfefefefe",
+        "s_mov_b32 s38, 0x1d1d1d1d",
+        "s_mov_b32 s52, s2",
+        "s_cmp_eq_u32 s53, 0",
+        "s_cbranch_scc1 .LA",
+        // wave B: a far jump (the A program is longer than a 16-bit branch reaches)
+        "s_getpc_b64 s[54:55]",
+    };
+    for (const char* p : pro) put(p);
+    s += ".Lpcb:\n";
+    line("s_add_u32 s54, s54, .LB-.Lpcb");
+    line("s_addc_u32 s55, s55, 0");
+    line("s_setpc_b64 s[54:55]");
+    // the item's lane -> (block, dword column) map (as emit_colprog_asm's W = 1 loop head)
+    const char* iter[] = {
+        "s_mov_b64 exec, -1",
+        "s_and_b32 s39, s52, 7",
+        "s_mul_i32 s39, s39, s17",
+        "s_lshr_b32 s40, s52, 3",
+        "s_add_u32 s39, s39, s40",
+        "s_cmp_lt_u32 s52, s18",
+        "s_cselect_b32 s39, s39, s52",
+        "s_lshl_b32 s20, s39, 6",
+        "v_lshrrev_b32_e32 v0, 2, V_SCROFF",
+        "v_add_u32_e32 v1, s20, v0",
+        "v_cmp_gt_u32_e64 s[22:23], s13, v1",
+        "s_and_b64 exec, exec, s[22:23]",
+        "v_mul_hi_u32 v2, v1, s14",
+        "v_lshrrev_b32_e32 v2, s15, v2",
+        "s_lshr_b32 s21, s12, 2",
+        "v_mul_lo_u32 v3, v2, s21",
+        "v_sub_u32_e32 v3, v1, v3",
+        "v_lshlrev_b32_e32 v3, 2, v3",
+        "v_mul_lo_u32 v4, v2, s10",
+        "v_add_u32_e32 V_SRCOFF, v4, v3",
+        "v_mul_lo_u32 v4, v2, s11",
+        "v_add_u32_e32 V_OUTOFF, v4, v3",
+    };
+    auto wave = [&](const MProg& mp, const char* tag, bool is_a) {
+        s += std::string(".L") + tag + ":\n";
+        const uint32_t nb = std::min<uint32_t>(SCR_BASES, mp.n_slots > 16 ? (mp.n_slots - 1) / 16 : 0);
+        for (uint32_t j = 0; j < nb; ++j) {
+            std::snprintf(buf, sizeof buf, "s_mov_b32 s%u, %u", 56 + j, 4096u * (j + 1));
+            line(buf);
+        }
+        if (!is_a)  // B trails A by `lag` transfers: its first `lag` barriers pair with A's first transfers
+            for (uint32_t j = 0; j < pp.lag; ++j) line("s_barrier");
+        s += std::string(".L") + tag + "_loop:\n";
+        line("s_cmp_lt_u32 s52, s48");
+        std::snprintf(buf, sizeof buf, "s_cbranch_scc1 .L%s_body", tag);
+        line(buf);
+        if (is_a)  // A's last `lag` barriers pair with B's barriers of the last item's last transfers
+            for (uint32_t j = 0; j < pp.lag; ++j) line("s_barrier");
+        line("s_endpgm");
+        s += std::string(".L") + tag + "_body:\n";
+        for (const char* p : iter) put(p);
+        emit_colprog_body(mp, 1, s);
+        line("s_waitcnt lgkmcnt(0)");
+        line("s_add_u32 s52, s52, s49");
+        line("s_getpc_b64 s[54:55]");
+        s += std::string(".L") + tag + "_pc:\n";
+        std::snprintf(buf, sizeof buf, "s_sub_u32 s54, s54, .L%s_pc-.L%s_loop", tag, tag);
+        line(buf);
+        line("s_subb_u32 s55, s55, 0");
+        line("s_setpc_b64 s[54:55]");
+    };
+    wave(A, "A", true);
+    wave(B, "B", false);
+    s += ".Lfunc_end:\n\t.size " + kname + ", .Lfunc_end-" + kname + "\n";
+    s += "\t.p2alignl 6, 3212836864\n\t.fill 256, 4, 3212836864\n";
+    s += "\t.section .rodata,\"a\",@progbits\n\t.p2align 6, 0x0\n\t.amdhsa_kernel " + kname + "\n";
+    const std::string lds = std::to_string(pair_lds_bytes(pp));
+    s += "\t\t.amdhsa_group_segment_fixed_size " + lds + "\n\t\t.amdhsa_private_segment_fixed_size 0\n";
+    s += "\t\t.amdhsa_kernarg_size 80\n\t\t.amdhsa_user_sgpr_count 2\n";
+    s += "\t\t.amdhsa_user_sgpr_kernarg_segment_ptr 1\n\t\t.amdhsa_system_sgpr_workgroup_id_x 1\n";
+    s += "\t\t.amdhsa_system_vgpr_workitem_id 0\n\t\t.amdhsa_next_free_vgpr " + std::to_string(n_regs) + "\n";
+    s += "\t\t.amdhsa_next_free_sgpr " + std::to_string(ROW_WIN + 32) + "\n\t\t.amdhsa_accum_offset " + std::to_string(acc_off) +
+         "\n\t\t.amdhsa_reserve_vcc 0\n";
+    s += "\t\t.amdhsa_ieee_mode 0\n\t\t.amdhsa_dx10_clamp 0\n\t.end_amdhsa_kernel\n\t.text\n";
+    s += "\t.amdgpu_metadata\n---\namdhsa.kernels:\n  - .agpr_count: " + std::to_string(n_regs - acc_off) + "\n    .args:\n";
+    s += "      - .offset: 0\n        .size: 80\n        .value_kind: by_value\n";
+    s += "    .group_segment_fixed_size: " + lds + "\n    .kernarg_segment_align: 8\n    .kernarg_segment_size: 80\n";
+    s += "    .max_flat_workgroup_size: 128\n    .name: " + kname + "\n    .private_segment_fixed_size: 0\n";
+    s += "    .sgpr_count: " + std::to_string(ROW_WIN + 32) + "\n    .symbol: " + kname + ".kd\n    .vgpr_count: " + std::to_string(n_regs) +
+         "\n    .wavefront_size: 64\n";
+    s += "amdhsa.target: amdgcn-amd-amdhsa--gfx950\namdhsa.version:\n  - 1\n  - 2\n...\n\t.end_amdgpu_metadata\n";
+    return s;
 }
 
 }  // namespace rq

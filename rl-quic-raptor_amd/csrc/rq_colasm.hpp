@@ -30,6 +30,9 @@ enum MOp : uint8_t {
     MI_LDLD,    // d <- LDS slot imm (ds_read_b32)
     MI_WAITL,   // s_waitcnt lgkmcnt(imm)
     MI_DMA,     // LDS slot d <- source row imm (buffer_load ... lds: no register, counts in vmcnt)
+    MI_RST,     // pair programs: ring slot imm <- a (ds_write_b32)
+    MI_RLD,     // pair programs: d <- ring slot imm (ds_read_b32)
+    MI_BAR,     // pair programs: s_barrier (after an lgkmcnt(0) the allocator emits)
 };
 
 constexpr int REG_A0 = 256;       // register ids: 0..255 VGPR, 256..511 AGPR
@@ -73,12 +76,14 @@ struct MProg {
     uint32_t n_out = 0;
     uint32_t K = 0;
     uint32_t wg_waves = 1;       // waves per workgroup (emit_colprog_asm): W consecutive items per CU
+    uint32_t lds_base = 0;       // LDS slot of the program's spill slot 0 (pair programs: after the ring)
     struct Stats {
         uint32_t valu = 0, ldsrc = 0, stout = 0, spst = 0, spld = 0, accw = 0, accr = 0, wait = 0, nop = 0;
         uint32_t sync_reload = 0;  // reloads that were not prefetched
         uint32_t ldst = 0, ldld = 0, waitl = 0;  // LDS spill stores / reloads / lgkm waits
         uint32_t migrate = 0;                    // LDS residents pushed out to global scratch
         uint32_t dma = 0;                        // source rows staged through LDS by DMA
+        uint32_t rst = 0, rld = 0, bar = 0;      // pair programs: ring stores / loads, barriers
     } st;
 };
 
@@ -128,6 +133,27 @@ uint32_t colprog_regs(const MProg& mp);
 // Executes the machine program on the host for one block (T/4 lanes), checking vmcnt waits and
 // scratch ordering as it goes.  Test infrastructure for the allocator, not a product path.
 bool emulate_colprog(const MProg& mp, const uint8_t* src, uint32_t T, uint8_t* out, std::string* err);
+
+// ---- two-wave (pair) column programs (split_pair in rq_colprog.hpp) ----
+struct PairProg {
+    MProg A, B;              // wave 0 (A: loads, forward pass, pushes) and wave 1 (B: HDPC, dense, outputs)
+    uint32_t lag = 0, ring = 0, n_xfer = 0, n_cross = 0;
+    uint32_t bmask = 0;      // IrNode::grp values run by wave B
+};
+// Splits and allocates (both waves with the budget of `o`, one wave per SIMD; LDS: the ring, then A's
+// spill slots, then B's; at most 80 KiB per workgroup so that two workgroups share a CU).
+bool compile_pair(const ColIR& ir, const AllocOpts& o, uint32_t bmask, uint32_t lag, uint32_t max_xfer, uint32_t ring,
+                  PairProg* pp, std::string* err);
+// Model of a pair launch's time per item (issue slots of the longer wave), comparable with
+// colprog_cost of a single-wave program.
+double pair_cost(const PairProg& pp);
+uint32_t pair_lds_bytes(const PairProg& pp);
+std::string emit_pair_asm(const PairProg& pp, const std::string& kname);
+// Runs wave A's and wave B's machine programs over `iters` consecutive items of one block (the ring
+// carries across items as on the GPU), checking that every ring read in B's barrier interval m sees
+// the last value A wrote before barrier m and that no A write to that slot lands in interval m.
+bool emulate_pair(const PairProg& pp, const uint8_t* src, uint32_t T, uint8_t* out, std::string* err,
+                  uint32_t iters = 2);
 
 // In-process assembly (amd_comgr, rq_comgr.cpp): assembly text -> gfx950 code object.
 bool comgr_assemble(const std::string& src, std::vector<char>* co, std::string* err);

@@ -44,7 +44,11 @@ enum IrKind : uint8_t {
     IR_XOR3 = 3,  // a ^ b ^ c
     IR_XT = 4,    // alpha * a (per byte, GF(256) poly 0x11D)
     IR_XTX = 5,   // alpha * a ^ b
-    IR_STORE = 6  // output imm <- a
+    IR_STORE = 6,  // output imm <- a
+    // two-wave (pair) programs only (split_pair): the hand-off between the waves through an LDS ring
+    IR_SEND = 7,   // ring slot imm <- a (wave A)
+    IR_RECV = 8,   // value <- ring slot imm (wave B)
+    IR_BAR = 9     // workgroup barrier closing a transfer (imm = transfer index)
 };
 constexpr uint32_t NOVAL = 0xFFFFFFFFu;
 // build_colprog's `passes` with this bit set: replacement-selection Horner runs with a buffer of
@@ -57,7 +61,10 @@ struct IrNode {
     uint8_t k = IR_ZERO;
     uint32_t a = NOVAL, b = NOVAL, c = NOVAL;  // operand value ids (node indices)
     uint32_t imm = 0;
-    uint8_t grp = 0;  // 1: HDPC bit accumulation (SCHED_4R subset sums, bit rows, bh); else 0
+    // what the node computes (SCHED_4R programs; split_pair assigns waves by it): 0 forward pass
+    // (peeling: y values and their pushes into dependent rows), 1 HDPC bit accumulation (subset sums,
+    // bit rows, bh), 2 pushes into the remaining-row and output sums (and b2), 3 dense part and outputs
+    uint8_t grp = 0;
 };
 
 struct ColIR {
@@ -80,6 +87,24 @@ bool build_colprog(const Params& p, const uint32_t* esi, uint32_t n_out, ColIR* 
                    uint32_t passes = 0);
 // Outputs are the L intermediate symbols C[0..L-1] (per-object encoder: GenSymbol gathers).
 bool build_colprog_C(const Params& p, ColIR* ir, std::string* err, uint32_t passes = 0);
+// Two-wave split of a column program (one workgroup of two waves per item, one wave per SIMD):
+// wave A runs the nodes whose grp is not in bmask -- every source load, the forward pass, the pushes
+// -- and wave B the others (the HDPC bit accumulation, the dense part and the outputs), so B's VALU
+// work never waits behind A's memory instructions in one in-order issue stream.  Every A value that
+// B uses goes through a ring of LDS slots in transfers of at most max_xfer values, each closed by a
+// workgroup barrier; B runs `lag` transfers behind A (B starts with `lag` barriers, A ends with
+// them).  No B value may feed an A node.
+struct PairIR {
+    ColIR A, B;
+    uint32_t lag = 0;
+    uint32_t ring = 0;       // ring slots (256 B each) at the start of the workgroup's LDS
+    uint32_t n_xfer = 0;     // transfers per item (= barriers per item on each side)
+    uint32_t n_cross = 0;    // values handed from A to B per item
+    uint32_t max_window = 0; // most slots in use at once (lag + 2 consecutive transfers)
+};
+bool split_pair(const ColIR& ir, uint32_t bmask, uint32_t lag, uint32_t max_xfer, uint32_t ring, PairIR* out,
+                std::string* err);
+
 // Host evaluation of the IR on one block (test reference for the compiler, not a product path):
 // src = K rows x T bytes, out = n_out rows x T bytes.
 void eval_colprog(const ColIR& ir, const uint8_t* src, uint32_t T, uint8_t* out);

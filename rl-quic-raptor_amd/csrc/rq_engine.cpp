@@ -89,6 +89,7 @@ struct ColKernel {
     uint32_t n_out = 0, n_slots = 0, n_ins = 0;
     uint32_t waves_per_cu = 4;     // residency of the code object (registers, LDS)
     uint32_t wg_waves = 1;         // waves per workgroup (MProg::wg_waves)
+    bool pair = false;             // two-wave program (emit_pair_asm): one item per workgroup iteration
     MProg::Stats st{};
     uint64_t last_use = 0;         // LRU clock of the per-device cache
     DevBuf mrep;                   // decode: outputs on the identity payload
@@ -396,12 +397,12 @@ uint64_t library_hash() {
 
 struct CacheHdr {
     char magic[8];
-    uint32_t n_out, n_slots, n_ins, waves_per_cu, name_len, n_rows, wg_waves, pad;
+    uint32_t n_out, n_slots, n_ins, waves_per_cu, name_len, n_rows, wg_waves, flags;  // flags bit 0: pair
     uint64_t co_len;
     MProg::Stats st;
     uint64_t body_hash;  // FNV-1a of the name, code object and row table (checked on load)
 };
-constexpr char CACHE_MAGIC[9] = "RQCO0004";
+constexpr char CACHE_MAGIC[9] = "RQCO0005";
 
 uint64_t cache_body_hash(const std::string& name, const std::vector<char>& co, const std::vector<uint32_t>& rows) {
     uint64_t h = fnv1a(name.data(), name.size());
@@ -473,6 +474,52 @@ uint32_t colprog_launch_shape(MProg* mp) {
 }
 
 // ---------------- column programs (the encode hot path) ----------------
+// Two-wave (pair) column programs (rq_colasm.hpp compile_pair): wave A streams the source rows and runs
+// the forward pass and pushes, wave B the HDPC bit accumulation, dense part and outputs, handed over
+// through an LDS ring.  Taken for the bit-accumulation (SCHED_4R) programs, whose single wave is bound
+// by its in-order issue behind the memory pipeline.  Experiments builds:
+// RQHIP_PAIR=0/1 forces the choice; RQHIP_PAIR_CFG="lag,max_transfer,ring_max".
+struct PairCfg {
+    int mode = 0;  // -1 on where it compiles, 0 off, 1 forced (RQHIP_PAIR)
+    uint32_t lag = 6, xfer = 16, ring = 192;
+};
+const PairCfg& pair_cfg() {
+    static const PairCfg c = [] {
+        PairCfg r;
+        if (const char* e = knob("RQHIP_PAIR")) r.mode = std::atoi(e);
+        if (const char* e = knob("RQHIP_PAIR_CFG")) {
+            unsigned a = 0, b = 0, d = 0;
+            std::sscanf(e, "%u,%u,%u", &a, &b, &d);
+            if (a) r.lag = a;
+            if (b) r.xfer = b;
+            if (d) r.ring = d;
+        }
+        return r;
+    }();
+    return c;
+}
+
+// The program the engine runs for (K', outputs): the single-wave program of compile_colprog, or its
+// pair split when that is chosen.  *use_pair says which; the debug entry points share this choice.
+bool compile_engine_program(const Params& p, const uint32_t* esi, uint32_t n_esi, const AllocOpts& ao,
+                            bool search_waves, ColIR* ir, MProg* mp, PairProg* pp, bool* use_pair, std::string* err) {
+    uint32_t passes = 0;
+    *use_pair = false;
+    if (!compile_colprog(p, esi, n_esi, ao, ir, mp, err, &passes, search_waves)) return false;
+    const PairCfg& c = pair_cfg();
+    if (!esi || c.mode == 0 || !(passes & SCHED_4R)) return true;  // (mode 1 also needs the 4R schedule)
+    std::string e2;
+    if (!compile_pair(*ir, ao, /*B: grp 1 and 3*/ 0xA, c.lag, c.xfer, c.ring, pp, &e2)) {
+        if (c.mode == 1) {
+            if (err) *err = e2;
+            return false;
+        }
+        return true;
+    }
+    *use_pair = true;
+    return true;
+}
+
 // Compile (once per device and (K', K, outputs)) the straight-line gfx950 program for the given
 // outputs: IR (rq_colprog.cpp) -> registers/scratch (rq_colasm.cpp) -> assembly -> code object
 // (amd_comgr, in process) -> hipModuleLoadData, or take the code object from the disk cache.
@@ -523,28 +570,38 @@ int get_col_kernel(DevCtx* ctx, const Params& p, const uint32_t* esi, uint32_t n
             ColIR ir;
             std::string err;
             MProg mp;
+            PairProg pp;
+            bool pair = false;
             const bool search_waves = !knob("RQHIP_ALLOC");  // experiments: the given budget as is
-            if (!compile_colprog(p, all_C ? nullptr : esi, n_esi, ao, &ir, &mp, &err, nullptr, search_waves)) {
+            if (!compile_engine_program(p, all_C ? nullptr : esi, n_esi, ao, search_waves, &ir, &mp, &pp, &pair, &err)) {
                 ctx->colk.erase(key);
                 return fail(RQ_ERR_PLAN, err);
             }
             // distinct symbol per program so kernel traces separate encode, decode and C programs
-            kname = "rq_colprog_K" + std::to_string(p.K) + (all_C ? "_C" : "_n" + std::to_string(n_esi));
-            const uint32_t wpc = colprog_launch_shape(&mp);
+            kname = "rq_colprog_K" + std::to_string(p.K) + (all_C ? "_C" : "_n" + std::to_string(n_esi)) + (pair ? "_pair" : "");
+            uint32_t wpc = 0;
             co.clear();
-            if (!comgr_assemble(emit_colprog_asm(mp, kname), &co, &err)) { ctx->colk.erase(key); return fail(RQ_ERR_PLAN, err); }
+            if (pair) {
+                wpc = 4;  // two workgroups of two 512-register waves per CU (pair_lds_bytes <= 80 KiB)
+                if (!comgr_assemble(emit_pair_asm(pp, kname), &co, &err)) { ctx->colk.erase(key); return fail(RQ_ERR_PLAN, err); }
+            } else {
+                wpc = colprog_launch_shape(&mp);
+                if (!comgr_assemble(emit_colprog_asm(mp, kname), &co, &err)) { ctx->colk.erase(key); return fail(RQ_ERR_PLAN, err); }
+            }
+            const MProg& lead = pair ? pp.A : mp;  // the wave that loads the source rows
             std::memset(&ch, 0, sizeof ch);
             ch.waves_per_cu = wpc;
             std::memcpy(ch.magic, CACHE_MAGIC, 8);
-            k->src_rows = colprog_src_rows(mp);
+            k->src_rows = colprog_src_rows(lead);
             ch.n_rows = (uint32_t)k->src_rows.size();
             ch.n_out = ir.n_out;
-            ch.n_slots = mp.n_slots;
-            ch.n_ins = (uint32_t)mp.ins.size();
-            ch.wg_waves = mp.wg_waves;
+            ch.n_slots = lead.n_slots;
+            ch.n_ins = (uint32_t)(pair ? pp.A.ins.size() + pp.B.ins.size() : mp.ins.size());
+            ch.wg_waves = pair ? 2 : mp.wg_waves;
+            ch.flags = pair ? 1u : 0u;
             ch.name_len = (uint32_t)kname.size();
             ch.co_len = co.size();
-            ch.st = mp.st;
+            ch.st = lead.st;
             ch.body_hash = cache_body_hash(kname, co, k->src_rows);
             if (hipModuleLoadData(&k->mod, co.data()) != hipSuccess ||
                 hipModuleGetFunction(&k->fn, k->mod, kname.c_str()) != hipSuccess) {
@@ -557,6 +614,7 @@ int get_col_kernel(DevCtx* ctx, const Params& p, const uint32_t* esi, uint32_t n
         k->n_slots = ch.n_slots;
         k->waves_per_cu = ch.waves_per_cu;
         k->wg_waves = std::max<uint32_t>(1, ch.wg_waves);
+        k->pair = (ch.flags & 1u) != 0;
         k->st = ch.st;
         k->n_ins = ch.n_ins;
         slot = std::move(k);
@@ -589,8 +647,9 @@ int launch_col(DevCtx* ctx, ColKernel* k, uint32_t T, uint32_t n_blocks, const v
         return fail(RQ_ERR_UNSUPPORTED, "block stride beyond the 4 GiB buffer-offset range");
     if ((uint64_t)per * Td > 0x7FFFFFFFull) return fail(RQ_ERR_UNSUPPORTED, "batch too large");
     const uint32_t Wg = k->wg_waves;
+    const uint32_t Wi = k->pair ? 1u : Wg;  // items per workgroup iteration (a pair's two waves share one)
     const uint32_t max_items = (uint32_t)(((uint64_t)per * Td + 63) / 64);
-    const uint32_t max_iters = (max_items + Wg - 1) / Wg;  // workgroup iterations
+    const uint32_t max_iters = (max_items + Wi - 1) / Wi;  // workgroup iterations
     // persistent grid: at most the resident workgroup count (scratch is per grid wave; RQHIP_WAVES caps
     // the waves in experiments builds)
     static const uint32_t cap = [] { const char* e = knob("RQHIP_WAVES"); return e ? (uint32_t)std::atoi(e) : 0u; }();
@@ -600,7 +659,7 @@ int launch_col(DevCtx* ctx, ColKernel* k, uint32_t T, uint32_t n_blocks, const v
     const size_t spw = (size_t)std::max<uint32_t>(k->n_slots, 1) * 256;
     int rc;
     Workspace* w = ctx->wsp(stream);
-    if ((rc = w->scratch.ensure(spw * max_wg * Wg))) return rc;
+    if ((rc = w->scratch.ensure(spw * max_wg * Wi))) return rc;  // a pair's wave A alone uses scratch
     auto& tab = k->row_off[T];
     if (!tab) {  // once per (program, T): the source loads' soffsets, padded to whole 16-entry groups
         std::unique_ptr<DevBuf> b(new DevBuf());
@@ -629,7 +688,7 @@ int launch_col(DevCtx* ctx, ColKernel* k, uint32_t T, uint32_t n_blocks, const v
         if (!divmagic(Td, a.n_cols, &a.magic, &a.shift)) return fail(RQ_ERR_UNSUPPORTED, "no division magic");
         size_t sz = sizeof a;
         void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
-        const uint32_t items = (a.n_cols + 63) / 64, iters = (items + Wg - 1) / Wg;
+        const uint32_t items = (a.n_cols + 63) / 64, iters = (items + Wi - 1) / Wi;
         // Balanced rounds: as many workgroups as spread the iterations evenly over the rounds the
         // resident set needs (a multiple of 8 for the XCD remap), not the whole resident set with a
         // partial last round -- 1024 blocks K=1024 = 4 800 items: 960 waves x 5 instead of 704 x 5 +
@@ -672,34 +731,11 @@ int encode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, c
     return launch_col(ctx, k, T, n_blocks, src, src_stride, out, out_stride, stream);
 }
 
-// Decode output set: every candidate repair ESI the batch holds.  A dense range [K, K+R) (R a
+// Decode output set (decode_pass): every candidate repair ESI the batch holds.  A dense range [K, K+R) (R a
 // multiple of 4) when the received ESIs are not too sparse -- one compiled program then serves
 // every erasure pattern of that range, and when the highest ESI received is the sender's last
 // (N - 1, N - K a multiple of 4) it is the sender's own encode program -- otherwise the exact
 // sorted set.
-std::vector<uint32_t> decode_union(uint32_t K, const std::vector<uint32_t>& rep) {
-    std::vector<uint32_t> u;
-    if (rep.empty()) return u;
-    const uint32_t mx = *std::max_element(rep.begin(), rep.end());
-    if ((uint64_t)mx - K < (1u << 22)) {  // presence map: O(n), no sort of the per-block lists
-        std::vector<uint8_t> seen((size_t)(mx - K) + 1, 0);
-        for (uint32_t e : rep) seen[e - K] = 1;
-        for (size_t i = 0; i < seen.size(); ++i)
-            if (seen[i]) u.push_back(K + (uint32_t)i);
-    } else {
-        u = rep;
-        std::sort(u.begin(), u.end());
-        u.erase(std::unique(u.begin(), u.end()), u.end());
-    }
-    const uint64_t span = ((uint64_t)u.back() - K + 4) & ~(uint64_t)3;
-    if (span <= 4 * u.size() + 64) {
-        std::vector<uint32_t> r((size_t)span);
-        for (uint32_t i = 0; i < span; ++i) r[i] = K + i;
-        return r;
-    }
-    return u;
-}
-
 // Coefficients of every output over the source rows: the program on the identity payload.
 int ensure_mrep(DevCtx* ctx, ColKernel* k, void* stream) {
     if (k->mrep_stride) return RQ_OK;
@@ -787,71 +823,112 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     uint32_t max_e = 0, max_lds_e = 0;
     bool need_general = false;  // some block may reach the general solver (e or candidates > 64)
     bool wide = false;          // some block has 64 < e <= 128
-    std::vector<uint32_t> cand;
-    std::vector<uint32_t> xoff(nw), goff(nw);
+    // Host work per call is bounded: per-thread scratch keeps its capacity between
+    // calls (nothing is cached across calls -- a receiver sees a new erasure pattern per batch), the
+    // union comes from a presence map with a direct ESI -> union-index table, and the descriptor words
+    // are written once, straight into the pinned staging the upload reads.
+    static thread_local std::vector<uint32_t> xoff, goff, uni, upos;
+    static thread_local std::vector<uint8_t> seen;
+    xoff.resize(nw);
+    goff.resize(nw);
     uint64_t xo = 0, go = 0;
+    uint32_t mx = 0, mn = 0xFFFFFFFFu;
+    size_t n_cand = 0, nz = 0;
     for (uint32_t bi = 0; bi < nw; ++bi) {
         const uint32_t b = blk_map[bi], e = eoff[b + 1] - eoff[b];
         max_e = std::max(max_e, e);
         if (e <= lds_e_max()) max_lds_e = std::max(max_lds_e, e);
         need_general |= (e > 64 || cnt[b] > std::min<uint32_t>(64, e + solve_row_margin()));
         wide |= (e > 64 && e <= 128);
-        cand.insert(cand.end(), repair_esi + roff[b], repair_esi + roff[b] + cnt[b]);
+        for (uint32_t i = roff[b]; i < roff[b] + cnt[b]; ++i) {
+            mx = std::max(mx, repair_esi[i]);
+            mn = std::min(mn, repair_esi[i]);
+        }
+        n_cand += cnt[b];
+        nz += e;
         xoff[bi] = (uint32_t)xo;
         xo += ((uint64_t)e * x_stride(e) + 63) / 64;
         goff[bi] = (uint32_t)go;
         if (e > lds_e_max()) go += (solve_ws_bytes(e) + 63) / 64;
     }
     if (xo >= (1ull << 32) || go >= (1ull << 32)) return fail(RQ_ERR_UNSUPPORTED, "decode workspace beyond 256 GiB");
-    const std::vector<uint32_t> uni = decode_union(p.K, cand);
+    // the union of the candidate repair ESIs (the rule above: a dense [K, K+R) range when the set is not
+    // too sparse, else the exact sorted set)
+    const uint32_t K = p.K;
+    const bool mapped = n_cand && (uint64_t)mx - K < (1u << 22);
+    uni.clear();
+    if (mapped) {
+        seen.assign((size_t)(mx - K) + 1, 0);
+        for (uint32_t b : blk_map)
+            for (uint32_t i = roff[b]; i < roff[b] + cnt[b]; ++i) seen[repair_esi[i] - K] = 1;
+        for (size_t i = 0; i < seen.size(); ++i)
+            if (seen[i]) uni.push_back(K + (uint32_t)i);
+    } else {
+        for (uint32_t b : blk_map) uni.insert(uni.end(), repair_esi + roff[b], repair_esi + roff[b] + cnt[b]);
+        std::sort(uni.begin(), uni.end());
+        uni.erase(std::unique(uni.begin(), uni.end()), uni.end());
+    }
+    if (!uni.empty()) {
+        const uint64_t span = ((uint64_t)uni.back() - K + 4) & ~(uint64_t)3;
+        if (span <= 4 * uni.size() + 64) {
+            uni.resize((size_t)span);
+            for (uint32_t i = 0; i < span; ++i) uni[i] = K + i;
+        }
+    }
+    (void)mn;
     ColKernel* k;
     if ((rc = get_col_kernel(ctx, p, uni.data(), (uint32_t)uni.size(), false, &k))) return rc;
     if ((rc = ensure_mrep(ctx, k, stream))) return rc;
-    // union index of every candidate repair: direct for a dense union, binary search otherwise
+    // union index of every candidate repair: direct for a dense union, a table for a mapped one,
+    // binary search otherwise
     const bool dense_uni = uni.back() - uni.front() + 1 == uni.size();
+    if (!dense_uni && mapped) {
+        upos.assign((size_t)(mx - K) + 1, 0);
+        for (uint32_t j = 0; j < uni.size(); ++j) upos[uni[j] - K] = j;
+    }
     const size_t n_er = eoff[n_blocks], n_rep = roff[n_blocks];
     // index workspace: blk_map | eoff | roff | cnt | erased | rep_uidx | status | xoff | goff
     // [| pack list (blk, row): host-memory decodes only]
-    std::vector<uint32_t> idx;
-    idx.reserve(nw * 3 + 3 * (n_blocks + 1) + n_er * (po ? 3 : 1) + n_rep + n_blocks);
-    const size_t o_map = 0;
-    idx.insert(idx.end(), blk_map.begin(), blk_map.end());
-    const size_t o_eoff = idx.size();
-    idx.insert(idx.end(), eoff.begin(), eoff.end());
-    const size_t o_roff = idx.size();
-    idx.insert(idx.end(), roff.begin(), roff.end());
-    const size_t o_cnt = idx.size();
-    idx.insert(idx.end(), cnt.begin(), cnt.end());
-    const size_t o_er = idx.size();
-    idx.insert(idx.end(), erased, erased + n_er);
-    const size_t o_ru = idx.size();
-    idx.resize(idx.size() + n_rep, 0);
-    for (uint32_t b : blk_map)
-        for (uint32_t i = roff[b]; i < roff[b] + cnt[b]; ++i) {
-            const uint32_t x = repair_esi[i];
-            uint32_t u;
+    const size_t o_map = 0, o_eoff = o_map + nw, o_roff = o_eoff + n_blocks + 1, o_cnt = o_roff + n_blocks + 1,
+                 o_er = o_cnt + n_blocks, o_ru = o_er + n_er, o_st = o_ru + n_rep, o_xo = o_st + n_blocks,
+                 o_go = o_xo + nw, o_zb = o_go + nw;
+    if (!po) nz = 0;
+    const size_t o_zr = o_zb + nz, n_idx = o_zr + nz;
+    auto fill_idx = [&](uint32_t* I) {
+        std::memcpy(I + o_map, blk_map.data(), nw * 4);
+        std::memcpy(I + o_eoff, eoff.data(), (n_blocks + 1) * 4);
+        std::memcpy(I + o_roff, roff.data(), (n_blocks + 1) * 4);
+        std::memcpy(I + o_cnt, cnt.data(), n_blocks * 4);
+        if (n_er) std::memcpy(I + o_er, erased, n_er * 4);
+        if (n_rep) std::memset(I + o_ru, 0, n_rep * 4);
+        for (uint32_t b : blk_map) {
+            uint32_t* u = I + o_ru;
+            const uint32_t* x = repair_esi;
+            const uint32_t r0 = roff[b], r1 = roff[b] + cnt[b];
             if (dense_uni) {
-                u = x - uni.front();
+                const uint32_t f = uni.front();
+                for (uint32_t i = r0; i < r1; ++i) u[i] = x[i] - f;
+            } else if (mapped) {
+                for (uint32_t i = r0; i < r1; ++i) u[i] = upos[x[i] - K];
             } else {
-                u = (uint32_t)(std::lower_bound(uni.begin(), uni.end(), x) - uni.begin());
+                for (uint32_t i = r0; i < r1; ++i)
+                    u[i] = (uint32_t)(std::lower_bound(uni.begin(), uni.end(), x[i]) - uni.begin());
             }
-            idx[o_ru + i] = u;
         }
-    const size_t o_st = idx.size();  // device status: host-decided values, ST_PENDING for the rest
-    for (uint32_t b = 0; b < n_blocks; ++b) idx.push_back((uint32_t)status[b]);
-    const size_t o_xo = idx.size();
-    idx.insert(idx.end(), xoff.begin(), xoff.end());
-    const size_t o_go = idx.size();
-    idx.insert(idx.end(), goff.begin(), goff.end());
-    const size_t o_zb = idx.size();
-    uint32_t nz = 0;
-    if (po) {  // recovered rows packed densely for the download, in blk_map order
-        for (uint32_t b : blk_map)
-            for (uint32_t i = eoff[b]; i < eoff[b + 1]; ++i, ++nz) idx.push_back(b);
-        for (uint32_t b : blk_map)
-            for (uint32_t i = eoff[b]; i < eoff[b + 1]; ++i) idx.push_back(erased[i]);
-    }
-    const size_t o_zr = o_zb + nz;
+        // device status: host-decided values, ST_PENDING for the rest
+        std::memcpy(I + o_st, status, n_blocks * 4);
+        std::memcpy(I + o_xo, xoff.data(), nw * 4);
+        std::memcpy(I + o_go, goff.data(), nw * 4);
+        if (po) {  // recovered rows packed densely for the download, in blk_map order
+            uint32_t* zb = I + o_zb;
+            uint32_t* zr = I + o_zr;
+            for (uint32_t b : blk_map)
+                for (uint32_t i = eoff[b]; i < eoff[b + 1]; ++i) {
+                    *zb++ = b;
+                    *zr++ = erased[i];
+                }
+        }
+    };
     // descriptors through pinned staging, without blocking this thread.  (An upload on a copy stream
     // of its own, joined by events, measured 0.25 ms slower per rq_decode_batch_async call, r02u.)
     Workspace* w = ctx->wsp(stream);
@@ -893,11 +970,11 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     // the set's staging and (zero copy / side upload) its device copy were last read by call n - 2's
     // kernels, which precede `up[set]`
     HIP_TRY(hipEventSynchronize(w->up[set]));
-    if ((rc = w->h_idx[set].ensure(idx.size() * 4)) || (rc = w->h_status.ensure((size_t)n_blocks * 4))) return rc;
-    if (w->idx[set].cap < idx.size() * 4 || w->dstatus.cap < (size_t)n_blocks * 4)
+    if ((rc = w->h_idx[set].ensure(n_idx * 4)) || (rc = w->h_status.ensure((size_t)n_blocks * 4))) return rc;
+    if (w->idx[set].cap < n_idx * 4 || w->dstatus.cap < (size_t)n_blocks * 4)
         HIP_TRY(hipStreamSynchronize((hipStream_t)stream));  // realloc: idle
-    if ((rc = w->idx[set].ensure(idx.size() * 4))) return rc;
-    std::memcpy(w->h_idx[set].p, idx.data(), idx.size() * 4);
+    if ((rc = w->idx[set].ensure(n_idx * 4))) return rc;
+    fill_idx(w->h_idx[set].as<uint32_t>());
     const uint32_t* di;
     int32_t* dst_status;
     // An error return after the side copy is queued must still leave `up[set]` behind that copy (and
@@ -916,7 +993,7 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     } up_guard{w, (hipStream_t)stream, set, false};
     if (side) {
         if ((rc = w->dstatus.ensure((size_t)n_blocks * 4))) return rc;
-        HIP_TRY(hipMemcpyAsync(w->idx[set].p, w->h_idx[set].p, idx.size() * 4, hipMemcpyHostToDevice, w->cs));
+        HIP_TRY(hipMemcpyAsync(w->idx[set].p, w->h_idx[set].p, n_idx * 4, hipMemcpyHostToDevice, w->cs));
         up_guard.armed = true;
         HIP_TRY(hipEventRecord(w->cpy[set], w->cs));
         di = w->idx[set].as<uint32_t>();
@@ -926,7 +1003,7 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
         di = static_cast<const uint32_t*>(w->h_idx[set].p);
         dst_status = w->dstatus.as<int32_t>();  // the host-decided statuses: copied by the first solver
     } else {
-        HIP_TRY(hipMemcpyAsync(w->idx[set].p, w->h_idx[set].p, idx.size() * 4, hipMemcpyHostToDevice,
+        HIP_TRY(hipMemcpyAsync(w->idx[set].p, w->h_idx[set].p, n_idx * 4, hipMemcpyHostToDevice,
                                (hipStream_t)stream));
         HIP_TRY(hipEventRecord(w->up[set], (hipStream_t)stream));
         di = w->idx[set].as<uint32_t>();
@@ -1635,11 +1712,56 @@ int rq_debug_colprog_assemble(uint32_t K, const uint32_t* esi, uint32_t n_out, s
     ColIR ir;
     std::string err;
     MProg mp;
-    if (!debug_compile(p, esi, n_out, alloc_options(), &ir, &mp, &err)) return fail(RQ_ERR_PLAN, err);
-    (void)colprog_launch_shape(&mp);
     std::vector<char> co;
+    if (g_debug_passes < 0) {  // the kernel the engine would build: the pair split where it is chosen
+        PairProg pp;
+        bool pair = false;
+        if (!compile_engine_program(p, esi, n_out, alloc_options(), true, &ir, &mp, &pp, &pair, &err))
+            return fail(RQ_ERR_PLAN, err);
+        if (pair) {
+            if (!comgr_assemble(emit_pair_asm(pp, "rq_colprog_pair"), &co, &err)) return fail(RQ_ERR_PLAN, err);
+            if (code_bytes) *code_bytes = co.size();
+            return RQ_OK;
+        }
+    } else if (!debug_compile(p, esi, n_out, alloc_options(), &ir, &mp, &err)) {
+        return fail(RQ_ERR_PLAN, err);
+    }
+    (void)colprog_launch_shape(&mp);
     if (!comgr_assemble(emit_colprog_asm(mp, "rq_colprog"), &co, &err)) return fail(RQ_ERR_PLAN, err);
     if (code_bytes) *code_bytes = co.size();
+    return RQ_OK;
+}
+
+int rq_debug_pair_emulate(uint32_t K, uint32_t T, const uint32_t* esi, uint32_t n_out, const uint8_t* src,
+                          uint8_t* out, const uint32_t cfg[3], uint32_t stats[16], size_t* code_bytes) {
+    Params p;
+    int rc = params_for_K(K, &p);
+    if (rc) return fail(rc, "k is too big");
+    if (T == 0 || T % 4) return fail(RQ_ERR_BAD_ARG, "T must be a positive multiple of 4");
+    if (!esi || !n_out) return fail(RQ_ERR_BAD_ARG, "pair programs need output ESIs");
+    const PairCfg& c = pair_cfg();
+    const uint32_t lag = cfg && cfg[0] ? cfg[0] : c.lag, xfer = cfg && cfg[1] ? cfg[1] : c.xfer,
+                   ring = cfg && cfg[2] ? cfg[2] : c.ring;
+    ColIR ir;
+    MProg mp;
+    PairProg pp;
+    std::string err;
+    uint32_t passes = 0;
+    if (!compile_colprog(p, esi, n_out, alloc_options(), &ir, &mp, &err, &passes, false)) return fail(RQ_ERR_PLAN, err);
+    if (!compile_pair(ir, alloc_options(), 0xA, lag, xfer, ring, &pp, &err)) return fail(RQ_ERR_PLAN, err);
+    if (src && out && !emulate_pair(pp, src, T, out, &err, 2)) return fail(RQ_ERR_PLAN, err);
+    if (stats) {
+        const uint32_t v[16] = {(uint32_t)pp.A.ins.size(), pp.A.st.valu, pp.A.st.ldsrc, pp.A.st.accw + pp.A.st.accr,
+                                pp.A.st.rst, pp.A.st.bar, (uint32_t)pp.B.ins.size(), pp.B.st.valu, pp.B.st.rld,
+                                pp.B.st.stout, pp.ring, pp.n_xfer, pp.n_cross, pair_lds_bytes(pp), pp.A.n_slots,
+                                (passes & SCHED_4R) ? 1u : 0u};
+        std::memcpy(stats, v, sizeof v);
+    }
+    if (code_bytes) {
+        std::vector<char> co;
+        if (!comgr_assemble(emit_pair_asm(pp, "rq_colprog_pair"), &co, &err)) return fail(RQ_ERR_PLAN, err);
+        *code_bytes = co.size();
+    }
     return RQ_OK;
 }
 

@@ -43,7 +43,7 @@ EXPORTED = (
     "rq_debug_colprog_eval", "rq_debug_colprog_emulate", "rq_debug_colprog_assemble", "rq_debug_decode_margin",
     "rq_decode_blocks_host", "rq_host_alloc", "rq_host_free", "rq_debug_colprog_passes",
     "rq_debug_shard_plan", "rq_debug_virtual_shards", "rq_debug_tuple", "rq_stream_release", "rq_shutdown",
-    "rq_launch_timing", "rq_launch_time",
+    "rq_launch_timing", "rq_launch_time", "rq_debug_pair_emulate",
 )
 
 
@@ -174,6 +174,8 @@ def lib():
             "rq_shutdown": ([], ctypes.c_int),
             "rq_launch_timing": ([ctypes.c_int], ctypes.c_int),
             "rq_launch_time": ([ctypes.POINTER(ctypes.c_double), u32p, ctypes.c_int], ctypes.c_int),
+            "rq_debug_pair_emulate": ([ctypes.c_uint32, ctypes.c_uint32, u32p, ctypes.c_uint32, vp, vp, u32p, u32p,
+                                       ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -272,6 +274,31 @@ def colprog_asm(K, esis):
     buf = ctypes.create_string_buffer(n.value)
     _check(lib().rq_debug_colprog_emulate(K, 4, P32(e), len(e), None, None, None, None, buf, n.value, ctypes.byref(n)))
     return buf.raw[:n.value].decode()
+
+
+PAIR_STATS = ("a_ins", "a_valu", "a_loads", "a_agpr_moves", "a_ring_stores", "a_barriers", "b_ins", "b_valu",
+              "b_ring_loads", "b_stores", "ring", "transfers", "handed", "lds_bytes", "a_scratch_slots", "sched_4r")
+
+
+def pair_emulate(K, T, esis, src=None, cfg=(0, 0, 0), assemble=False):
+    """rq_debug_pair_emulate: the two-wave split of the (K, esis) program, run on the host over two items
+    of one block (src: K*T bytes, or None for statistics only).  Returns (outputs or None, stats dict)."""
+    import numpy as np
+    e = np.asarray(esis, np.uint32)
+    c = np.asarray(cfg, np.uint32)
+    st = np.zeros(16, np.uint32)
+    out = None
+    sp = op = None
+    if src is not None:
+        s = np.ascontiguousarray(np.frombuffer(bytes(src), np.uint8))
+        out = np.zeros(len(esis) * T, np.uint8)
+        sp, op = s.ctypes.data, out.ctypes.data
+    n = ctypes.c_size_t(0)
+    P = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+    _check(lib().rq_debug_pair_emulate(K, T, P(e), len(e), sp, op, P(c), P(st), ctypes.byref(n) if assemble else None))
+    d = dict(zip(PAIR_STATS, (int(x) for x in st)))
+    d["code_bytes"] = n.value
+    return (out.reshape(len(esis), T) if out is not None else None), d
 
 
 def colprog_assemble(K, esis):

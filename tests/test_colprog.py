@@ -141,3 +141,49 @@ def test_every_ir_schedule_matches_oracle(rq, oracle, K, T, nrep, passes):
         ref = enc.gen_symbol(e)
         assert np.array_equal(ir_out[i], ref), (K, passes, e)
         assert np.array_equal(mp_out[i], ref), (K, passes, e)
+
+
+# ---- two-wave (pair) programs: rq_colprog.cpp split_pair + rq_colasm.cpp compile_pair / emulate_pair ----
+@pytest.mark.parametrize("K,T,esis", [
+    (1024, 16, list(range(1024, 1100))),                                  # config 3's encode program
+    (1024, 8, [1024 + i for i in range(0, 160, 2)] + [0, 1023, 7000]),   # a sparse decode union + sources
+    (2048, 8, list(range(2048, 2260))),                                   # config 5's K=2048 shape
+    (1500, 12, list(range(1500, 1658))),
+])
+def test_pair_program_matches_oracle(rq, oracle, K, T, esis):
+    """Wave A (loads, forward pass, pushes) and wave B (HDPC bit accumulation, dense part, outputs) run on
+    the host over two consecutive items, every ring read checked against the barrier intervals; the
+    outputs equal the oracle's symbols, and the kernel assembles."""
+    rng = np.random.default_rng(K + T)
+    data = rng.integers(0, 256, K * T, dtype=np.uint8)
+    out, st = rq.pair_emulate(K, T, esis, data.tobytes(), assemble=(K == 1024 and T == 16))
+    assert st["sched_4r"] == 1
+    assert st["a_barriers"] == st["transfers"] and st["a_ring_stores"] == st["b_ring_loads"] == st["handed"]
+    assert st["b_stores"] <= len(esis) and st["a_loads"] >= K
+    assert st["lds_bytes"] <= 80 * 1024
+    enc = oracle.OracleEncoder(data.tobytes(), T)
+    for i, e in enumerate(esis):
+        assert np.array_equal(out[i], enc.gen_symbol(e)), (K, e)
+    if K == 1024 and T == 16:
+        assert st["code_bytes"] > 0
+
+
+@pytest.mark.parametrize("cfg", [(1, 8, 0), (2, 4, 0), (10, 16, 320), (3, 32, 0)])
+def test_pair_lag_and_transfer_sizes(rq, oracle, cfg):
+    """Other lags / transfer sizes / rings: the same bytes (the ring window check and the barrier
+    intervals hold for each)."""
+    K, T = 1024, 8
+    esis = list(range(K, K + 76))
+    rng = np.random.default_rng(sum(cfg))
+    data = rng.integers(0, 256, K * T, dtype=np.uint8)
+    out, st = rq.pair_emulate(K, T, esis, data.tobytes(), cfg=cfg)
+    enc = oracle.OracleEncoder(data.tobytes(), T)
+    for i, e in enumerate(esis):
+        assert np.array_equal(out[i], enc.gen_symbol(e))
+    assert st["ring"] >= min(cfg[1], 16)
+
+
+def test_pair_ring_too_small_is_refused(rq):
+    """A ring that cannot hold lag + 2 transfers is refused at compile time (never a runtime race)."""
+    with pytest.raises(rq.RaptorQError):
+        rq.pair_emulate(1024, 8, list(range(1024, 1100)), cfg=(8, 16, 40))
