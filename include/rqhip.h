@@ -199,13 +199,14 @@ int rq_debug_colprog_assemble(uint32_t K, const uint32_t* esi, uint32_t n_out, s
 /* The two-wave (pair) split of the output program for (K, esi) -- wave A: source loads, forward pass,
  * pushes; wave B: HDPC bit accumulation, dense part, outputs; an LDS ring between them -- evaluated on
  * the host over two consecutive items of one block (the ring carries across items as on the GPU), every
- * ring read checked against the barrier intervals (tests).  cfg = {lag, max transfer, ring slots}, 0 =
- * the engine's default; stats[16] = A {instructions, VALU, source loads, AGPR moves, ring stores,
- * barriers}, B {instructions, VALU, ring loads, output stores}, ring, transfers, values handed over, LDS
- * bytes per workgroup, A's scratch slots, 1 if the program uses the bit-accumulation schedule.
+ * ring read checked against the barrier intervals (tests).  cfg = {lag, max transfer, ring slots, wave A's
+ * four-row staging quads (UINT32_MAX = none)}, 0 = the engine's default; stats[16] = A {instructions,
+ * VALU, source loads, AGPR moves, ring stores, barriers}, B {instructions, VALU, ring loads, output
+ * stores}, ring, transfers, values handed over, LDS bytes per workgroup, A's four-row DMAs, 1 if the
+ * program uses the bit-accumulation schedule.
  * code_bytes (optional): the kernel assembled in process. */
 int rq_debug_pair_emulate(uint32_t K, uint32_t T, const uint32_t* esi, uint32_t n_out, const uint8_t* src,
-                          uint8_t* out, const uint32_t cfg[3], uint32_t stats[16], size_t* code_bytes);
+                          uint8_t* out, const uint32_t cfg[4], uint32_t stats[16], size_t* code_bytes);
 /* Synchronous decodes first solve each block on its first e + margin received repairs (default 8)
  * and re-solve on all of them only if that subset is rank-deficient.  Sets the margin (tests force
  * the second pass with 0) and returns the previous one.  Results never depend on it. */

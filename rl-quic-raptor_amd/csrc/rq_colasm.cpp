@@ -30,6 +30,13 @@ struct Allocator {
     std::vector<int32_t> lslot;                     // value -> LDS slot with a valid copy or -1
     std::vector<uint8_t> issued;                    // LOAD value already issued
     std::vector<uint64_t> dma_seq;                  // LOAD value staged in LDS by DMA: its vmem seq
+    // four-row staging: quads of LDS slots [slot0 + 4q, +4), rows still to be read per quad, free quads,
+    // the next group and its table read (lgkm seq)
+    uint32_t slot0 = 0;
+    std::vector<uint32_t> quad_left;
+    std::deque<uint32_t> free_quads;
+    uint32_t gj = 0;
+    uint64_t tseq = 0;
     int32_t owner[512];
     uint64_t inflight[512];                         // vector-memory load into the register (seq) or 0
     uint64_t linflight[512];                        // LDS load into the register (lgkm seq) or 0
@@ -251,7 +258,12 @@ struct Allocator {
     }
     void free_lds(uint32_t v) {
         lds_res.erase({nu(v), v});
-        free_lslots.push_back(lslot[v]);
+        if (o.dma4 && (uint32_t)lslot[v] >= slot0) {  // a staged row read: its quad frees with its last row
+            const uint32_t q = ((uint32_t)lslot[v] - slot0) / 4;
+            if (--quad_left[q] == 0) free_quads.push_back(q);
+        } else {
+            free_lslots.push_back(lslot[v]);
+        }
         lslot[v] = -1;
     }
     void reload_into(uint32_t v, int r) {
@@ -349,7 +361,10 @@ struct Allocator {
         reg.assign(nv, -1);
         slot.assign(nv, -1);
         lslot.assign(nv, -1);
-        for (int s = (int)o.n_lds - 1; s >= 0; --s) free_lslots.push_back(s);
+        slot0 = o.dma4 ? o.n_lds - 4 * o.dma4 : o.n_lds;  // quads at the top of the LDS budget
+        for (int s = (int)slot0 - 1; s >= 0; --s) free_lslots.push_back(s);
+        quad_left.assign(o.dma4, 0);
+        for (uint32_t q = 0; q < o.dma4; ++q) free_quads.push_back(q);
         issued.assign(nv, 0);
         dma_seq.assign(nv, 0);
         for (int r = 0; r < 512; ++r) { owner[r] = -1; inflight[r] = 0; linflight[r] = 0; pinned[r] = 0; last_accw[r] = -100; }
@@ -364,10 +379,57 @@ struct Allocator {
         mp->n_out = ir.n_out;
         mp->K = ir.p.K;
 
+        std::vector<uint32_t> ld;  // loads with uses, in order: the four-row groups' rows
+        for (uint32_t v : loads)
+            if (!uses[v].empty()) ld.push_back(v);
+        size_t lq = 0;  // next load not yet put in a group
+        if (o.dma4) {
+            mp->dma4_quads = o.dma4;
+            mp->dma4_slot0 = slot0;
+            mp->n_lds_slots = std::max<uint32_t>(mp->n_lds_slots, o.n_lds);
+            if (!ld.empty()) {  // the first group's table read; each DMA then reads the next group's
+                tseq = issue_lgkm();
+                emit(MI_DMAT, 0, -1, -1, -1, 0);
+            }
+        }
         for (uint32_t i = 0; i < nv && !failed; ++i) {
             cur = i;
+            // -- four-row staging far ahead: one buffer_load_dwordx4 ... lds per group of four rows
+            while (o.dma4 && lq < ld.size() && ld[lq] <= i + o.la_dma) {
+                if (free_quads.empty() || seq - retired >= o.max_vmem) break;
+                size_t j = lq;
+                std::vector<uint32_t> g;
+                while (j < ld.size() && g.size() < 4) {
+                    if (!issued[ld[j]]) g.push_back(ld[j]);
+                    ++j;
+                }
+                lq = j;
+                if (g.empty()) break;
+                wait_lseq(tseq);  // this group's row offsets are in the table VGPR
+                const uint32_t q = free_quads.front();
+                free_quads.pop_front();
+                const uint64_t sq = issue_vmem();
+                emit(MI_DMA4, (int)q, -1, -1, -1, gj);
+                mp->st.dma++;
+                for (uint32_t k = 0; k < 4; ++k)
+                    mp->dma4_rows.push_back(ir.nodes[g[k < g.size() ? k : 0]].imm);
+                quad_left[q] = (uint32_t)g.size();
+                for (size_t k = 0; k < g.size(); ++k) {
+                    const uint32_t v = g[k];
+                    lslot[v] = (int32_t)(slot0 + 4 * q + k);
+                    dma_seq[v] = sq;
+                    issued[v] = 1;
+                    mp->st.ldsrc++;
+                    reload_q.push({nu(v), v});
+                }
+                ++gj;
+                if (lq < ld.size()) {  // the next group's table read, into the other table VGPR
+                    tseq = issue_lgkm();
+                    emit(MI_DMAT, (int)(gj & 1), -1, -1, -1, gj);
+                }
+            }
             // -- stage source rows in LDS by DMA far ahead (no register held while in flight)
-            while (o.la_dma && dp < loads.size() && loads[dp] <= i + o.la_dma) {
+            while (!o.dma4 && o.la_dma && dp < loads.size() && loads[dp] <= i + o.la_dma) {
                 const uint32_t v = loads[dp];
                 if (issued[v] || uses[v].empty()) { ++dp; continue; }
                 if (seq - retired >= o.max_vmem) break;
@@ -652,9 +714,14 @@ static uint32_t diag_mask() {
     return e ? (uint32_t)std::atoi(e) : 0u;
 }
 
+// First AGPR in the unified register file: above the allocatable VGPRs and the reserved ones (four more
+// with four-row staging -- they must not alias an AGPR).
+uint32_t colprog_acc_off(const MProg& mp) {
+    return (mp.n_vgpr + (mp.dma4_quads ? N_RESERVED_DMA4 : N_RESERVED) + 3) & ~3u;
+}
+
 uint32_t colprog_regs(const MProg& mp) {
-    const uint32_t acc_off = (mp.n_vgpr + N_RESERVED + 3) & ~3u;
-    return (acc_off + std::max<uint32_t>(mp.n_agpr, 1) + 7) & ~7u;
+    return (colprog_acc_off(mp) + std::max<uint32_t>(mp.n_agpr, 1) + 7) & ~7u;
 }
 
 // SGPR map of the emitted kernel beyond the prologue's s0..s55: s56..s63 scratch soffset bases,
@@ -669,6 +736,14 @@ std::vector<uint32_t> colprog_src_rows(const MProg& mp) {
     for (const MInst& m : mp.ins)
         if (m.op == MI_LDSRC) rows.push_back((diag & 16) ? (uint32_t)(rows.size() % mp.K) : m.imm);
     return rows;
+}
+
+uint32_t colprog_row_end(const MProg& mp) {
+    uint32_t e = 1;
+    for (const MInst& m : mp.ins)
+        if (m.op == MI_LDSRC || m.op == MI_DMA) e = std::max(e, m.imm + 1);
+    for (uint32_t r : mp.dma4_rows) e = std::max(e, r + 1);
+    return e;
 }
 
 // Scratch slot s sits at soffset 4096 * (s / 16) + offset (s % 16) * 256: soffset 0 or one of
@@ -821,11 +896,31 @@ static void emit_colprog_body(const MProg& mp, uint32_t W, std::string& s) {
                 std::snprintf(buf, sizeof buf, "s_waitcnt vmcnt(%u)", m.imm); line(buf); break;
             case MI_NOP:
                 std::snprintf(buf, sizeof buf, "s_nop %u", m.imm); line(buf); break;
+            case MI_DMAT: {  // row offsets of group imm for this lane's row group (table at LDS 0), all lanes
+                line("s_mov_b64 exec, -1");
+                std::snprintf(buf, sizeof buf, "ds_read_b32 v%d, v%d offset:%u", m.d ? rv.tbl1 : rv.tbl0, rv.grp4,
+                              m.imm * 16u);
+                line(buf);
+                line("s_mov_b64 exec, s[22:23]");
+                break;
+            }
+            case MI_DMA4: {  // lane l: 16 B of row (l / 16) of the group at its chunk base -> quad d, all lanes
+                const int tr = (m.imm & 1u) ? rv.tbl1 : rv.tbl0;
+                line("s_mov_b64 exec, -1");
+                std::snprintf(buf, sizeof buf, "v_add_u32_e32 v%d, v%d, v%d", tr, rv.dmabase, tr); line(buf);
+                std::snprintf(buf, sizeof buf, "s_mov_b32 m0, %u", (mp.lds_base + mp.dma4_slot0 + 4u * (uint32_t)m.d) * 256u);
+                line(buf);
+                line("s_nop 0");
+                std::snprintf(buf, sizeof buf, "buffer_load_dwordx4 v%d, s[24:27], 0 offen lds%s", tr, pol.src.c_str());
+                line(buf);
+                line("s_mov_b64 exec, s[22:23]");
+                break;
+            }
             case MI_LDST:
-            case MI_RST: {  // spill slots sit after the ring (lds_base); ring slots from 0
+            case MI_RST: {  // spill slots sit after the ring (lds_base); ring slots after the group table
                 if (diag & 2 && m.op == MI_LDST) break;
                 int vb;
-                const uint32_t off = lds_at(m.op == MI_RST ? m.imm : m.imm + mp.lds_base, &vb);
+                const uint32_t off = lds_at(m.op == MI_RST ? m.imm + mp.ring_base : m.imm + mp.lds_base, &vb);
                 std::snprintf(buf, sizeof buf, "ds_write_b32 v%d, %s offset:%u", vb, R(m.a), off);
                 line(buf);
                 break;
@@ -834,7 +929,7 @@ static void emit_colprog_body(const MProg& mp, uint32_t W, std::string& s) {
             case MI_RLD: {
                 if (diag & 2 && m.op == MI_LDLD) break;
                 int vb;
-                const uint32_t off = lds_at(m.op == MI_RLD ? m.imm : m.imm + mp.lds_base, &vb);
+                const uint32_t off = lds_at(m.op == MI_RLD ? m.imm + mp.ring_base : m.imm + mp.lds_base, &vb);
                 std::snprintf(buf, sizeof buf, "ds_read_b32 %s, v%d offset:%u", R(m.d), vb, off);
                 line(buf);
                 break;
@@ -848,13 +943,25 @@ static void emit_colprog_body(const MProg& mp, uint32_t W, std::string& s) {
     }
 }
 
+std::vector<uint32_t> colprog_row_table(const MProg& mp, uint32_t T) {
+    const std::vector<uint32_t> rows = colprog_src_rows(mp);
+    std::vector<uint32_t> off((rows.size() + 15) / 16 * 16 + 16, 0);
+    for (size_t j = 0; j < rows.size(); ++j) off[j] = rows[j] * T;
+    for (uint32_t r : mp.dma4_rows) off.push_back(r * T);
+    return off;
+}
+
+uint32_t colprog_dma4_table_offset(const MProg& mp) {
+    return (uint32_t)((colprog_src_rows(mp).size() + 15) / 16 * 16 + 16) * 4u;
+}
+
 std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
     static const Policy pol;
     static const uint32_t diag = diag_mask();
     const Reserved rv(mp.n_vgpr);
     const int V_SCROFF = rv.scroff, V_OUTOFF = rv.outoff, V_SRCOFF = rv.srcoff;
-    const uint32_t acc_off = (mp.n_vgpr + N_RESERVED + 3) & ~3u;        // first AGPR in the unified file
-    const uint32_t n_regs = (acc_off + std::max<uint32_t>(mp.n_agpr, 1) + 7) & ~7u;
+    const uint32_t acc_off = colprog_acc_off(mp);  // first AGPR in the unified file
+    const uint32_t n_regs = colprog_regs(mp);
     std::string s;
     s.reserve(mp.ins.size() * 48 + 8192);
     char buf[256];
@@ -874,7 +981,7 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
         "v_add_u32_e32 V_LDS2, 0x10000, V_SCROFF",
         "s_mov_b32 s24, s4",
         "s_and_b32 s25, s5, 0xffff",
-        "s_mov_b32 s26, -1",
+        "s_mov_b32 s26, s19",
         "s_mov_b32 s27, 0x20000",
         "s_mov_b32 s28, s6",
         "s_and_b32 s29, s7, 0xffff",
@@ -1084,6 +1191,8 @@ struct WaveEmu {
     std::function<bool(uint32_t, const std::vector<uint32_t>&)> ring_store;
     std::function<bool(uint32_t, std::vector<uint32_t>*)> ring_load;
     std::function<void()> barrier;
+    uint64_t tbl_seq[2] = {0, 0};           // four-row staging: the table read into each table VGPR
+    uint32_t tbl_grp[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};
     char buf[200];
 
     WaveEmu(const MProg& m, const uint8_t* s, uint32_t t, uint8_t* o, std::string* e)
@@ -1104,7 +1213,8 @@ struct WaveEmu {
 
     bool step(size_t i, const MInst& m) {
         if (!ready(m.a) || !ready(m.b) || !ready(m.c)) return bad(i, "operand read before its load completed");
-        if (m.op != MI_DMA && m.d >= 0 && !ready(m.d)) return bad(i, "register overwritten while a load into it is pending");
+        if (m.op != MI_DMA && m.op != MI_DMA4 && m.op != MI_DMAT && m.d >= 0 && !ready(m.d))
+            return bad(i, "register overwritten while a load into it is pending");
         switch (m.op) {
             case MI_XOR2:
                 for (uint32_t c = 0; c < Td; ++c) R[m.d][c] = R[m.a][c] ^ R[m.b][c];
@@ -1196,6 +1306,31 @@ struct WaveEmu {
                 if (!barrier) return bad(i, "barrier outside a pair program");
                 barrier();
                 break;
+            case MI_DMAT:
+                if (m.d < 0 || m.d > 1) return bad(i, "table register out of range");
+                if ((size_t)m.imm * 4 + 4 > mp.dma4_rows.size()) return bad(i, "table read beyond the group table");
+                if (++lseq - lretired > 15) return bad(i, "more than 15 LDS operations outstanding");
+                tbl_seq[m.d] = lseq;
+                tbl_grp[m.d] = m.imm;
+                break;
+            case MI_DMA4: {
+                const uint32_t tr = m.imm & 1u;
+                if (tbl_grp[tr] != m.imm) return bad(i, "four-row DMA without its table read");
+                if (tbl_seq[tr] > lretired) return bad(i, "four-row DMA before its table read completed");
+                if (m.d < 0 || (uint32_t)m.d >= mp.dma4_quads) return bad(i, "quad out of range");
+                for (uint32_t g = 0; g < 4; ++g) {
+                    const uint32_t sl = mp.dma4_slot0 + 4u * (uint32_t)m.d + g;
+                    if (sl >= mp.n_lds_slots) return bad(i, "quad slot out of range");
+                    if (lds_dma[sl] > retired) return bad(i, "DMA over a pending DMA");
+                    const uint32_t row = mp.dma4_rows[(size_t)m.imm * 4 + g];
+                    if (row >= mp.K) return bad(i, "source row >= K");
+                    std::memcpy(lds[sl].data(), src + (size_t)row * T, (size_t)Td * 4);
+                }
+                if (!vmem()) return bad(i, "more than 63 vector-memory operations outstanding");
+                for (uint32_t g = 0; g < 4; ++g) lds_dma[mp.dma4_slot0 + 4u * (uint32_t)m.d + g] = seq;
+                tbl_grp[tr] = 0xFFFFFFFFu;  // the add consumed the table register
+                break;
+            }
         }
         if ((m.op == MI_XOR2 || m.op == MI_XOR3 || m.op == MI_XT || m.op == MI_XTX || m.op == MI_ZERO) &&
             (m.d >= REG_A0 || m.a >= REG_A0 || m.b >= REG_A0 || m.c >= REG_A0))
@@ -1246,18 +1381,39 @@ bool compile_pair(const ColIR& ir, const AllocOpts& o, uint32_t bmask, uint32_t 
     AllocOpts ob = o;
     ob.n_lds = std::min<uint32_t>(o.n_lds, 32);
     ob.la_dma = 0;
+    ob.dma4 = 0;
+    if (o.dma4) ob.n_vgpr = std::min<uint32_t>(o.n_vgpr, V_ALLOC - (N_RESERVED_DMA4 - N_RESERVED));  // same reserved VGPRs
     if (!allocate_colprog(px.B, ob, &pp->B, err)) return false;
     if (pp->B.n_slots) {
         if (err) *err = "compile_pair: wave B needs global scratch";
         return false;
     }
     AllocOpts oa = o;
-    oa.n_lds = std::min<uint32_t>(o.n_lds, WG_SLOTS - ring - pp->B.n_lds_slots);
-    oa.la_dma = 0;
+    // four-row staging: the group table (16 B per group; at most one group per load) sits at LDS 0
+    uint32_t n_loads = 0;
+    for (const IrNode& d : px.A.nodes) n_loads += d.k == IR_LOAD;
+    // (groups hold four rows unless rows were already loaded directly: a few more than n_loads / 4)
+    const uint32_t tbl_est = o.dma4 ? ((n_loads + 3) / 4 + 32) * 16 / 256 + 1 : 0;
+    uint32_t quads = o.dma4;
+    while (quads && ring + tbl_est + pp->B.n_lds_slots + 4 * quads + 32 > WG_SLOTS) quads /= 2;  // keep 32 spill slots
+    oa.dma4 = quads;
+    oa.n_lds = std::min<uint32_t>(o.n_lds + 4 * quads, WG_SLOTS - ring - tbl_est - pp->B.n_lds_slots);
+    if (o.dma4) oa.n_vgpr = ob.n_vgpr;  // both waves: the same reserved VGPRs (the prologue sets them once)
+    if (!quads) oa.la_dma = 0;
     if (!allocate_colprog(px.A, oa, &pp->A, err)) return false;
-    pp->A.lds_base = ring;
-    pp->B.lds_base = ring + pp->A.n_lds_slots;
+    if (pp->A.n_vgpr != pp->B.n_vgpr) {
+        if (err) *err = "compile_pair: the waves' register layouts differ";
+        return false;
+    }
+    pp->tbl_slots = (uint32_t)((pp->A.dma4_rows.size() / 4 * 16 + 255) / 256);
+    pp->A.ring_base = pp->B.ring_base = pp->tbl_slots;
+    pp->A.lds_base = pp->tbl_slots + ring;
+    pp->B.lds_base = pp->tbl_slots + ring + pp->A.n_lds_slots;
     pp->A.wg_waves = pp->B.wg_waves = 2;
+    if (pair_lds_bytes(*pp) > WG_SLOTS * 256u) {
+        if (err) *err = "compile_pair: LDS budget";
+        return false;
+    }
     return true;
 }
 
@@ -1268,7 +1424,7 @@ double pair_cost(const PairProg& pp) {
 }
 
 uint32_t pair_lds_bytes(const PairProg& pp) {
-    return (pp.ring + pp.A.n_lds_slots + pp.B.n_lds_slots) * 256u;
+    return (pp.tbl_slots + pp.ring + pp.A.n_lds_slots + pp.B.n_lds_slots) * 256u;
 }
 
 bool emulate_pair(const PairProg& pp, const uint8_t* src, uint32_t T, uint8_t* out, std::string* err, uint32_t iters) {
@@ -1315,8 +1471,9 @@ std::string emit_pair_asm(const PairProg& pp, const std::string& kname) {
     const MProg& A = pp.A;
     const MProg& B = pp.B;
     const Reserved rv(A.n_vgpr);
-    const uint32_t acc_off = (A.n_vgpr + N_RESERVED + 3) & ~3u;
-    const uint32_t n_regs = std::max(colprog_regs(A), colprog_regs(B));
+    // one register layout for both waves: A's reservation (B never stages, but shares A's VGPR count)
+    const uint32_t acc_off = std::max(colprog_acc_off(A), colprog_acc_off(B));
+    const uint32_t n_regs = (acc_off + std::max<uint32_t>(std::max(A.n_agpr, B.n_agpr), 1) + 7) & ~7u;
     std::string s;
     s.reserve((A.ins.size() + B.ins.size()) * 48 + 16384);
     char buf[256];
@@ -1347,7 +1504,7 @@ std::string emit_pair_asm(const PairProg& pp, const std::string& kname) {
         "s_waitcnt lgkmcnt(0)",
         "s_mov_b32 s24, s4",
         "s_and_b32 s25, s5, 0xffff",
-        "s_mov_b32 s26, -1",
+        "s_mov_b32 s26, s19",
         "s_mov_b32 s27, 0x20000",
         "s_mov_b32 s28, s6",
         "s_and_b32 s29, s7, 0xffff",
@@ -1399,12 +1556,33 @@ std::string emit_pair_asm(const PairProg& pp, const std::string& kname) {
         "v_mul_lo_u32 v4, v2, s11",
         "v_add_u32_e32 V_OUTOFF, v4, v3",
     };
+    const bool dma4 = A.dma4_quads > 0;
+    const uint32_t tbl_bytes = (uint32_t)(A.dma4_rows.size() / 4 * 16);
     auto wave = [&](const MProg& mp, const char* tag, bool is_a) {
         s += std::string(".L") + tag + ":\n";
         const uint32_t nb = std::min<uint32_t>(SCR_BASES, mp.n_slots > 16 ? (mp.n_slots - 1) / 16 : 0);
         for (uint32_t j = 0; j < nb; ++j) {
             std::snprintf(buf, sizeof buf, "s_mov_b32 s%u, %u", 56 + j, 4096u * (j + 1));
             line(buf);
+        }
+        if (is_a && dma4) {
+            // four-row staging: the lane group's table offset, and the group table itself into LDS 0
+            // (LDS-DMA, 1 KiB per instruction, bounds-checked at the table's size)
+            std::snprintf(buf, sizeof buf, "s_add_u32 s40, s50, %u", colprog_dma4_table_offset(A)); line(buf);
+            line("s_addc_u32 s41, s51, 0");
+            line("s_and_b32 s41, s41, 0xffff");
+            std::snprintf(buf, sizeof buf, "s_mov_b32 s42, %u", tbl_bytes); line(buf);
+            line("s_mov_b32 s43, 0x20000");
+            line("v_lshlrev_b32_e32 v1, 4, v0");
+            for (uint32_t k = 0; k * 1024 < tbl_bytes; ++k) {
+                if (k) line("v_add_u32_e32 v1, 0x400, v1");
+                std::snprintf(buf, sizeof buf, "s_mov_b32 m0, %u", k * 1024); line(buf);
+                line("s_nop 0");
+                line("buffer_load_dwordx4 v1, s[40:43], 0 offen lds");
+            }
+            line("s_waitcnt vmcnt(0)");
+            std::snprintf(buf, sizeof buf, "v_lshrrev_b32_e32 v%d, 4, v0", rv.grp4); line(buf);
+            std::snprintf(buf, sizeof buf, "v_lshlrev_b32_e32 v%d, 2, v%d", rv.grp4, rv.grp4); line(buf);
         }
         if (!is_a)  // B trails A by `lag` transfers: its first `lag` barriers pair with A's first transfers
             for (uint32_t j = 0; j < pp.lag; ++j) line("s_barrier");
@@ -1416,7 +1594,27 @@ std::string emit_pair_asm(const PairProg& pp, const std::string& kname) {
             for (uint32_t j = 0; j < pp.lag; ++j) line("s_barrier");
         line("s_endpgm");
         s += std::string(".L") + tag + "_body:\n";
-        for (const char* p : iter) put(p);
+        for (const char* p : iter) {
+            if (is_a && dma4 && std::strcmp(p, "v_add_u32_e32 v1, s20, v0") == 0) {
+                // lane l's 16-B chunk: dword columns 4 (l % 16) .. + 3 of the item (T % 16 == 0 keeps a chunk
+                // inside one block); its base offset, 0 (valid memory, unused) beyond the last column.  All
+                // lanes: the staging runs with exec = -1, the item's mask is in s[22:23].
+                line("s_lshr_b32 s21, s12, 2");
+                line("v_and_b32_e32 v1, 15, v0");
+                line("v_lshlrev_b32_e32 v1, 2, v1");
+                line("v_add_u32_e32 v1, s20, v1");
+                line("v_cmp_gt_u32_e64 s[46:47], s13, v1");
+                line("v_mul_hi_u32 v2, v1, s14");
+                line("v_lshrrev_b32_e32 v2, s15, v2");
+                line("v_mul_lo_u32 v3, v2, s21");
+                line("v_sub_u32_e32 v3, v1, v3");
+                line("v_lshlrev_b32_e32 v3, 2, v3");
+                line("v_mul_lo_u32 v4, v2, s10");
+                std::snprintf(buf, sizeof buf, "v_add_u32_e32 v%d, v4, v3", rv.dmabase); line(buf);
+                std::snprintf(buf, sizeof buf, "v_cndmask_b32_e64 v%d, 0, v%d, s[46:47]", rv.dmabase, rv.dmabase); line(buf);
+            }
+            put(p);
+        }
         emit_colprog_body(mp, 1, s);
         line("s_waitcnt lgkmcnt(0)");
         line("s_add_u32 s52, s52, s49");

@@ -33,6 +33,8 @@ enum MOp : uint8_t {
     MI_RST,     // pair programs: ring slot imm <- a (ds_write_b32)
     MI_RLD,     // pair programs: d <- ring slot imm (ds_read_b32)
     MI_BAR,     // pair programs: s_barrier (after an lgkmcnt(0) the allocator emits)
+    MI_DMAT,    // four-row staging: row offsets of group imm -> reserved table VGPR d (ds_read_b32)
+    MI_DMA4,    // four-row staging: the four rows of group imm -> LDS quad d (buffer_load_dwordx4 ... lds)
 };
 
 constexpr int REG_A0 = 256;       // register ids: 0..255 VGPR, 256..511 AGPR
@@ -40,10 +42,14 @@ constexpr int V_ALLOC = 250;      // at most v0..v249 allocatable; 6 reserved VG
 // Reserved VGPRs of a program with n allocatable VGPRs: v(n)..v(n+5).  lds2 = scroff + 64 KiB
 // addresses LDS slots 256.. (the ds offset field is 16 bits).
 constexpr int N_RESERVED = 6;
+// Four-row staging programs reserve four more just above those: the lane group's table offset
+// ((lane / 16) * 4), the lane's 16-B chunk base in the source block, and two table registers.
+constexpr int N_RESERVED_DMA4 = 10;
 struct Reserved {
-    int t2, t1, scroff, outoff, srcoff, lds2;
+    int t2, t1, scroff, outoff, srcoff, lds2, grp4, dmabase, tbl0, tbl1;
     explicit Reserved(uint32_t n)
-        : t2((int)n), t1((int)n + 1), scroff((int)n + 2), outoff((int)n + 3), srcoff((int)n + 4), lds2((int)n + 5) {}
+        : t2((int)n), t1((int)n + 1), scroff((int)n + 2), outoff((int)n + 3), srcoff((int)n + 4), lds2((int)n + 5),
+          grp4((int)n + 6), dmabase((int)n + 7), tbl0((int)n + 8), tbl1((int)n + 9) {}
 };
 
 struct MInst {
@@ -61,6 +67,13 @@ struct AllocOpts {
     uint32_t n_lds = 156;        // LDS spill slots per wave (256 B each; 4 waves/CU -> 40 KB; <= 512)
     uint32_t lds_horizon = 200;  // push an LDS resident out only if its next use is this much further
     uint32_t la_dma = 0;         // look-ahead (IR nodes) for LDS-DMA source staging (0 = off)
+    // Four-row staging (0 = off): source rows go to LDS four at a time, one buffer_load_dwordx4 ... lds
+    // per group of four rows (1 KiB: 16 B per lane, lane group g = lane / 16 on row g), into `dma4`
+    // quads of four LDS slots taken from the top of n_lds, la_dma IR nodes ahead; each row then reaches
+    // a register by ds_read_b32.  Four times the bytes per outstanding vector-memory operation (the
+    // vmcnt budget bounds a wave's bytes in flight).  Needs T and the block stride multiples of 16 and
+    // n_vgpr <= 246 (four more reserved VGPRs).
+    uint32_t dma4 = 0;
     uint32_t src_bias = 100;     // victim choice: a source row's next use counts this % as far
     uint32_t src_lds = 1;        // evicted source rows may take LDS slots (else dropped at once)
     uint32_t wait_age = 320;     // a vmcnt wait also covers operations issued this many instructions ago
@@ -77,6 +90,11 @@ struct MProg {
     uint32_t K = 0;
     uint32_t wg_waves = 1;       // waves per workgroup (emit_colprog_asm): W consecutive items per CU
     uint32_t lds_base = 0;       // LDS slot of the program's spill slot 0 (pair programs: after the ring)
+    uint32_t ring_base = 0;      // LDS slot of ring slot 0 (pair programs: after the four-row table)
+    // four-row staging: quads, the first quad slot (spill slots below it), and the rows of every group
+    // (4 per group, padded with the group's first row)
+    uint32_t dma4_quads = 0, dma4_slot0 = 0;
+    std::vector<uint32_t> dma4_rows;
     struct Stats {
         uint32_t valu = 0, ldsrc = 0, stout = 0, spst = 0, spld = 0, accw = 0, accr = 0, wait = 0, nop = 0;
         uint32_t sync_reload = 0;  // reloads that were not prefetched
@@ -115,7 +133,7 @@ struct ColKernArgs {
     uint32_t magic, shift;  // b = mulhi(g, magic) >> shift == g / (T/4) for g < n_cols
     uint32_t scr_per_wave;  // bytes
     uint32_t xcd_q, xcd_n;  // XCD-aware item order: q = items / 8, n = 8q (0, 0 = identity order)
-    uint32_t pad;
+    uint32_t src_bytes;   // source buffer resource size: the launch's source span (loads beyond it read 0)
     uint32_t n_items;     // workgroup iterations: ceil(64-column items / W) (W = MProg::wg_waves)
     uint32_t n_wg;        // persistent grid size (workgroups): workgroup g takes iterations g, g + n_wg, ...
                           // and its wave w the item iteration * W + w
@@ -127,8 +145,16 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname);
 // Source rows of the program's buffer loads in issue order (the kernel's row_off table is these
 // times T, padded to a multiple of 16 entries).
 std::vector<uint32_t> colprog_src_rows(const MProg& mp);
+// 1 + the largest source row any load of the program reads (the source resource's extent per block).
+uint32_t colprog_row_end(const MProg& mp);
+// The kernel's row-offset buffer for symbol size T: colprog_src_rows * T (padded to 16 entries + 16),
+// then, for four-row staging, every group's four row offsets (dma4_rows * T).  Both waves of a pair
+// read it through the same pointer; colprog_dma4_table_offset is where the group table starts (bytes).
+std::vector<uint32_t> colprog_row_table(const MProg& mp, uint32_t T);
+uint32_t colprog_dma4_table_offset(const MProg& mp);
 // Registers (VGPR + AGPR, allocation granule 8) per lane of the emitted kernel.
 uint32_t colprog_regs(const MProg& mp);
+uint32_t colprog_acc_off(const MProg& mp);
 
 // Executes the machine program on the host for one block (T/4 lanes), checking vmcnt waits and
 // scratch ordering as it goes.  Test infrastructure for the allocator, not a product path.
@@ -139,9 +165,11 @@ struct PairProg {
     MProg A, B;              // wave 0 (A: loads, forward pass, pushes) and wave 1 (B: HDPC, dense, outputs)
     uint32_t lag = 0, ring = 0, n_xfer = 0, n_cross = 0;
     uint32_t bmask = 0;      // IrNode::grp values run by wave B
+    uint32_t tbl_slots = 0;  // four-row staging: LDS slots of A's group table (at LDS 0)
 };
-// Splits and allocates (both waves with the budget of `o`, one wave per SIMD; LDS: the ring, then A's
-// spill slots, then B's; at most 80 KiB per workgroup so that two workgroups share a CU).
+// Splits and allocates (both waves with the budget of `o`, one wave per SIMD; LDS: A's four-row group
+// table, the ring, A's spill slots and quads, B's spill slots; at most 80 KiB per workgroup so that two
+// workgroups share a CU).  o.dma4 / o.la_dma apply to wave A (its source rows staged four at a time).
 bool compile_pair(const ColIR& ir, const AllocOpts& o, uint32_t bmask, uint32_t lag, uint32_t max_xfer, uint32_t ring,
                   PairProg* pp, std::string* err);
 // Model of a pair launch's time per item (issue slots of the longer wave), comparable with

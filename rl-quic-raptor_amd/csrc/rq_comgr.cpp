@@ -3,6 +3,10 @@
 // No subprocess: the library may run inside a process that already owns the GPU.
 #include <amd_comgr/amd_comgr.h>
 
+#include <algorithm>
+#include <cctype>
+#include <cstdlib>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -24,9 +28,48 @@ std::string log_of(amd_comgr_data_set_t set) {
     if (s.size() > 2000) s.resize(2000);
     return s;
 }
+
+// The generated code must stay inside the registers its descriptor allocates: an architectural VGPR
+// at or above .amdhsa_accum_offset is an AGPR of the unified file (silently aliased, not rejected by
+// the assembler), and an AGPR at or above next_free_vgpr - accum_offset is another wave's.
+uint32_t directive(const std::string& src, const char* name) {
+    const size_t at = src.find(name);
+    return at == std::string::npos ? 0u : (uint32_t)std::strtoul(src.c_str() + at + std::strlen(name), nullptr, 10);
+}
+
+bool check_registers(const std::string& src, std::string* msg) {
+    const uint32_t acc = directive(src, ".amdhsa_accum_offset"), total = directive(src, ".amdhsa_next_free_vgpr");
+    if (!acc || !total || acc > total) { *msg += "no register allocation directives"; return false; }
+    const size_t end = src.find(".amdhsa_kernel");
+    auto ident = [](char c) { return std::isalnum((unsigned char)c) || c == '_' || c == '.'; };
+    for (size_t i = 1; i < std::min(end, src.size()); ++i) {
+        const char c = src[i];
+        if ((c != 'v' && c != 'a') || ident(src[i - 1])) continue;
+        size_t j = i + 1;
+        if (j < src.size() && src[j] == '[') ++j;  // v[a:b]: the upper end is checked below
+        if (j >= src.size() || !std::isdigit((unsigned char)src[j])) continue;
+        uint32_t r = (uint32_t)std::strtoul(src.c_str() + j, nullptr, 10);
+        while (j < src.size() && std::isdigit((unsigned char)src[j])) ++j;
+        if (src[i + 1] == '[' && j < src.size() && src[j] == ':') r = (uint32_t)std::strtoul(src.c_str() + j + 1, nullptr, 10);
+        else if (src[i + 1] != '[' && j < src.size() && ident(src[j])) continue;
+        const uint32_t lim = c == 'v' ? acc : total - acc;
+        if (r >= lim) {
+            *msg += std::string("register ") + c + std::to_string(r) + " beyond the allocation (" + std::to_string(lim) + ")";
+            return false;
+        }
+    }
+    return true;
+}
 }  // namespace
 
 bool comgr_assemble(const std::string& src, std::vector<char>* co, std::string* err) {
+    {
+        std::string m = "comgr: ";
+        if (!check_registers(src, &m)) {
+            if (err) *err = m;
+            return false;
+        }
+    }
     amd_comgr_data_t in_d{};
     amd_comgr_data_set_t in{}, reloc{}, exe{};
     amd_comgr_action_info_t ai{};

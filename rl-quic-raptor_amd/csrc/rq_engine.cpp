@@ -90,11 +90,13 @@ struct ColKernel {
     uint32_t waves_per_cu = 4;     // residency of the code object (registers, LDS)
     uint32_t wg_waves = 1;         // waves per workgroup (MProg::wg_waves)
     bool pair = false;             // two-wave program (emit_pair_asm): one item per workgroup iteration
+    std::vector<uint32_t> dma4_rows;  // four-row staging: every group's rows (needs 16-B aligned rows)
     MProg::Stats st{};
     uint64_t last_use = 0;         // LRU clock of the per-device cache
     DevBuf mrep;                   // decode: outputs on the identity payload
     uint32_t mrep_stride = 0;
     std::vector<uint32_t> src_rows;                 // source row of each buffer load, in issue order
+    uint32_t row_end = 1;                           // 1 + the largest source row any load reads
     std::map<uint32_t, std::unique_ptr<DevBuf>> row_off;  // T -> src_rows * T (the kernel's soffsets)
     ~ColKernel() { if (mod) (void)hipModuleUnload(mod); }
 };
@@ -398,11 +400,12 @@ uint64_t library_hash() {
 struct CacheHdr {
     char magic[8];
     uint32_t n_out, n_slots, n_ins, waves_per_cu, name_len, n_rows, wg_waves, flags;  // flags bit 0: pair
+    uint32_t n_dma4, row_end;  // four-row staging rows after the n_rows source-load rows; 1 + largest source row
     uint64_t co_len;
     MProg::Stats st;
     uint64_t body_hash;  // FNV-1a of the name, code object and row table (checked on load)
 };
-constexpr char CACHE_MAGIC[9] = "RQCO0005";
+constexpr char CACHE_MAGIC[9] = "RQCO0007";
 
 uint64_t cache_body_hash(const std::string& name, const std::vector<char>& co, const std::vector<uint32_t>& rows) {
     uint64_t h = fnv1a(name.data(), name.size());
@@ -482,17 +485,20 @@ uint32_t colprog_launch_shape(MProg* mp) {
 struct PairCfg {
     int mode = 0;  // -1 on where it compiles, 0 off, 1 forced (RQHIP_PAIR)
     uint32_t lag = 6, xfer = 16, ring = 192;
+    uint32_t dma4 = 32, la_dma = 1200;  // wave A's four-row staging (quads, look-ahead); 16-B aligned rows only
 };
 const PairCfg& pair_cfg() {
     static const PairCfg c = [] {
         PairCfg r;
         if (const char* e = knob("RQHIP_PAIR")) r.mode = std::atoi(e);
         if (const char* e = knob("RQHIP_PAIR_CFG")) {
-            unsigned a = 0, b = 0, d = 0;
-            std::sscanf(e, "%u,%u,%u", &a, &b, &d);
+            unsigned a = 0, b = 0, d = 0, q = 9999, la = 0;
+            std::sscanf(e, "%u,%u,%u,%u,%u", &a, &b, &d, &q, &la);
             if (a) r.lag = a;
             if (b) r.xfer = b;
             if (d) r.ring = d;
+            if (q != 9999) r.dma4 = q;
+            if (la) r.la_dma = la;
         }
         return r;
     }();
@@ -502,14 +508,18 @@ const PairCfg& pair_cfg() {
 // The program the engine runs for (K', outputs): the single-wave program of compile_colprog, or its
 // pair split when that is chosen.  *use_pair says which; the debug entry points share this choice.
 bool compile_engine_program(const Params& p, const uint32_t* esi, uint32_t n_esi, const AllocOpts& ao,
-                            bool search_waves, ColIR* ir, MProg* mp, PairProg* pp, bool* use_pair, std::string* err) {
+                            bool search_waves, bool aligned16, ColIR* ir, MProg* mp, PairProg* pp, bool* use_pair,
+                            std::string* err) {
     uint32_t passes = 0;
     *use_pair = false;
     if (!compile_colprog(p, esi, n_esi, ao, ir, mp, err, &passes, search_waves)) return false;
     const PairCfg& c = pair_cfg();
     if (!esi || c.mode == 0 || !(passes & SCHED_4R)) return true;  // (mode 1 also needs the 4R schedule)
     std::string e2;
-    if (!compile_pair(*ir, ao, /*B: grp 1 and 3*/ 0xA, c.lag, c.xfer, c.ring, pp, &e2)) {
+    AllocOpts pa = ao;
+    pa.dma4 = aligned16 ? c.dma4 : 0;
+    pa.la_dma = c.la_dma;
+    if (!compile_pair(*ir, pa, /*B: grp 1 and 3*/ 0xA, c.lag, c.xfer, c.ring, pp, &e2)) {
         if (c.mode == 1) {
             if (err) *err = e2;
             return false;
@@ -524,8 +534,11 @@ bool compile_engine_program(const Params& p, const uint32_t* esi, uint32_t n_esi
 // outputs: IR (rq_colprog.cpp) -> registers/scratch (rq_colasm.cpp) -> assembly -> code object
 // (amd_comgr, in process) -> hipModuleLoadData, or take the code object from the disk cache.
 // Caller holds ctx->mu.
-int get_col_kernel(DevCtx* ctx, const Params& p, const uint32_t* esi, uint32_t n_esi, bool all_C, ColKernel** out) {
-    std::string key = std::to_string(p.Kp) + ":" + std::to_string(p.K) + (all_C ? ":C" : ":E");
+// aligned16: every launch of this program has T, the block stride and the base a multiple of 16 bytes
+// (the four-row staging of pair programs reads 16-B chunks); a separate program otherwise.
+int get_col_kernel(DevCtx* ctx, const Params& p, const uint32_t* esi, uint32_t n_esi, bool all_C, ColKernel** out,
+                   bool aligned16 = false) {
+    std::string key = std::to_string(p.Kp) + ":" + std::to_string(p.K) + (all_C ? ":C" : ":E") + (aligned16 ? "a" : "");
     if (!all_C) {
         key.reserve(key.size() + n_esi * 6);
         for (uint32_t i = 0; i < n_esi; ++i) key += "," + std::to_string(esi[i]);
@@ -555,7 +568,14 @@ int get_col_kernel(DevCtx* ctx, const Params& p, const uint32_t* esi, uint32_t n
         CacheHdr ch;
         std::string kname;
         std::vector<char> co;
-        bool cached = !path.empty() && cache_load(path, &ch, &kname, &co, &k->src_rows);
+        std::vector<uint32_t> rows;  // source-load rows, then the four-row groups' rows
+        bool cached = !path.empty() && cache_load(path, &ch, &kname, &co, &rows);
+        if (cached && (size_t)ch.n_rows + ch.n_dma4 == rows.size()) {
+            k->src_rows.assign(rows.begin(), rows.begin() + ch.n_rows);
+            k->dma4_rows.assign(rows.begin() + ch.n_rows, rows.end());
+        } else if (cached) {
+            cached = false;
+        }
         if (cached && (hipModuleLoadData(&k->mod, co.data()) != hipSuccess ||
                        hipModuleGetFunction(&k->fn, k->mod, kname.c_str()) != hipSuccess)) {
             // a cached object the runtime refuses: drop the entry and build the program afresh
@@ -573,7 +593,8 @@ int get_col_kernel(DevCtx* ctx, const Params& p, const uint32_t* esi, uint32_t n
             PairProg pp;
             bool pair = false;
             const bool search_waves = !knob("RQHIP_ALLOC");  // experiments: the given budget as is
-            if (!compile_engine_program(p, all_C ? nullptr : esi, n_esi, ao, search_waves, &ir, &mp, &pp, &pair, &err)) {
+            if (!compile_engine_program(p, all_C ? nullptr : esi, n_esi, ao, search_waves, aligned16, &ir, &mp, &pp, &pair,
+                                        &err)) {
                 ctx->colk.erase(key);
                 return fail(RQ_ERR_PLAN, err);
             }
@@ -593,7 +614,12 @@ int get_col_kernel(DevCtx* ctx, const Params& p, const uint32_t* esi, uint32_t n
             ch.waves_per_cu = wpc;
             std::memcpy(ch.magic, CACHE_MAGIC, 8);
             k->src_rows = colprog_src_rows(lead);
+            k->dma4_rows = lead.dma4_rows;
             ch.n_rows = (uint32_t)k->src_rows.size();
+            ch.n_dma4 = (uint32_t)k->dma4_rows.size();
+            ch.row_end = colprog_row_end(lead);
+            rows = k->src_rows;
+            rows.insert(rows.end(), k->dma4_rows.begin(), k->dma4_rows.end());
             ch.n_out = ir.n_out;
             ch.n_slots = lead.n_slots;
             ch.n_ins = (uint32_t)(pair ? pp.A.ins.size() + pp.B.ins.size() : mp.ins.size());
@@ -602,15 +628,16 @@ int get_col_kernel(DevCtx* ctx, const Params& p, const uint32_t* esi, uint32_t n
             ch.name_len = (uint32_t)kname.size();
             ch.co_len = co.size();
             ch.st = lead.st;
-            ch.body_hash = cache_body_hash(kname, co, k->src_rows);
+            ch.body_hash = cache_body_hash(kname, co, rows);
             if (hipModuleLoadData(&k->mod, co.data()) != hipSuccess ||
                 hipModuleGetFunction(&k->fn, k->mod, kname.c_str()) != hipSuccess) {
                 ctx->colk.erase(key);
                 return fail(RQ_ERR_DEVICE, "hipModuleLoadData/GetFunction failed for the column program");
             }
-            if (!path.empty()) cache_store(path, ch, kname, co, k->src_rows);
+            if (!path.empty()) cache_store(path, ch, kname, co, rows);
         }
         k->n_out = ch.n_out;
+        k->row_end = std::max<uint32_t>(ch.row_end, 1);
         k->n_slots = ch.n_slots;
         k->waves_per_cu = ch.waves_per_cu;
         k->wg_waves = std::max<uint32_t>(1, ch.wg_waves);
@@ -638,6 +665,8 @@ int launch_col(DevCtx* ctx, ColKernel* k, uint32_t T, uint32_t n_blocks, const v
                void* out, uint64_t out_stride, void* stream) {
     if (T < 8 || T % 4) return fail(RQ_ERR_BAD_ARG, "device-resident symbols: T must be a multiple of 4, at least 8");
     if (n_blocks == 0) return RQ_OK;
+    if (!k->dma4_rows.empty() && (T % 16 || src_stride % 16 || (uintptr_t)src % 16))
+        return fail(RQ_ERR_PLAN, "internal: a 16-B staged program launched on unaligned rows");
     const uint32_t Td = T / 4;
     // every buffer offset is 32-bit: split so that each launch spans < 4 GiB per buffer
     const uint64_t lim = 0xFFFFFFFFull - (uint64_t)std::max(k->p.K, k->n_out) * T;
@@ -665,6 +694,7 @@ int launch_col(DevCtx* ctx, ColKernel* k, uint32_t T, uint32_t n_blocks, const v
         std::unique_ptr<DevBuf> b(new DevBuf());
         std::vector<uint32_t> off((k->src_rows.size() + 15) / 16 * 16 + 16, 0);
         for (size_t j = 0; j < k->src_rows.size(); ++j) off[j] = k->src_rows[j] * T;
+        for (uint32_t r : k->dma4_rows) off.push_back(r * T);  // colprog_row_table's layout
         if ((rc = b->ensure(off.size() * 4))) { k->row_off.erase(T); return rc; }
         if (hipMemcpy(b->p, off.data(), off.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
             k->row_off.erase(T);
@@ -680,6 +710,8 @@ int launch_col(DevCtx* ctx, ColKernel* k, uint32_t T, uint32_t n_blocks, const v
         a.out = (uint64_t)(uintptr_t)out + (uint64_t)b0 * out_stride;
         a.scratch = (uint64_t)(uintptr_t)w->scratch.p;
         a.src_stride = (uint32_t)src_stride;
+        // the source resource's size: the launch's rows, so a wrong offset reads 0 instead of faulting
+        a.src_bytes = (uint32_t)std::min<uint64_t>(0xFFFFFFFFull, (uint64_t)(nb - 1) * src_stride + (uint64_t)k->row_end * T);
         a.out_stride = (uint32_t)out_stride;
         a.T = T;
         a.n_cols = nb * Td;
@@ -726,7 +758,8 @@ int encode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, c
                   const uint32_t* esi, uint32_t n_esi, void* out, uint64_t out_stride, void* stream) {
     if (!n_esi || !n_blocks) return RQ_OK;
     ColKernel* k;
-    int rc = get_col_kernel(ctx, p, esi, n_esi, false, &k);
+    const bool a16 = T % 16 == 0 && src_stride % 16 == 0 && (uintptr_t)src % 16 == 0;
+    int rc = get_col_kernel(ctx, p, esi, n_esi, false, &k, a16);
     if (rc) return rc;
     return launch_col(ctx, k, T, n_blocks, src, src_stride, out, out_stride, stream);
 }
@@ -739,7 +772,7 @@ int encode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, c
 // Coefficients of every output over the source rows: the program on the identity payload.
 int ensure_mrep(DevCtx* ctx, ColKernel* k, void* stream) {
     if (k->mrep_stride) return RQ_OK;
-    const uint32_t K = k->p.K, Tid = pad_row(K);
+    const uint32_t K = k->p.K, Tid = (K + 15) & ~15u;  // 16-B rows: every program variant takes them
     std::vector<uint8_t> id((size_t)K * Tid, 0);
     for (uint32_t i = 0; i < K; ++i) id[(size_t)i * Tid + i] = 1;
     DevBuf src;
@@ -877,7 +910,8 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     }
     (void)mn;
     ColKernel* k;
-    if ((rc = get_col_kernel(ctx, p, uni.data(), (uint32_t)uni.size(), false, &k))) return rc;
+    const bool a16 = T % 16 == 0 && data_stride % 16 == 0 && (uintptr_t)data % 16 == 0;
+    if ((rc = get_col_kernel(ctx, p, uni.data(), (uint32_t)uni.size(), false, &k, a16))) return rc;
     if ((rc = ensure_mrep(ctx, k, stream))) return rc;
     // union index of every candidate repair: direct for a dense union, a table for a mapped one,
     // binary search otherwise
@@ -1716,7 +1750,7 @@ int rq_debug_colprog_assemble(uint32_t K, const uint32_t* esi, uint32_t n_out, s
     if (g_debug_passes < 0) {  // the kernel the engine would build: the pair split where it is chosen
         PairProg pp;
         bool pair = false;
-        if (!compile_engine_program(p, esi, n_out, alloc_options(), true, &ir, &mp, &pp, &pair, &err))
+        if (!compile_engine_program(p, esi, n_out, alloc_options(), true, true, &ir, &mp, &pp, &pair, &err))
             return fail(RQ_ERR_PLAN, err);
         if (pair) {
             if (!comgr_assemble(emit_pair_asm(pp, "rq_colprog_pair"), &co, &err)) return fail(RQ_ERR_PLAN, err);
@@ -1733,7 +1767,7 @@ int rq_debug_colprog_assemble(uint32_t K, const uint32_t* esi, uint32_t n_out, s
 }
 
 int rq_debug_pair_emulate(uint32_t K, uint32_t T, const uint32_t* esi, uint32_t n_out, const uint8_t* src,
-                          uint8_t* out, const uint32_t cfg[3], uint32_t stats[16], size_t* code_bytes) {
+                          uint8_t* out, const uint32_t cfg[4], uint32_t stats[16], size_t* code_bytes) {
     Params p;
     int rc = params_for_K(K, &p);
     if (rc) return fail(rc, "k is too big");
@@ -1748,12 +1782,15 @@ int rq_debug_pair_emulate(uint32_t K, uint32_t T, const uint32_t* esi, uint32_t 
     std::string err;
     uint32_t passes = 0;
     if (!compile_colprog(p, esi, n_out, alloc_options(), &ir, &mp, &err, &passes, false)) return fail(RQ_ERR_PLAN, err);
-    if (!compile_pair(ir, alloc_options(), 0xA, lag, xfer, ring, &pp, &err)) return fail(RQ_ERR_PLAN, err);
+    AllocOpts pa = alloc_options();
+    pa.dma4 = !cfg || !cfg[3] ? c.dma4 : cfg[3] == 0xFFFFFFFFu ? 0u : cfg[3];  // wave A's four-row staging
+    pa.la_dma = c.la_dma;
+    if (!compile_pair(ir, pa, 0xA, lag, xfer, ring, &pp, &err)) return fail(RQ_ERR_PLAN, err);
     if (src && out && !emulate_pair(pp, src, T, out, &err, 2)) return fail(RQ_ERR_PLAN, err);
     if (stats) {
         const uint32_t v[16] = {(uint32_t)pp.A.ins.size(), pp.A.st.valu, pp.A.st.ldsrc, pp.A.st.accw + pp.A.st.accr,
                                 pp.A.st.rst, pp.A.st.bar, (uint32_t)pp.B.ins.size(), pp.B.st.valu, pp.B.st.rld,
-                                pp.B.st.stout, pp.ring, pp.n_xfer, pp.n_cross, pair_lds_bytes(pp), pp.A.n_slots,
+                                pp.B.st.stout, pp.ring, pp.n_xfer, pp.n_cross, pair_lds_bytes(pp), pp.A.st.dma,
                                 (passes & SCHED_4R) ? 1u : 0u};
         std::memcpy(stats, v, sizeof v);
     }
