@@ -207,6 +207,13 @@ int rq_debug_colprog_assemble(uint32_t K, const uint32_t* esi, uint32_t n_out, s
  * code_bytes (optional): the kernel assembled in process. */
 int rq_debug_pair_emulate(uint32_t K, uint32_t T, const uint32_t* esi, uint32_t n_out, const uint8_t* src,
                           uint8_t* out, const uint32_t cfg[4], uint32_t stats[16], size_t* code_bytes);
+/* Tests: the single-wave program of (K, esi) re-allocated with four-row staging of its source rows
+ * (`quads` quads of four LDS slots, `la` IR nodes ahead, 0 = the engine's default), evaluated on the
+ * host over one item (T a multiple of 16).  stats[8] = {instructions, VALU, four-row DMAs, global
+ * scratch slots, LDS table slots, LDS slots after them, instructions without staging, 1 if the program
+ * uses the bit-accumulation schedule}.  code_bytes (optional): the kernel assembled in process. */
+int rq_debug_dma4_emulate(uint32_t K, uint32_t T, const uint32_t* esi, uint32_t n_out, const uint8_t* src, uint8_t* out,
+                          uint32_t quads, uint32_t la, uint32_t stats[8], size_t* code_bytes);
 /* Synchronous decodes first solve each block on its first e + margin received repairs (default 8)
  * and re-solve on all of them only if that subset is rank-deficient.  Sets the margin (tests force
  * the second pass with 0) and returns the previous one.  Results never depend on it. */

@@ -665,6 +665,31 @@ bool compile_colprog(const Params& p, const uint32_t* esi, uint32_t n_out, const
     return have;
 }
 
+bool compile_colprog_dma4(const ColIR& ir, const AllocOpts& o, uint32_t quads, uint32_t la, MProg* mp,
+                          std::string* err) {
+    constexpr uint32_t WAVE_SLOTS = 160;  // 40 KiB per one-wave workgroup: four per CU
+    uint32_t n_loads = 0;
+    for (const IrNode& d : ir.nodes) n_loads += d.k == IR_LOAD;
+    const uint32_t tbl_est = ((n_loads + 3) / 4 + 32) * 16 / 256 + 1;
+    if (!quads || tbl_est + 4 * quads + 16 > WAVE_SLOTS) {
+        if (err) *err = "compile_colprog_dma4: LDS budget";
+        return false;
+    }
+    AllocOpts so = o;
+    so.dma4 = quads;
+    so.la_dma = la;
+    so.n_vgpr = std::min<uint32_t>(o.n_vgpr, V_ALLOC - (N_RESERVED_DMA4 - N_RESERVED));
+    so.n_lds = WAVE_SLOTS - tbl_est;  // spill slots, then the quads at the top
+    if (!allocate_colprog(ir, so, mp, err)) return false;
+    mp->lds_base = (uint32_t)((mp->dma4_rows.size() / 4 * 16 + 255) / 256);
+    mp->wg_waves = 1;
+    if (mp->lds_base + mp->n_lds_slots > WAVE_SLOTS) {
+        if (err) *err = "compile_colprog_dma4: LDS budget";
+        return false;
+    }
+    return true;
+}
+
 bool divmagic(uint32_t d, uint32_t limit, uint32_t* magic, uint32_t* shift) {
     if (d == 0) return false;
     for (uint32_t s = 0; s < 32; ++s) {
@@ -955,6 +980,52 @@ uint32_t colprog_dma4_table_offset(const MProg& mp) {
     return (uint32_t)((colprog_src_rows(mp).size() + 15) / 16 * 16 + 16) * 4u;
 }
 
+// Four-row staging, once per wave: the group table (16 B per group: the four rows' offsets row * T)
+// into LDS 0 by LDS-DMA, 1 KiB per instruction, range-checked at the table's size through the VGPR
+// offset; then the lane's table offset (lane group l / 16 reads entry l / 16 of a group).  v0 = lane.
+static void emit_dma4_prologue(const MProg& mp, const Reserved& rv, std::string& s) {
+    char buf[160];
+    auto line = [&](const char* t) { s += '\t'; s += t; s += '\n'; };
+    const uint32_t tbl_bytes = (uint32_t)(mp.dma4_rows.size() / 4 * 16);
+    std::snprintf(buf, sizeof buf, "s_add_u32 s40, s50, %u", colprog_dma4_table_offset(mp)); line(buf);
+    line("s_addc_u32 s41, s51, 0");
+    line("s_and_b32 s41, s41, 0xffff");
+    std::snprintf(buf, sizeof buf, "s_mov_b32 s42, %u", tbl_bytes); line(buf);
+    line("s_mov_b32 s43, 0x20000");
+    line("v_lshlrev_b32_e32 v1, 4, v0");
+    for (uint32_t k = 0; k * 1024 < tbl_bytes; ++k) {
+        if (k) line("v_add_u32_e32 v1, 0x400, v1");
+        std::snprintf(buf, sizeof buf, "s_mov_b32 m0, %u", k * 1024); line(buf);
+        line("s_nop 0");
+        line("buffer_load_dwordx4 v1, s[40:43], 0 offen lds");
+    }
+    line("s_waitcnt vmcnt(0)");
+    std::snprintf(buf, sizeof buf, "v_lshrrev_b32_e32 v%d, 4, v0", rv.grp4); line(buf);
+    std::snprintf(buf, sizeof buf, "v_lshlrev_b32_e32 v%d, 2, v%d", rv.grp4, rv.grp4); line(buf);
+}
+
+// Four-row staging, per item (before the item's column map; v0 = lane, s20 = the item's first column):
+// lane l's 16-B chunk is dword columns 4 (l % 16) .. + 3 of the item (T % 16 == 0 keeps a chunk inside
+// one block); its base offset, 0 (valid memory, unused) beyond the last column.  All lanes: the staging
+// runs with exec = -1, the item's mask is in s[22:23].  Uses v1..v4, s21, s[46:47].
+static void emit_dma4_item_base(const Reserved& rv, std::string& s) {
+    char buf[160];
+    auto line = [&](const char* t) { s += '\t'; s += t; s += '\n'; };
+    line("s_lshr_b32 s21, s12, 2");
+    line("v_and_b32_e32 v1, 15, v0");
+    line("v_lshlrev_b32_e32 v1, 2, v1");
+    line("v_add_u32_e32 v1, s20, v1");
+    line("v_cmp_gt_u32_e64 s[46:47], s13, v1");
+    line("v_mul_hi_u32 v2, v1, s14");
+    line("v_lshrrev_b32_e32 v2, s15, v2");
+    line("v_mul_lo_u32 v3, v2, s21");
+    line("v_sub_u32_e32 v3, v1, v3");
+    line("v_lshlrev_b32_e32 v3, 2, v3");
+    line("v_mul_lo_u32 v4, v2, s10");
+    std::snprintf(buf, sizeof buf, "v_add_u32_e32 v%d, v4, v3", rv.dmabase); line(buf);
+    std::snprintf(buf, sizeof buf, "v_cndmask_b32_e64 v%d, 0, v%d, s[46:47]", rv.dmabase, rv.dmabase); line(buf);
+}
+
 std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
     static const Policy pol;
     static const uint32_t diag = diag_mask();
@@ -1082,6 +1153,8 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
         std::snprintf(buf, sizeof buf, "s_mov_b32 s%u, %u", 56 + j, 4096u * (j + 1));
         line(buf);
     }
+    const bool dma4 = mp.dma4_quads > 0;  // (W = 1 only: compile_colprog_dma4)
+    if (dma4) emit_dma4_prologue(mp, rv, s);
     // Code warm-up (W = 1): the program is ~180 KB of straight-line code that every wave starts at
     // once, and when the previous kernel was not a column program its lines are in neither L2 nor the
     // memory-side cache, so round 1's instruction fetches go to HBM one after another (12-15 us per
@@ -1125,6 +1198,7 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
             std::snprintf(buf, sizeof buf, "s_mul_i32 s39, s39, %u", W); line(buf);
             line("s_add_u32 s39, s39, s53");
         }
+        if (dma4 && l == "v_add_u32_e32 v1, s20, v0") emit_dma4_item_base(rv, s);
         if (W > 1 && l.rfind("v_lshrrev_b32_e32 v0, 2, V_SCROFF", 0) == 0) {  // lane id (V_SCROFF has w * LB)
             line("v_mbcnt_lo_u32_b32 v0, -1, 0");
             line("v_mbcnt_hi_u32_b32 v0, -1, v0");
@@ -1150,7 +1224,7 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
     s += ".Lfunc_end:\n\t.size " + kname + ", .Lfunc_end-" + kname + "\n";
     s += "\t.p2alignl 6, 3212836864\n\t.fill 256, 4, 3212836864\n";
     s += "\t.section .rodata,\"a\",@progbits\n\t.p2align 6, 0x0\n\t.amdhsa_kernel " + kname + "\n";
-    const std::string lds = std::to_string(mp.n_lds_slots * 256u * W);
+    const std::string lds = std::to_string((mp.lds_base + mp.n_lds_slots) * 256u * W);
     s += "\t\t.amdhsa_group_segment_fixed_size " + lds + "\n\t\t.amdhsa_private_segment_fixed_size 0\n";
     s += "\t\t.amdhsa_kernarg_size 80\n\t\t.amdhsa_user_sgpr_count 2\n";
     s += "\t\t.amdhsa_user_sgpr_kernarg_segment_ptr 1\n\t\t.amdhsa_system_sgpr_workgroup_id_x 1\n";
@@ -1557,7 +1631,6 @@ std::string emit_pair_asm(const PairProg& pp, const std::string& kname) {
         "v_add_u32_e32 V_OUTOFF, v4, v3",
     };
     const bool dma4 = A.dma4_quads > 0;
-    const uint32_t tbl_bytes = (uint32_t)(A.dma4_rows.size() / 4 * 16);
     auto wave = [&](const MProg& mp, const char* tag, bool is_a) {
         s += std::string(".L") + tag + ":\n";
         const uint32_t nb = std::min<uint32_t>(SCR_BASES, mp.n_slots > 16 ? (mp.n_slots - 1) / 16 : 0);
@@ -1565,25 +1638,7 @@ std::string emit_pair_asm(const PairProg& pp, const std::string& kname) {
             std::snprintf(buf, sizeof buf, "s_mov_b32 s%u, %u", 56 + j, 4096u * (j + 1));
             line(buf);
         }
-        if (is_a && dma4) {
-            // four-row staging: the lane group's table offset, and the group table itself into LDS 0
-            // (LDS-DMA, 1 KiB per instruction, bounds-checked at the table's size)
-            std::snprintf(buf, sizeof buf, "s_add_u32 s40, s50, %u", colprog_dma4_table_offset(A)); line(buf);
-            line("s_addc_u32 s41, s51, 0");
-            line("s_and_b32 s41, s41, 0xffff");
-            std::snprintf(buf, sizeof buf, "s_mov_b32 s42, %u", tbl_bytes); line(buf);
-            line("s_mov_b32 s43, 0x20000");
-            line("v_lshlrev_b32_e32 v1, 4, v0");
-            for (uint32_t k = 0; k * 1024 < tbl_bytes; ++k) {
-                if (k) line("v_add_u32_e32 v1, 0x400, v1");
-                std::snprintf(buf, sizeof buf, "s_mov_b32 m0, %u", k * 1024); line(buf);
-                line("s_nop 0");
-                line("buffer_load_dwordx4 v1, s[40:43], 0 offen lds");
-            }
-            line("s_waitcnt vmcnt(0)");
-            std::snprintf(buf, sizeof buf, "v_lshrrev_b32_e32 v%d, 4, v0", rv.grp4); line(buf);
-            std::snprintf(buf, sizeof buf, "v_lshlrev_b32_e32 v%d, 2, v%d", rv.grp4, rv.grp4); line(buf);
-        }
+        if (is_a && dma4) emit_dma4_prologue(A, rv, s);
         if (!is_a)  // B trails A by `lag` transfers: its first `lag` barriers pair with A's first transfers
             for (uint32_t j = 0; j < pp.lag; ++j) line("s_barrier");
         s += std::string(".L") + tag + "_loop:\n";
@@ -1595,24 +1650,7 @@ std::string emit_pair_asm(const PairProg& pp, const std::string& kname) {
         line("s_endpgm");
         s += std::string(".L") + tag + "_body:\n";
         for (const char* p : iter) {
-            if (is_a && dma4 && std::strcmp(p, "v_add_u32_e32 v1, s20, v0") == 0) {
-                // lane l's 16-B chunk: dword columns 4 (l % 16) .. + 3 of the item (T % 16 == 0 keeps a chunk
-                // inside one block); its base offset, 0 (valid memory, unused) beyond the last column.  All
-                // lanes: the staging runs with exec = -1, the item's mask is in s[22:23].
-                line("s_lshr_b32 s21, s12, 2");
-                line("v_and_b32_e32 v1, 15, v0");
-                line("v_lshlrev_b32_e32 v1, 2, v1");
-                line("v_add_u32_e32 v1, s20, v1");
-                line("v_cmp_gt_u32_e64 s[46:47], s13, v1");
-                line("v_mul_hi_u32 v2, v1, s14");
-                line("v_lshrrev_b32_e32 v2, s15, v2");
-                line("v_mul_lo_u32 v3, v2, s21");
-                line("v_sub_u32_e32 v3, v1, v3");
-                line("v_lshlrev_b32_e32 v3, 2, v3");
-                line("v_mul_lo_u32 v4, v2, s10");
-                std::snprintf(buf, sizeof buf, "v_add_u32_e32 v%d, v4, v3", rv.dmabase); line(buf);
-                std::snprintf(buf, sizeof buf, "v_cndmask_b32_e64 v%d, 0, v%d, s[46:47]", rv.dmabase, rv.dmabase); line(buf);
-            }
+            if (is_a && dma4 && std::strcmp(p, "v_add_u32_e32 v1, s20, v0") == 0) emit_dma4_item_base(rv, s);
             put(p);
         }
         emit_colprog_body(mp, 1, s);

@@ -187,6 +187,11 @@ bool emulate_pair(const PairProg& pp, const uint8_t* src, uint32_t T, uint8_t* o
 bool comgr_assemble(const std::string& src, std::vector<char>* co, std::string* err);
 
 // magic/shift such that (uint64(g) * magic) >> (32 + shift) == g / d for all g < limit.
+// Re-allocate a single-wave program with four-row staging of its source rows (quads of four LDS slots,
+// la IR nodes ahead): the group table at LDS 0, spill slots after it (lds_base); one wave per workgroup,
+// 16-B aligned rows only.
+bool compile_colprog_dma4(const ColIR& ir, const AllocOpts& o, uint32_t quads, uint32_t la, MProg* mp,
+                          std::string* err);
 bool divmagic(uint32_t d, uint32_t limit, uint32_t* magic, uint32_t* shift);
 
 }  // namespace rq

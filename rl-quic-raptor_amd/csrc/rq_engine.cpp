@@ -468,7 +468,7 @@ uint32_t colprog_wg_waves(uint32_t waves_per_cu, uint32_t lds_per_wave) {
 // Residency (waves per CU, from registers and LDS) of an allocated program; sets its waves per
 // workgroup.  The engine and the debug entry points emit the same code.
 uint32_t colprog_launch_shape(MProg* mp) {
-    const uint32_t regs = colprog_regs(*mp), lds = mp->n_lds_slots * 256u;
+    const uint32_t regs = colprog_regs(*mp), lds = (mp->lds_base + mp->n_lds_slots) * 256u;
     uint32_t w = 4 * std::max<uint32_t>(1, 512 / regs);
     if (lds) w = std::min<uint32_t>(w, 163840u / lds);
     const uint32_t wpc = std::max<uint32_t>(1, std::min<uint32_t>(w, 32));
@@ -507,12 +507,37 @@ const PairCfg& pair_cfg() {
 
 // The program the engine runs for (K', outputs): the single-wave program of compile_colprog, or its
 // pair split when that is chosen.  *use_pair says which; the debug entry points share this choice.
+// Four-row staging in single-wave programs (16-B aligned rows, one-wave-per-SIMD programs): quads and
+// look-ahead; RQHIP_DMA4="quads,lookahead" in experiments builds, off (0 quads) by default.
+struct Dma4Cfg {
+    uint32_t quads = 0, la = 1200;
+};
+const Dma4Cfg& dma4_cfg() {
+    static const Dma4Cfg c = [] {
+        Dma4Cfg r;
+        if (const char* e = knob("RQHIP_DMA4")) {
+            unsigned q = 0, la = 0;
+            const int n = std::sscanf(e, "%u,%u", &q, &la);
+            if (n >= 1) r.quads = q;
+            if (n >= 2 && la) r.la = la;
+        }
+        return r;
+    }();
+    return c;
+}
+
 bool compile_engine_program(const Params& p, const uint32_t* esi, uint32_t n_esi, const AllocOpts& ao,
                             bool search_waves, bool aligned16, ColIR* ir, MProg* mp, PairProg* pp, bool* use_pair,
                             std::string* err) {
     uint32_t passes = 0;
     *use_pair = false;
     if (!compile_colprog(p, esi, n_esi, ao, ir, mp, err, &passes, search_waves)) return false;
+    const Dma4Cfg& d4 = dma4_cfg();
+    if (d4.quads && aligned16 && (passes & SCHED_4R) && mp->wg_waves <= 1) {
+        MProg m4;
+        std::string e2;
+        if (compile_colprog_dma4(*ir, ao, d4.quads, d4.la, &m4, &e2) && m4.n_slots <= mp->n_slots) *mp = std::move(m4);
+    }
     const PairCfg& c = pair_cfg();
     if (!esi || c.mode == 0 || !(passes & SCHED_4R)) return true;  // (mode 1 also needs the 4R schedule)
     std::string e2;
@@ -1763,6 +1788,33 @@ int rq_debug_colprog_assemble(uint32_t K, const uint32_t* esi, uint32_t n_out, s
     (void)colprog_launch_shape(&mp);
     if (!comgr_assemble(emit_colprog_asm(mp, "rq_colprog"), &co, &err)) return fail(RQ_ERR_PLAN, err);
     if (code_bytes) *code_bytes = co.size();
+    return RQ_OK;
+}
+
+int rq_debug_dma4_emulate(uint32_t K, uint32_t T, const uint32_t* esi, uint32_t n_out, const uint8_t* src, uint8_t* out,
+                          uint32_t quads, uint32_t la, uint32_t stats[8], size_t* code_bytes) {
+    Params p;
+    int rc = params_for_K(K, &p);
+    if (rc) return fail(rc, "k is too big");
+    if (T == 0 || T % 16) return fail(RQ_ERR_BAD_ARG, "four-row staging needs T a multiple of 16");
+    ColIR ir;
+    MProg mp, m4;
+    std::string err;
+    uint32_t passes = 0;
+    if (!compile_colprog(p, esi, n_out, alloc_options(), &ir, &mp, &err, &passes, false)) return fail(RQ_ERR_PLAN, err);
+    if (!compile_colprog_dma4(ir, alloc_options(), quads, la ? la : dma4_cfg().la, &m4, &err)) return fail(RQ_ERR_PLAN, err);
+    if (src && out && !emulate_colprog(m4, src, T, out, &err)) return fail(RQ_ERR_PLAN, err);
+    if (stats) {
+        const uint32_t v[8] = {(uint32_t)m4.ins.size(), m4.st.valu, m4.st.dma, m4.n_slots, m4.lds_base, m4.n_lds_slots,
+                               (uint32_t)mp.ins.size(), (passes & SCHED_4R) ? 1u : 0u};
+        std::memcpy(stats, v, sizeof v);
+    }
+    if (code_bytes) {
+        (void)colprog_launch_shape(&m4);
+        std::vector<char> co;
+        if (!comgr_assemble(emit_colprog_asm(m4, "rq_colprog_dma4"), &co, &err)) return fail(RQ_ERR_PLAN, err);
+        *code_bytes = co.size();
+    }
     return RQ_OK;
 }
 

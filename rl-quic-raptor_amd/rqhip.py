@@ -43,7 +43,7 @@ EXPORTED = (
     "rq_debug_colprog_eval", "rq_debug_colprog_emulate", "rq_debug_colprog_assemble", "rq_debug_decode_margin",
     "rq_decode_blocks_host", "rq_host_alloc", "rq_host_free", "rq_debug_colprog_passes",
     "rq_debug_shard_plan", "rq_debug_virtual_shards", "rq_debug_tuple", "rq_stream_release", "rq_shutdown",
-    "rq_launch_timing", "rq_launch_time", "rq_debug_pair_emulate",
+    "rq_launch_timing", "rq_launch_time", "rq_debug_pair_emulate", "rq_debug_dma4_emulate",
 )
 
 
@@ -176,6 +176,8 @@ def lib():
             "rq_launch_time": ([ctypes.POINTER(ctypes.c_double), u32p, ctypes.c_int], ctypes.c_int),
             "rq_debug_pair_emulate": ([ctypes.c_uint32, ctypes.c_uint32, u32p, ctypes.c_uint32, vp, vp, u32p, u32p,
                                        ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+            "rq_debug_dma4_emulate": ([ctypes.c_uint32, ctypes.c_uint32, u32p, ctypes.c_uint32, vp, vp, ctypes.c_uint32,
+                                       ctypes.c_uint32, u32p, ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -297,6 +299,29 @@ def pair_emulate(K, T, esis, src=None, cfg=(0, 0, 0, 0), assemble=False):
     P = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
     _check(lib().rq_debug_pair_emulate(K, T, P(e), len(e), sp, op, P(c), P(st), ctypes.byref(n) if assemble else None))
     d = dict(zip(PAIR_STATS, (int(x) for x in st)))
+    d["code_bytes"] = n.value
+    return (out.reshape(len(esis), T) if out is not None else None), d
+
+
+DMA4_STATS = ("ins", "valu", "dma4", "scratch_slots", "tbl_slots", "lds_slots", "ins_plain", "sched_4r")
+
+
+def dma4_emulate(K, T, esis, src=None, quads=8, la=0, assemble=False):
+    """rq_debug_dma4_emulate: the single-wave program with four-row staging, run on the host over one
+    item (src: K*T bytes, or None for statistics only).  Returns (outputs or None, stats dict)."""
+    import numpy as np
+    e = np.asarray(esis, np.uint32)
+    st = np.zeros(8, np.uint32)
+    out = None
+    sp = op = None
+    if src is not None:
+        s = np.ascontiguousarray(np.frombuffer(bytes(src), np.uint8))
+        out = np.zeros(len(esis) * T, np.uint8)
+        sp, op = s.ctypes.data, out.ctypes.data
+    n = ctypes.c_size_t(0)
+    P = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+    _check(lib().rq_debug_dma4_emulate(K, T, P(e), len(e), sp, op, quads, la, P(st), ctypes.byref(n) if assemble else None))
+    d = dict(zip(DMA4_STATS, (int(x) for x in st)))
     d["code_bytes"] = n.value
     return (out.reshape(len(esis), T) if out is not None else None), d
 

@@ -183,6 +183,25 @@ def test_pair_lag_and_transfer_sizes(rq, oracle, cfg):
     assert st["ring"] >= min(cfg[1], 16)
 
 
+@pytest.mark.parametrize("K,quads", [(1024, 4), (1024, 8), (2048, 8)])
+def test_single_wave_four_row_staging_matches_oracle(rq, oracle, K, quads):
+    """The single-wave program re-allocated with four-row staging (1 KiB LDS-DMA per four source rows,
+    rows then read from LDS): run on the host with the DMA / table-read ordering checked, the outputs
+    equal the oracle's symbols, and the kernel assembles within its register and LDS budget."""
+    T = 16
+    esis = list(range(K, K + K // 10 + 8)) if K == 1024 else [0, 5, K - 1] + list(range(K, K + 40))
+    rng = np.random.default_rng(K + quads)
+    data = rng.integers(0, 256, K * T, dtype=np.uint8)
+    out, st = rq.dma4_emulate(K, T, esis, data.tobytes(), quads=quads, assemble=(K == 1024))
+    assert st["sched_4r"] == 1 and st["dma4"] > 0
+    assert st["tbl_slots"] + st["lds_slots"] <= 160
+    enc = oracle.OracleEncoder(data.tobytes(), T)
+    for i, e in enumerate(esis):
+        assert np.array_equal(out[i], enc.gen_symbol(e)), (K, e)
+    if K == 1024:
+        assert st["code_bytes"] > 0
+
+
 def test_pair_ring_too_small_is_refused(rq):
     """A ring that cannot hold lag + 2 transfers is refused at compile time (never a runtime race)."""
     with pytest.raises(rq.RaptorQError):
