@@ -200,13 +200,14 @@ int rq_debug_colprog_assemble(uint32_t K, const uint32_t* esi, uint32_t n_out, s
  * pushes; wave B: HDPC bit accumulation, dense part, outputs; an LDS ring between them -- evaluated on
  * the host over two consecutive items of one block (the ring carries across items as on the GPU), every
  * ring read checked against the barrier intervals (tests).  cfg = {lag, max transfer, ring slots, wave A's
- * four-row staging quads (UINT32_MAX = none)}, 0 = the engine's default; stats[16] = A {instructions,
+ * four-row staging quads (UINT32_MAX = none), HDPC rows accumulated by wave A (UINT32_MAX = none)},
+ * 0 = the engine's default; stats[16] = A {instructions,
  * VALU, source loads, AGPR moves, ring stores, barriers}, B {instructions, VALU, ring loads, output
  * stores}, ring, transfers, values handed over, LDS bytes per workgroup, A's four-row DMAs, 1 if the
  * program uses the bit-accumulation schedule.
  * code_bytes (optional): the kernel assembled in process. */
 int rq_debug_pair_emulate(uint32_t K, uint32_t T, const uint32_t* esi, uint32_t n_out, const uint8_t* src,
-                          uint8_t* out, const uint32_t cfg[4], uint32_t stats[16], size_t* code_bytes);
+                          uint8_t* out, const uint32_t cfg[5], uint32_t stats[16], size_t* code_bytes);
 /* Tests: the single-wave program of (K, esi) re-allocated with four-row staging of its source rows
  * (`quads` quads of four LDS slots, `la` IR nodes ahead, 0 = the engine's default), evaluated on the
  * host over one item (T a multiple of 16).  stats[8] = {instructions, VALU, four-row DMAs, global

@@ -533,13 +533,19 @@ bool build(const Params& p, const std::vector<OutDesc>& outs, uint32_t passes, C
         // operand keeps it pending for the next chunk's (Acc) instead of an XOR2 now
         std::vector<Acc> S8((size_t)H * 8);
         std::vector<uint32_t> chunk;  // pivot indices of produced y (column < KS)
+        // SCHED_HA(n): the first n HDPC rows are tagged 4 (pair programs: wave A accumulates them, with
+        // its own copies of the subset sums, so the two waves' VALU work balances), the others 1
+        const uint32_t hA = std::min<uint32_t>(H, (passes >> SCHED_HA_SHIFT) & 0xFFu);
         auto flush = [&]() {
             if (chunk.empty()) return;
-            B.grp = 1;
             const size_t ng = (chunk.size() + 3) / 4;
-            std::vector<std::array<uint32_t, 16>> sub(ng);
-            for (size_t g = 0; g < ng; ++g) sub[g].fill(NOVAL);
+            std::vector<std::array<uint32_t, 16>> sub_all[2];
+            sub_all[0].resize(ng);
+            sub_all[1].resize(ng);
+            for (size_t g = 0; g < ng; ++g) { sub_all[0][g].fill(NOVAL); sub_all[1][g].fill(NOVAL); }
+            std::vector<std::array<uint32_t, 16>>* subp = &sub_all[0];
             auto subset = [&](size_t g, uint32_t m) -> uint32_t {  // XOR of group g's members in mask m
+                auto& sub = *subp;
                 auto& s = sub[g];
                 if (s[m] != NOVAL) return s[m];
                 std::vector<uint32_t> terms;
@@ -556,7 +562,9 @@ bool build(const Params& p, const std::vector<OutDesc>& outs, uint32_t passes, C
                 s[m] = B.xsum(terms);
                 return s[m];
             };
-            for (uint32_t h = 0; h < H; ++h)
+            for (uint32_t h = 0; h < H; ++h) {
+                B.grp = h < hA ? 4 : 1;
+                subp = &sub_all[h < hA ? 1 : 0];
                 for (uint32_t b = 0; b < 8; ++b)
                     for (size_t g = 0; g < ng; ++g) {
                         uint32_t m = 0;
@@ -566,6 +574,7 @@ bool build(const Params& p, const std::vector<OutDesc>& outs, uint32_t passes, C
                         }
                         if (m) S8[h * 8 + b].push(B, subset(g, m));
                     }
+            }
             chunk.clear();
             B.grp = 0;
         };
@@ -590,8 +599,8 @@ bool build(const Params& p, const std::vector<OutDesc>& outs, uint32_t passes, C
         }
         flush();
         bh_direct.assign(H, NOVAL);
-        B.grp = 1;
         for (uint32_t h = 0; h < H; ++h) {
+            B.grp = h < hA ? 4 : 1;
             uint32_t acc = NOVAL;
             for (int b = 7; b >= 0; --b) acc = B.xt(acc, S8[h * 8 + b].get(B));
             bh_direct[h] = acc;

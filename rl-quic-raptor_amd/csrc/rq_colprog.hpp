@@ -56,6 +56,9 @@ constexpr uint32_t NOVAL = 0xFFFFFFFFu;
 constexpr uint32_t SCHED_RS = 1u << 16;
 // ... with this bit set instead: no Horner scan, bh accumulated bit by bit over groups of produced y.
 constexpr uint32_t SCHED_4R = 1u << 17;
+// ... and (SCHED_4R only) bits 20..27 = n: the first n HDPC rows' bit accumulation tagged grp 4 with
+// their own subset sums (split_pair then runs them on wave A unless bmask has bit 4).
+constexpr uint32_t SCHED_HA_SHIFT = 20;
 
 struct IrNode {
     uint8_t k = IR_ZERO;
@@ -63,7 +66,8 @@ struct IrNode {
     uint32_t imm = 0;
     // what the node computes (SCHED_4R programs; split_pair assigns waves by it): 0 forward pass
     // (peeling: y values and their pushes into dependent rows), 1 HDPC bit accumulation (subset sums,
-    // bit rows, bh), 2 pushes into the remaining-row and output sums (and b2), 3 dense part and outputs
+    // bit rows, bh), 2 pushes into the remaining-row and output sums (and b2), 3 dense part and outputs,
+    // 4 the bit accumulation of the HDPC rows given to wave A (SCHED_HA_SHIFT)
     uint8_t grp = 0;
 };
 

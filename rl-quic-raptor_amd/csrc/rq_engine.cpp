@@ -481,19 +481,21 @@ uint32_t colprog_launch_shape(MProg* mp) {
 // the forward pass and pushes, wave B the HDPC bit accumulation, dense part and outputs, handed over
 // through an LDS ring.  Taken for the bit-accumulation (SCHED_4R) programs, whose single wave is bound
 // by its in-order issue behind the memory pipeline.  Experiments builds:
-// RQHIP_PAIR=0/1 forces the choice; RQHIP_PAIR_CFG="lag,max_transfer,ring_max".
+// RQHIP_PAIR=0/1 forces the choice; RQHIP_PAIR_CFG="lag,max_transfer,ring_max,quads,lookahead,hdpc_rows_on_A".
 struct PairCfg {
     int mode = 0;  // -1 on where it compiles, 0 off, 1 forced (RQHIP_PAIR)
     uint32_t lag = 6, xfer = 16, ring = 192;
     uint32_t dma4 = 32, la_dma = 1200;  // wave A's four-row staging (quads, look-ahead); 16-B aligned rows only
+    uint32_t ha = 0;  // HDPC rows whose bit accumulation wave A runs (SCHED_HA_SHIFT)
 };
 const PairCfg& pair_cfg() {
     static const PairCfg c = [] {
         PairCfg r;
         if (const char* e = knob("RQHIP_PAIR")) r.mode = std::atoi(e);
         if (const char* e = knob("RQHIP_PAIR_CFG")) {
-            unsigned a = 0, b = 0, d = 0, q = 9999, la = 0;
-            std::sscanf(e, "%u,%u,%u,%u,%u", &a, &b, &d, &q, &la);
+            unsigned a = 0, b = 0, d = 0, q = 9999, la = 0, ha = 9999;
+            std::sscanf(e, "%u,%u,%u,%u,%u,%u", &a, &b, &d, &q, &la, &ha);
+            if (ha != 9999) r.ha = ha;
             if (a) r.lag = a;
             if (b) r.xfer = b;
             if (d) r.ring = d;
@@ -544,7 +546,15 @@ bool compile_engine_program(const Params& p, const uint32_t* esi, uint32_t n_esi
     AllocOpts pa = ao;
     pa.dma4 = aligned16 ? c.dma4 : 0;
     pa.la_dma = c.la_dma;
-    if (!compile_pair(*ir, pa, /*B: grp 1 and 3*/ 0xA, c.lag, c.xfer, c.ring, pp, &e2)) {
+    ColIR irh;  // the first c.ha HDPC rows' bit accumulation on wave A (its own subset sums)
+    if (c.ha && !build_colprog(p, esi, n_esi, &irh, &e2, passes | (c.ha << SCHED_HA_SHIFT))) {
+        if (c.mode == 1) {
+            if (err) *err = e2;
+            return false;
+        }
+        return true;
+    }
+    if (!compile_pair(c.ha ? irh : *ir, pa, /*B: grp 1 and 3*/ 0xA, c.lag, c.xfer, c.ring, pp, &e2)) {
         if (c.mode == 1) {
             if (err) *err = e2;
             return false;
@@ -1819,7 +1829,7 @@ int rq_debug_dma4_emulate(uint32_t K, uint32_t T, const uint32_t* esi, uint32_t 
 }
 
 int rq_debug_pair_emulate(uint32_t K, uint32_t T, const uint32_t* esi, uint32_t n_out, const uint8_t* src,
-                          uint8_t* out, const uint32_t cfg[4], uint32_t stats[16], size_t* code_bytes) {
+                          uint8_t* out, const uint32_t cfg[5], uint32_t stats[16], size_t* code_bytes) {
     Params p;
     int rc = params_for_K(K, &p);
     if (rc) return fail(rc, "k is too big");
@@ -1837,6 +1847,12 @@ int rq_debug_pair_emulate(uint32_t K, uint32_t T, const uint32_t* esi, uint32_t 
     AllocOpts pa = alloc_options();
     pa.dma4 = !cfg || !cfg[3] ? c.dma4 : cfg[3] == 0xFFFFFFFFu ? 0u : cfg[3];  // wave A's four-row staging
     pa.la_dma = c.la_dma;
+    const uint32_t ha = cfg && cfg[4] ? (cfg[4] == 0xFFFFFFFFu ? 0u : cfg[4]) : c.ha;
+    if (ha) {
+        ColIR irh;
+        if (!build_colprog(p, esi, n_out, &irh, &err, passes | (ha << SCHED_HA_SHIFT))) return fail(RQ_ERR_PLAN, err);
+        ir = std::move(irh);
+    }
     if (!compile_pair(ir, pa, 0xA, lag, xfer, ring, &pp, &err)) return fail(RQ_ERR_PLAN, err);
     if (src && out && !emulate_pair(pp, src, T, out, &err, 2)) return fail(RQ_ERR_PLAN, err);
     if (stats) {

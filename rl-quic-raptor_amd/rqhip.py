@@ -282,12 +282,12 @@ PAIR_STATS = ("a_ins", "a_valu", "a_loads", "a_agpr_moves", "a_ring_stores", "a_
               "b_ring_loads", "b_stores", "ring", "transfers", "handed", "lds_bytes", "a_dma4", "sched_4r")
 
 
-def pair_emulate(K, T, esis, src=None, cfg=(0, 0, 0, 0), assemble=False):
+def pair_emulate(K, T, esis, src=None, cfg=(0, 0, 0, 0, 0), assemble=False):
     """rq_debug_pair_emulate: the two-wave split of the (K, esis) program, run on the host over two items
     of one block (src: K*T bytes, or None for statistics only).  Returns (outputs or None, stats dict)."""
     import numpy as np
     e = np.asarray(esis, np.uint32)
-    c = np.asarray(tuple(cfg) + (0,) * (4 - len(cfg)), np.uint32)
+    c = np.asarray(tuple(cfg) + (0,) * (5 - len(cfg)), np.uint32)
     st = np.zeros(16, np.uint32)
     out = None
     sp = op = None

@@ -168,10 +168,10 @@ def test_pair_program_matches_oracle(rq, oracle, K, T, esis):
         assert st["code_bytes"] > 0
 
 
-@pytest.mark.parametrize("cfg", [(1, 8, 0), (2, 4, 0), (10, 16, 320), (3, 32, 0)])
+@pytest.mark.parametrize("cfg", [(1, 8, 0), (2, 4, 0), (10, 16, 320), (3, 32, 0), (6, 16, 192, 32, 3), (2, 16, 0, 0xFFFFFFFF, 5)])
 def test_pair_lag_and_transfer_sizes(rq, oracle, cfg):
-    """Other lags / transfer sizes / rings: the same bytes (the ring window check and the barrier
-    intervals hold for each)."""
+    """Other lags / transfer sizes / rings / staging / HDPC rows accumulated on wave A: the same bytes (the
+    ring window check and the barrier intervals hold for each)."""
     K, T = 1024, 8
     esis = list(range(K, K + 76))
     rng = np.random.default_rng(sum(cfg))

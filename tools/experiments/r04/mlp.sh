@@ -11,6 +11,7 @@ run() { # tag env...
 CB="1024 1200 1100 16 3"
 run pair4_small RQHIP_PAIR=1
 run single_d4_small RQHIP_PAIR=0 RQHIP_DMA4=8
+run pair_ha3_small RQHIP_PAIR=1 RQHIP_PAIR_CFG=6,16,192,32,1200,3
 CB="1024 1200 1100 1024 10"
 run single RQHIP_PAIR=0
 run single_d4q4 RQHIP_PAIR=0 RQHIP_DMA4=4
@@ -19,6 +20,9 @@ run pair_dword RQHIP_PAIR=1 RQHIP_PAIR_CFG=6,16,192,0
 run pair4 RQHIP_PAIR=1
 run pair4_q16 RQHIP_PAIR=1 RQHIP_PAIR_CFG=6,16,192,16,800
 run pair4_lag2 RQHIP_PAIR=1 RQHIP_PAIR_CFG=2,16,192
+run pair4_ha2 RQHIP_PAIR=1 RQHIP_PAIR_CFG=6,16,192,32,1200,2
+run pair4_ha3 RQHIP_PAIR=1 RQHIP_PAIR_CFG=6,16,192,32,1200,3
+run pair4_ha4 RQHIP_PAIR=1 RQHIP_PAIR_CFG=6,16,192,32,1200,4
 run single_w512 RQHIP_PAIR=0 RQHIP_WAVES=512
 run single2 RQHIP_PAIR=0
 run pair4_2 RQHIP_PAIR=1
