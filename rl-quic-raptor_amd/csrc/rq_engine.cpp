@@ -137,6 +137,9 @@ struct Workspace {
     // program; the caller's stream waits for `cpy[n % 2]` before the solve
     hipStream_t cs = nullptr;
     hipEvent_t cpy[2] = {nullptr, nullptr};
+    // solve beside the syndrome program (solve_beside()): `go` on the caller's stream before the
+    // syndrome program, `solved` on `cs` after the solver kernels
+    hipEvent_t go = nullptr, solved = nullptr;
 
     uint32_t flip = 0;
     uint64_t last_use = 0;          // LRU clock (DevCtx::wsp)
@@ -159,6 +162,8 @@ struct Workspace {
             if (e) (void)hipEventDestroy(e);
         for (hipEvent_t& e : cpy)
             if (e) (void)hipEventDestroy(e);
+        if (go) (void)hipEventDestroy(go);
+        if (solved) (void)hipEventDestroy(solved);
         if (cs) (void)hipStreamDestroy(cs);
     }
 };
@@ -881,6 +886,15 @@ uint32_t solve_row_margin() {
 
 // One solve pass over the blocks of `blocks` (each pending; cnt[b] = candidate repairs offered).
 // Caller holds ctx->mu.  Host arrays as in rq_decode_desc.
+// Decode solve beside the syndrome program (decode_pass); RQHIP_SOLVE_BESIDE=0/1 in experiments builds.
+bool solve_beside() {
+    static const bool on = [] {
+        const char* e = knob("RQHIP_SOLVE_BESIDE");
+        return e ? e[0] == '1' : false;
+    }();
+    return on;
+}
+
 int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, void* data, uint64_t data_stride,
                 const std::vector<uint32_t>& eoff, const uint32_t* erased, const std::vector<uint32_t>& roff,
                 const uint32_t* repair_esi, const std::vector<uint32_t>& cnt, const std::vector<uint32_t>& blk_map,
@@ -1082,16 +1096,38 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     if ((rc = w->xb.ensure((size_t)xo * 64))) return rc;
     if ((rc = w->xp.ensure(std::max<size_t>(n_er, 1) * 2))) return rc;
     if (go && (rc = w->gws.ensure((size_t)go * 64))) return rc;
+    // The solve reads only the descriptors and M (the program's repair-coefficient matrix), not the
+    // syndromes: it can run on the side stream beside the syndrome program, which leaves SIMDs and
+    // LDS free (960 one-wave workgroups on 1 024 SIMDs at K=1024).  The side stream first waits for
+    // this call's start on the caller's stream (`go`: the previous call's apply and downloads have
+    // finished with X, the statuses and the workspace); the apply waits for `solved`.
+    const bool beside = side && solve_beside();
+    if (beside && !w->go) {
+        hipEvent_t ev[2] = {nullptr, nullptr};
+        if (hipEventCreateWithFlags(&ev[0], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&ev[1], hipEventDisableTiming) != hipSuccess) {
+            for (hipEvent_t e : ev)
+                if (e) (void)hipEventDestroy(e);
+            return fail(RQ_ERR_DEVICE, "side-stream events failed");
+        }
+        w->go = ev[0];
+        w->solved = ev[1];
+    }
+    if (beside) {
+        HIP_TRY(hipEventRecord(w->go, (hipStream_t)stream));
+        HIP_TRY(hipStreamWaitEvent(w->cs, w->go, 0));
+    }
 
     // 1) r0 = the column program on every block, erased rows as they are (whatever bytes g_E they
     //    hold): the syndromes s = r ^ r0 = M (x_E ^ g_E), and k_apply starts each output from g_E
     PackArgs z;
     z.blk = di + o_zb; z.row = di + o_zr; z.data = static_cast<uint8_t*>(data); z.data_stride = data_stride;
     z.T = T; z.n = nz; z.pack = nullptr;
-    if ((rc = launch_col(ctx, k, T, n_blocks, data, data_stride, w->r0.p, (uint64_t)uni.size() * T, stream)))
+    // 2) per-block solve (after the side stream's descriptor upload): on the side stream, or after the
+    //    syndrome program on the caller's
+    if (!beside && (rc = launch_col(ctx, k, T, n_blocks, data, data_stride, w->r0.p, (uint64_t)uni.size() * T, stream)))
         return rc;
-    // 2) per-block solve (after the side stream's descriptor upload)
-    if (side) HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, w->cpy[set], 0));
+    if (side && !beside) HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, w->cpy[set], 0));
     SolveArgs s;
     s.blk_map = di + o_map;
     s.erased_off = di + o_eoff;
@@ -1113,7 +1149,14 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     s.row_margin = solve_row_margin();
     s.n_map = nw;
     s.diag_steps = 0;
-    if (launch_solve(s, nw, need_general, wide, max_lds_e, stream)) return fail(RQ_ERR_DEVICE, "k_solve launch failed");
+    if (launch_solve(s, nw, need_general, wide, max_lds_e, beside ? (void*)w->cs : stream))
+        return fail(RQ_ERR_DEVICE, "k_solve launch failed");
+    if (beside) {
+        HIP_TRY(hipEventRecord(w->solved, w->cs));
+        if ((rc = launch_col(ctx, k, T, n_blocks, data, data_stride, w->r0.p, (uint64_t)uni.size() * T, stream)))
+            return rc;
+        HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, w->solved, 0));
+    }
     // 3) apply: x_E = X * s
     ApplyArgs ap;
     ap.blk_map = di + o_map;

@@ -33,6 +33,14 @@ for step in "$@"; do
             -- python3 $BENCH --cpu-sample 0 --steps 3 --warmup 1 > $log.p$k.log 2>&1 || { tail -5 $log.p$k.log; exit 1; }
         done
         python3 tools/experiments/pmc_sum.py $log ;;
+    bytes) # HBM traffic of the kernels matching ARG (default k_apply) over a short bench: FETCH_SIZE and
+        # WRITE_SIZE in separate passes (per-launch sums in KiB; bytes = KiB x 1024 / the calibration
+        # ratio of tools/gpu_profile.sh: 0.5 for FETCH_SIZE, 1.0 for WRITE_SIZE on gfx950)
+        for c in FETCH_SIZE WRITE_SIZE; do
+          timeout -s KILL 90 rocprofv3 --pmc $c --kernel-include-regex "${arg:-k_apply}" --output-format csv -d $log/p$c -o p \
+            -- python3 $BENCH --cpu-sample 0 --steps 3 --warmup 1 > $log.$c.log 2>&1 || { tail -5 $log.$c.log; exit 1; }
+        done
+        python3 tools/experiments/pmc_sum.py $log ;;
     py) s=${arg%%:*}; a=""; [ "$arg" != "$s" ] && a=${arg#*:}
         timeout -k 10 300 python3 $s $a > $log.log 2>&1 || { tail -20 $log.log; exit 1; }; tail -5 $log.log ;;
     *) echo "unknown step $name"; exit 2 ;;
