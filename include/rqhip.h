@@ -208,6 +208,12 @@ int rq_debug_colprog_assemble(uint32_t K, const uint32_t* esi, uint32_t n_out, s
  * code_bytes (optional): the kernel assembled in process. */
 int rq_debug_pair_emulate(uint32_t K, uint32_t T, const uint32_t* esi, uint32_t n_out, const uint8_t* src,
                           uint8_t* out, const uint32_t cfg[5], uint32_t stats[16], size_t* code_bytes);
+/* Tests: the host side of one rq_decode_batch_async call on these descriptor arrays (argument checks,
+ * host-decided statuses, the union of the candidate repairs, the descriptor words), no device work;
+ * repeated `iters` times, the mean wall time of calls 2..iters in us.  n_idx_words: descriptor words. */
+int rq_debug_decode_plan(uint32_t T, uint32_t K, uint32_t n_blocks, const uint32_t* n_erased, const uint32_t* erased,
+                         const uint32_t* n_repair, const uint32_t* repair_esi, uint32_t iters, double* us_per_call,
+                         uint32_t* n_idx_words);
 /* Tests: the single-wave program of (K, esi) re-allocated with four-row staging of its source rows
  * (`quads` quads of four LDS slots, `la` IR nodes ahead, 0 = the engine's default), evaluated on the
  * host over one item (T a multiple of 16).  stats[8] = {instructions, VALU, four-row DMAs, global

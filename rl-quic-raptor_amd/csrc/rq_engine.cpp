@@ -884,6 +884,189 @@ uint32_t solve_row_margin() {
     return m;
 }
 
+// Host side of one decode pass (bounded per call, nothing cached across calls -- a
+// receiver sees a new erasure pattern per batch).  plan_decode: per-block offsets of X and of the
+// general solver's workspace, the union of the candidate repair ESIs (a presence map, then a dense
+// [K, K+R) range when the set is not too sparse), and the index-workspace layout.  fill_decode_idx:
+// the descriptor words, written once, straight into the pinned staging the upload reads.  The vectors
+// keep their capacity per thread between calls.
+struct DecodePlan {
+    uint32_t nw = 0, max_e = 0, max_lds_e = 0;
+    bool need_general = false;  // some block may reach the general solver (e or candidates > 64)
+    bool wide = false;          // some block has 64 < e <= 128
+    uint64_t xo = 0, go = 0;    // X and general-workspace sizes (64-B units)
+    size_t nz = 0;              // recovered rows to pack (host-memory decodes)
+    uint32_t K = 0, mx = 0;
+    bool mapped = false, dense_uni = false;
+    std::vector<uint32_t> xoff, goff, uni, upos;
+    std::vector<uint8_t> seen;
+    // index workspace: blk_map | eoff | roff | cnt | erased | rep_uidx | status | xoff | goff
+    // [| pack list (blk, row): host-memory decodes only]
+    size_t o_map = 0, o_eoff = 0, o_roff = 0, o_cnt = 0, o_er = 0, o_ru = 0, o_st = 0, o_xo = 0, o_go = 0, o_zb = 0,
+           o_zr = 0, n_idx = 0;
+};
+
+DecodePlan& decode_plan_scratch() {
+    static thread_local DecodePlan pl;
+    return pl;
+}
+
+// mx_hint: the largest candidate ESI when the caller knows it (every block offers all its received
+// repairs: the argument check's maximum), else 0.
+int plan_decode(const Params& p, uint32_t n_blocks, const std::vector<uint32_t>& eoff, const std::vector<uint32_t>& roff,
+                const uint32_t* repair_esi, const std::vector<uint32_t>& cnt, const std::vector<uint32_t>& blk_map,
+                bool pack, DecodePlan* pl, uint32_t mx_hint = 0) {
+    const uint32_t nw = (uint32_t)blk_map.size();
+    pl->nw = nw;
+    pl->max_e = pl->max_lds_e = 0;
+    pl->need_general = pl->wide = false;
+    pl->xoff.resize(nw);
+    pl->goff.resize(nw);
+    uint64_t xo = 0, go = 0;
+    uint32_t mx = 0;
+    size_t n_cand = 0, nz = 0;
+    const uint32_t lds_max = lds_e_max(), margin = solve_row_margin();
+    for (uint32_t bi = 0; bi < nw; ++bi) {
+        const uint32_t b = blk_map[bi], e = eoff[b + 1] - eoff[b];
+        pl->max_e = std::max(pl->max_e, e);
+        if (e <= lds_max) pl->max_lds_e = std::max(pl->max_lds_e, e);
+        pl->need_general |= (e > 64 || cnt[b] > std::min<uint32_t>(64, e + margin));
+        pl->wide |= (e > 64 && e <= 128);
+        if (!mx_hint) {
+            const uint32_t* x = repair_esi + roff[b];
+            uint32_t m = 0;
+            for (uint32_t i = 0; i < cnt[b]; ++i) m = std::max(m, x[i]);
+            mx = std::max(mx, m);
+        }
+        n_cand += cnt[b];
+        nz += e;
+        pl->xoff[bi] = (uint32_t)xo;
+        xo += ((uint64_t)e * x_stride(e) + 63) / 64;
+        pl->goff[bi] = (uint32_t)go;
+        if (e > lds_max) go += (solve_ws_bytes(e) + 63) / 64;
+    }
+    if (xo >= (1ull << 32) || go >= (1ull << 32)) return fail(RQ_ERR_UNSUPPORTED, "decode workspace beyond 256 GiB");
+    pl->xo = xo;
+    pl->go = go;
+    if (mx_hint) mx = mx_hint;
+    const uint32_t K = p.K;
+    pl->K = K;
+    pl->mx = mx;
+    pl->mapped = n_cand && (uint64_t)mx - K < (1u << 22);
+    auto& uni = pl->uni;
+    uni.clear();
+    // The rule below makes the union the dense range [K, K + span) when span <= 4 |union| + 64.  The
+    // distinct candidates of the block that offers the most are a lower bound on |union|: when that
+    // bound already satisfies the rule, the presence pass over every candidate is skipped (same union).
+    bool dense_known = false;
+    if (pl->mapped) {
+        uint32_t bmax = blk_map[0];
+        for (uint32_t b : blk_map)
+            if (cnt[b] > cnt[bmax]) bmax = b;
+        pl->seen.assign((size_t)(mx - K) + 1, 0);
+        uint8_t* seen = pl->seen.data();
+        uint32_t lb = 0;
+        for (uint32_t i = 0; i < cnt[bmax]; ++i) {
+            const uint32_t v = repair_esi[roff[bmax] + i] - K;
+            lb += !seen[v];
+            seen[v] = 1;
+        }
+        const uint64_t span = ((uint64_t)mx - K + 4) & ~(uint64_t)3;
+        if (span <= 4ull * lb + 64) {
+            uni.resize((size_t)span);
+            for (uint32_t i = 0; i < span; ++i) uni[i] = K + i;
+            dense_known = true;
+        }
+    }
+    if (dense_known) {
+    } else if (pl->mapped) {
+        pl->seen.assign((size_t)(mx - K) + 1, 0);
+        uint8_t* seen = pl->seen.data();
+        for (uint32_t b : blk_map) {
+            const uint32_t* x = repair_esi + roff[b];
+            for (uint32_t i = 0; i < cnt[b]; ++i) seen[x[i] - K] = 1;
+        }
+        for (size_t i = 0; i < pl->seen.size(); ++i)
+            if (seen[i]) uni.push_back(K + (uint32_t)i);
+    } else {
+        for (uint32_t b : blk_map) uni.insert(uni.end(), repair_esi + roff[b], repair_esi + roff[b] + cnt[b]);
+        std::sort(uni.begin(), uni.end());
+        uni.erase(std::unique(uni.begin(), uni.end()), uni.end());
+    }
+    if (!uni.empty() && !dense_known) {
+        const uint64_t span = ((uint64_t)uni.back() - K + 4) & ~(uint64_t)3;
+        if (span <= 4 * uni.size() + 64) {
+            uni.resize((size_t)span);
+            for (uint32_t i = 0; i < span; ++i) uni[i] = K + i;
+        }
+    }
+    // union index of every candidate repair: direct for a dense union, a table for a mapped one,
+    // binary search otherwise
+    pl->dense_uni = !uni.empty() && uni.back() - uni.front() + 1 == uni.size();
+    if (!pl->dense_uni && pl->mapped) {
+        pl->upos.assign((size_t)(mx - K) + 1, 0);
+        for (uint32_t j = 0; j < uni.size(); ++j) pl->upos[uni[j] - K] = j;
+    }
+    const size_t n_er = eoff[n_blocks], n_rep = roff[n_blocks];
+    if (!pack) nz = 0;
+    pl->nz = nz;
+    pl->o_map = 0;
+    pl->o_eoff = pl->o_map + nw;
+    pl->o_roff = pl->o_eoff + n_blocks + 1;
+    pl->o_cnt = pl->o_roff + n_blocks + 1;
+    pl->o_er = pl->o_cnt + n_blocks;
+    pl->o_ru = pl->o_er + n_er;
+    pl->o_st = pl->o_ru + n_rep;
+    pl->o_xo = pl->o_st + n_blocks;
+    pl->o_go = pl->o_xo + nw;
+    pl->o_zb = pl->o_go + nw;
+    pl->o_zr = pl->o_zb + nz;
+    pl->n_idx = pl->o_zr + nz;
+    return RQ_OK;
+}
+
+void fill_decode_idx(const DecodePlan& pl, uint32_t n_blocks, const std::vector<uint32_t>& eoff, const uint32_t* erased,
+                     const std::vector<uint32_t>& roff, const uint32_t* repair_esi, const std::vector<uint32_t>& cnt,
+                     const std::vector<uint32_t>& blk_map, const int32_t* status, uint32_t* I) {
+    const uint32_t nw = pl.nw;
+    const size_t n_er = eoff[n_blocks];
+    std::memcpy(I + pl.o_map, blk_map.data(), nw * 4);
+    std::memcpy(I + pl.o_eoff, eoff.data(), (n_blocks + 1) * 4);
+    std::memcpy(I + pl.o_roff, roff.data(), (n_blocks + 1) * 4);
+    std::memcpy(I + pl.o_cnt, cnt.data(), n_blocks * 4);
+    if (n_er) std::memcpy(I + pl.o_er, erased, n_er * 4);
+    // union indices of the mapped blocks' candidates (the kernels read no other block's entries)
+    uint32_t* u = I + pl.o_ru;
+    for (uint32_t b : blk_map) {
+        const uint32_t* x = repair_esi + roff[b];
+        uint32_t* ub = u + roff[b];
+        const uint32_t n = cnt[b];
+        if (pl.dense_uni) {
+            const uint32_t f = pl.uni.front();
+            for (uint32_t i = 0; i < n; ++i) ub[i] = x[i] - f;
+        } else if (pl.mapped) {
+            const uint32_t K = pl.K;
+            for (uint32_t i = 0; i < n; ++i) ub[i] = pl.upos[x[i] - K];
+        } else {
+            for (uint32_t i = 0; i < n; ++i)
+                ub[i] = (uint32_t)(std::lower_bound(pl.uni.begin(), pl.uni.end(), x[i]) - pl.uni.begin());
+        }
+    }
+    // device status: host-decided values, ST_PENDING for the rest
+    std::memcpy(I + pl.o_st, status, n_blocks * 4);
+    std::memcpy(I + pl.o_xo, pl.xoff.data(), nw * 4);
+    std::memcpy(I + pl.o_go, pl.goff.data(), nw * 4);
+    if (pl.nz) {  // recovered rows packed densely for the download, in blk_map order
+        uint32_t* zb = I + pl.o_zb;
+        uint32_t* zr = I + pl.o_zr;
+        for (uint32_t b : blk_map)
+            for (uint32_t i = eoff[b]; i < eoff[b + 1]; ++i) {
+                *zb++ = b;
+                *zr++ = erased[i];
+            }
+    }
+}
+
 // One solve pass over the blocks of `blocks` (each pending; cnt[b] = candidate repairs offered).
 // Caller holds ctx->mu.  Host arrays as in rq_decode_desc.
 // Decode solve beside the syndrome program (decode_pass); RQHIP_SOLVE_BESIDE=0/1 in experiments builds.
@@ -898,120 +1081,25 @@ bool solve_beside() {
 int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, void* data, uint64_t data_stride,
                 const std::vector<uint32_t>& eoff, const uint32_t* erased, const std::vector<uint32_t>& roff,
                 const uint32_t* repair_esi, const std::vector<uint32_t>& cnt, const std::vector<uint32_t>& blk_map,
-                const void* repair, int32_t* status, void* stream, PackOut* po, Fin fin) {
+                const void* repair, int32_t* status, void* stream, PackOut* po, Fin fin, uint32_t mx_hint = 0) {
     int rc;
     const bool async = fin == Fin::Async;
-    const uint32_t nw = (uint32_t)blk_map.size();
-    uint32_t max_e = 0, max_lds_e = 0;
-    bool need_general = false;  // some block may reach the general solver (e or candidates > 64)
-    bool wide = false;          // some block has 64 < e <= 128
-    // Host work per call is bounded: per-thread scratch keeps its capacity between
-    // calls (nothing is cached across calls -- a receiver sees a new erasure pattern per batch), the
-    // union comes from a presence map with a direct ESI -> union-index table, and the descriptor words
-    // are written once, straight into the pinned staging the upload reads.
-    static thread_local std::vector<uint32_t> xoff, goff, uni, upos;
-    static thread_local std::vector<uint8_t> seen;
-    xoff.resize(nw);
-    goff.resize(nw);
-    uint64_t xo = 0, go = 0;
-    uint32_t mx = 0, mn = 0xFFFFFFFFu;
-    size_t n_cand = 0, nz = 0;
-    for (uint32_t bi = 0; bi < nw; ++bi) {
-        const uint32_t b = blk_map[bi], e = eoff[b + 1] - eoff[b];
-        max_e = std::max(max_e, e);
-        if (e <= lds_e_max()) max_lds_e = std::max(max_lds_e, e);
-        need_general |= (e > 64 || cnt[b] > std::min<uint32_t>(64, e + solve_row_margin()));
-        wide |= (e > 64 && e <= 128);
-        for (uint32_t i = roff[b]; i < roff[b] + cnt[b]; ++i) {
-            mx = std::max(mx, repair_esi[i]);
-            mn = std::min(mn, repair_esi[i]);
-        }
-        n_cand += cnt[b];
-        nz += e;
-        xoff[bi] = (uint32_t)xo;
-        xo += ((uint64_t)e * x_stride(e) + 63) / 64;
-        goff[bi] = (uint32_t)go;
-        if (e > lds_e_max()) go += (solve_ws_bytes(e) + 63) / 64;
-    }
-    if (xo >= (1ull << 32) || go >= (1ull << 32)) return fail(RQ_ERR_UNSUPPORTED, "decode workspace beyond 256 GiB");
-    // the union of the candidate repair ESIs (the rule above: a dense [K, K+R) range when the set is not
-    // too sparse, else the exact sorted set)
-    const uint32_t K = p.K;
-    const bool mapped = n_cand && (uint64_t)mx - K < (1u << 22);
-    uni.clear();
-    if (mapped) {
-        seen.assign((size_t)(mx - K) + 1, 0);
-        for (uint32_t b : blk_map)
-            for (uint32_t i = roff[b]; i < roff[b] + cnt[b]; ++i) seen[repair_esi[i] - K] = 1;
-        for (size_t i = 0; i < seen.size(); ++i)
-            if (seen[i]) uni.push_back(K + (uint32_t)i);
-    } else {
-        for (uint32_t b : blk_map) uni.insert(uni.end(), repair_esi + roff[b], repair_esi + roff[b] + cnt[b]);
-        std::sort(uni.begin(), uni.end());
-        uni.erase(std::unique(uni.begin(), uni.end()), uni.end());
-    }
-    if (!uni.empty()) {
-        const uint64_t span = ((uint64_t)uni.back() - K + 4) & ~(uint64_t)3;
-        if (span <= 4 * uni.size() + 64) {
-            uni.resize((size_t)span);
-            for (uint32_t i = 0; i < span; ++i) uni[i] = K + i;
-        }
-    }
-    (void)mn;
+    DecodePlan& pl = decode_plan_scratch();
+    if ((rc = plan_decode(p, n_blocks, eoff, roff, repair_esi, cnt, blk_map, po != nullptr, &pl, mx_hint))) return rc;
+    const uint32_t nw = pl.nw, max_e = pl.max_e, max_lds_e = pl.max_lds_e;
+    const bool need_general = pl.need_general, wide = pl.wide;
+    const uint64_t xo = pl.xo, go = pl.go;
+    const size_t nz = pl.nz;
+    const std::vector<uint32_t>& uni = pl.uni;
     ColKernel* k;
     const bool a16 = T % 16 == 0 && data_stride % 16 == 0 && (uintptr_t)data % 16 == 0;
     if ((rc = get_col_kernel(ctx, p, uni.data(), (uint32_t)uni.size(), false, &k, a16))) return rc;
     if ((rc = ensure_mrep(ctx, k, stream))) return rc;
-    // union index of every candidate repair: direct for a dense union, a table for a mapped one,
-    // binary search otherwise
-    const bool dense_uni = uni.back() - uni.front() + 1 == uni.size();
-    if (!dense_uni && mapped) {
-        upos.assign((size_t)(mx - K) + 1, 0);
-        for (uint32_t j = 0; j < uni.size(); ++j) upos[uni[j] - K] = j;
-    }
-    const size_t n_er = eoff[n_blocks], n_rep = roff[n_blocks];
-    // index workspace: blk_map | eoff | roff | cnt | erased | rep_uidx | status | xoff | goff
-    // [| pack list (blk, row): host-memory decodes only]
-    const size_t o_map = 0, o_eoff = o_map + nw, o_roff = o_eoff + n_blocks + 1, o_cnt = o_roff + n_blocks + 1,
-                 o_er = o_cnt + n_blocks, o_ru = o_er + n_er, o_st = o_ru + n_rep, o_xo = o_st + n_blocks,
-                 o_go = o_xo + nw, o_zb = o_go + nw;
-    if (!po) nz = 0;
-    const size_t o_zr = o_zb + nz, n_idx = o_zr + nz;
-    auto fill_idx = [&](uint32_t* I) {
-        std::memcpy(I + o_map, blk_map.data(), nw * 4);
-        std::memcpy(I + o_eoff, eoff.data(), (n_blocks + 1) * 4);
-        std::memcpy(I + o_roff, roff.data(), (n_blocks + 1) * 4);
-        std::memcpy(I + o_cnt, cnt.data(), n_blocks * 4);
-        if (n_er) std::memcpy(I + o_er, erased, n_er * 4);
-        if (n_rep) std::memset(I + o_ru, 0, n_rep * 4);
-        for (uint32_t b : blk_map) {
-            uint32_t* u = I + o_ru;
-            const uint32_t* x = repair_esi;
-            const uint32_t r0 = roff[b], r1 = roff[b] + cnt[b];
-            if (dense_uni) {
-                const uint32_t f = uni.front();
-                for (uint32_t i = r0; i < r1; ++i) u[i] = x[i] - f;
-            } else if (mapped) {
-                for (uint32_t i = r0; i < r1; ++i) u[i] = upos[x[i] - K];
-            } else {
-                for (uint32_t i = r0; i < r1; ++i)
-                    u[i] = (uint32_t)(std::lower_bound(uni.begin(), uni.end(), x[i]) - uni.begin());
-            }
-        }
-        // device status: host-decided values, ST_PENDING for the rest
-        std::memcpy(I + o_st, status, n_blocks * 4);
-        std::memcpy(I + o_xo, xoff.data(), nw * 4);
-        std::memcpy(I + o_go, goff.data(), nw * 4);
-        if (po) {  // recovered rows packed densely for the download, in blk_map order
-            uint32_t* zb = I + o_zb;
-            uint32_t* zr = I + o_zr;
-            for (uint32_t b : blk_map)
-                for (uint32_t i = eoff[b]; i < eoff[b + 1]; ++i) {
-                    *zb++ = b;
-                    *zr++ = erased[i];
-                }
-        }
-    };
+    const size_t n_er = eoff[n_blocks];
+    const size_t o_map = pl.o_map, o_eoff = pl.o_eoff, o_er = pl.o_er, o_ru = pl.o_ru, o_st = pl.o_st,
+                 o_xo = pl.o_xo, o_go = pl.o_go, o_zb = pl.o_zb, o_zr = pl.o_zr, n_idx = pl.n_idx;
+    const size_t o_roff = pl.o_roff, o_cnt = pl.o_cnt;
+    auto fill_idx = [&](uint32_t* I) { fill_decode_idx(pl, n_blocks, eoff, erased, roff, repair_esi, cnt, blk_map, status, I); };
     // descriptors through pinned staging, without blocking this thread.  (An upload on a copy stream
     // of its own, joined by events, measured 0.25 ms slower per rq_decode_batch_async call, r02u.)
     Workspace* w = ctx->wsp(stream);
@@ -1216,9 +1304,12 @@ struct DecodeJob {
     int32_t* status = nullptr;
     void* stream = nullptr;
     std::vector<uint32_t> eoff, roff, blk_map, cnt;
+    uint32_t rmax = 0;        // the largest received repair ESI (decode_args)
+    bool all_repairs = false;  // every block to solve offers all its received repairs (async)
 };
 
-int decode_begin(DevCtx* ctx, DecodeJob* j, const uint32_t* n_erased, PackOut* po, Fin fin) {
+// decode_begin's host part: offsets, argument checks, host-decided statuses, the blocks to solve.
+int decode_args(DecodeJob* j, const uint32_t* n_erased, Fin fin) {
     const uint32_t n_blocks = j->n_blocks;
     j->eoff.assign(n_blocks + 1, 0);
     j->roff.assign(n_blocks + 1, 0);
@@ -1226,25 +1317,47 @@ int decode_begin(DevCtx* ctx, DecodeJob* j, const uint32_t* n_erased, PackOut* p
         j->eoff[b + 1] = j->eoff[b] + n_erased[b];
         j->roff[b + 1] = j->roff[b] + j->n_repair[b];
     }
+    // argument checks over the whole arrays (vectorised reductions), before any status is written
+    const size_t n_er = j->eoff[n_blocks], n_rep = j->roff[n_blocks];
+    uint32_t emax = 0, rmin = 0xFFFFFFFFu, rmax = 0, nrmax = 0;
+    const uint32_t *er = j->erased, *re = j->repair_esi;
+    for (size_t i = 0; i < n_er; ++i) emax = std::max(emax, er[i]);
+    for (size_t i = 0; i < n_rep; ++i) {
+        rmin = std::min(rmin, re[i]);
+        rmax = std::max(rmax, re[i]);
+    }
+    for (uint32_t b = 0; b < n_blocks; ++b) nrmax = std::max(nrmax, j->n_repair[b]);
+    // the solvers keep a received repair's index within its block as uint16 (rowid / xpiv)
+    if (nrmax > 65535) return fail(RQ_ERR_UNSUPPORTED, "more than 65535 received repair symbols in one block");
+    if (n_er && emax >= j->p.K) return fail(RQ_ERR_BAD_ARG, "erased ESI >= K");
+    if (n_rep && rmin < j->p.K) return fail(RQ_ERR_BAD_ARG, "repair ESI < K");
+    j->rmax = rmax;
+    j->all_repairs = fin == Fin::Async;
     j->blk_map.clear();
     j->cnt.assign(n_blocks, 0);
     for (uint32_t b = 0; b < n_blocks; ++b) {
         const uint32_t e = n_erased[b], nr = j->n_repair[b];
-        // the solvers keep a received repair's index within its block as uint16 (rowid / xpiv)
-        if (nr > 65535) return fail(RQ_ERR_UNSUPPORTED, "more than 65535 received repair symbols in one block");
-        for (uint32_t i = j->eoff[b]; i < j->eoff[b + 1]; ++i)
-            if (j->erased[i] >= j->p.K) return fail(RQ_ERR_BAD_ARG, "erased ESI >= K");
-        for (uint32_t i = j->roff[b]; i < j->roff[b + 1]; ++i)
-            if (j->repair_esi[i] < j->p.K) return fail(RQ_ERR_BAD_ARG, "repair ESI < K");
         if (e > nr) { j->status[b] = RQ_ERR_NOT_ENOUGH; continue; }  // (K - e) + nr < K held symbols
         if (e == 0) { j->status[b] = 1; continue; }
         j->status[b] = ST_PENDING;
         j->cnt[b] = fin == Fin::Async ? nr : std::min(nr, e + g_subset_margin);
         j->blk_map.push_back(b);
     }
-    if (j->blk_map.empty()) return RQ_OK;
+    return RQ_OK;
+}
+
+// The largest candidate ESI of a pass over every block with all their received repairs: the argument
+// check's maximum (0: plan_decode computes it).
+uint32_t decode_mx_hint(const DecodeJob& j) {
+    return j.all_repairs && j.blk_map.size() == j.n_blocks ? j.rmax : 0u;
+}
+
+int decode_begin(DevCtx* ctx, DecodeJob* j, const uint32_t* n_erased, PackOut* po, Fin fin) {
+    int rc = decode_args(j, n_erased, fin);
+    if (rc || j->blk_map.empty()) return rc;
+    const uint32_t n_blocks = j->n_blocks;
     return decode_pass(ctx, j->p, j->T, n_blocks, j->data, j->data_stride, j->eoff, j->erased, j->roff, j->repair_esi,
-                       j->cnt, j->blk_map, j->repair, j->status, j->stream, po, fin);
+                       j->cnt, j->blk_map, j->repair, j->status, j->stream, po, fin, decode_mx_hint(*j));
 }
 
 // After a Sync pass (or a Deferred one and a sync of its stream): the all-repairs pass for the
@@ -1841,6 +1954,37 @@ int rq_debug_colprog_assemble(uint32_t K, const uint32_t* esi, uint32_t n_out, s
     (void)colprog_launch_shape(&mp);
     if (!comgr_assemble(emit_colprog_asm(mp, "rq_colprog"), &co, &err)) return fail(RQ_ERR_PLAN, err);
     if (code_bytes) *code_bytes = co.size();
+    return RQ_OK;
+}
+
+int rq_debug_decode_plan(uint32_t T, uint32_t K, uint32_t n_blocks, const uint32_t* n_erased, const uint32_t* erased,
+                         const uint32_t* n_repair, const uint32_t* repair_esi, uint32_t iters, double* us_per_call,
+                         uint32_t* n_idx_words) {
+    Params p;
+    int rc = params_for_K(K, &p);
+    if (rc) return fail(rc, "k is too big");
+    std::vector<int32_t> status(n_blocks);
+    std::vector<uint32_t> idx;
+    double total = 0;
+    for (uint32_t it = 0; it < std::max<uint32_t>(iters, 1); ++it) {
+        const auto t0 = std::chrono::steady_clock::now();
+        DecodeJob j;
+        j.p = p; j.T = T; j.n_blocks = n_blocks; j.erased = erased; j.n_repair = n_repair; j.repair_esi = repair_esi;
+        j.status = status.data();
+        // decode_begin's host part (Async: every received repair offered), then decode_pass's
+        if ((rc = decode_args(&j, n_erased, Fin::Async))) return rc;
+        DecodePlan& pl = decode_plan_scratch();
+        if (!j.blk_map.empty()) {
+            if ((rc = plan_decode(p, n_blocks, j.eoff, j.roff, repair_esi, j.cnt, j.blk_map, false, &pl, decode_mx_hint(j))))
+                return rc;
+            if (idx.size() < pl.n_idx) idx.resize(pl.n_idx);  // (the engine writes into pinned staging)
+            fill_decode_idx(pl, n_blocks, j.eoff, erased, j.roff, repair_esi, j.cnt, j.blk_map, status.data(), idx.data());
+        }
+        const auto t1 = std::chrono::steady_clock::now();
+        if (it) total += std::chrono::duration<double, std::micro>(t1 - t0).count();  // the first call warms up
+        if (n_idx_words) *n_idx_words = j.blk_map.empty() ? 0u : (uint32_t)pl.n_idx;
+    }
+    if (us_per_call) *us_per_call = iters > 1 ? total / (iters - 1) : total;
     return RQ_OK;
 }
 

@@ -43,7 +43,7 @@ EXPORTED = (
     "rq_debug_colprog_eval", "rq_debug_colprog_emulate", "rq_debug_colprog_assemble", "rq_debug_decode_margin",
     "rq_decode_blocks_host", "rq_host_alloc", "rq_host_free", "rq_debug_colprog_passes",
     "rq_debug_shard_plan", "rq_debug_virtual_shards", "rq_debug_tuple", "rq_stream_release", "rq_shutdown",
-    "rq_launch_timing", "rq_launch_time", "rq_debug_pair_emulate", "rq_debug_dma4_emulate",
+    "rq_launch_timing", "rq_launch_time", "rq_debug_pair_emulate", "rq_debug_dma4_emulate", "rq_debug_decode_plan",
 )
 
 
@@ -176,6 +176,8 @@ def lib():
             "rq_launch_time": ([ctypes.POINTER(ctypes.c_double), u32p, ctypes.c_int], ctypes.c_int),
             "rq_debug_pair_emulate": ([ctypes.c_uint32, ctypes.c_uint32, u32p, ctypes.c_uint32, vp, vp, u32p, u32p,
                                        ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+            "rq_debug_decode_plan": ([ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, u32p, u32p, u32p, u32p, ctypes.c_uint32,
+                                      ctypes.POINTER(ctypes.c_double), u32p], ctypes.c_int),
             "rq_debug_dma4_emulate": ([ctypes.c_uint32, ctypes.c_uint32, u32p, ctypes.c_uint32, vp, vp, ctypes.c_uint32,
                                        ctypes.c_uint32, u32p, ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
         }
@@ -526,6 +528,16 @@ class DecodeBatch:
                           data_stride=data.stride(0), n_erased=ne, erased=er, n_repair=nr, repair_esi=re_,
                           repair=repair.data_ptr(), status=status.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
                           stream=_stream_ptr(stream))
+
+    def host_plan_us(self, iters=20):
+        """rq_debug_decode_plan: mean host time (us) of one async call's host side on these arrays (no
+        device work); returns (us, descriptor words)."""
+        us = ctypes.c_double(0)
+        n = ctypes.c_uint32(0)
+        ne, er, nr, re_ = self._ptrs
+        _check(lib().rq_debug_decode_plan(self.T, self.K, self.n_blocks, ne, er, nr, re_, iters, ctypes.byref(us),
+                                          ctypes.byref(n)))
+        return us.value, n.value
 
     def run(self, data, repair, stream=None):
         """rq_decode_batch: synchronous, returns the status array."""

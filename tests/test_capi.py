@@ -5,6 +5,7 @@ import ctypes
 import re
 from pathlib import Path
 
+import numpy as np
 import pytest
 
 ROOT = Path(__file__).resolve().parent.parent
@@ -13,7 +14,7 @@ ROOT = Path(__file__).resolve().parent.parent
 def header_functions():
     txt = (ROOT / "include/rqhip.h").read_text()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b(rq_[a-z_]+)\s*\(", txt)))
+    return sorted(set(re.findall(r"\b(rq_\w+)\s*\(", txt)))
 
 
 def test_header_symbols_exported(rq):
@@ -87,3 +88,39 @@ def test_device_paths_fail_loudly_without_gpu(rq):
     with pytest.raises(rq.RaptorQError) as ei:
         rq.decode_batch_host(db, np.zeros((2, 64 * 64), np.uint8), np.zeros((2, 64), np.uint8))
     assert ei.value.code == rq.RQ_ERR_DEVICE
+
+
+def _config3_batch(rq, n_blocks=1024, seed=1):
+    K, N = 1024, 1100
+    rng = np.random.default_rng(seed)
+    el, rl = [], []
+    for _ in range(n_blocks):
+        lost = set(rng.choice(N, 55, replace=False).tolist())
+        el.append(sorted(x for x in lost if x < K))
+        rl.append([x for x in range(K, N) if x not in lost])
+    return rq.DecodeBatch(K, 1200, el, rl)
+
+
+def test_decode_host_plan_is_bounded(rq):
+    """The host side of one async decode call on the config-3 descriptors (1 024 blocks, 55 of 1 100
+    symbols lost each): argument checks, the union of the candidate repairs and the
+    descriptor words, with nothing cached across calls.  The word count is the layout's; the time bound
+    is loose here (a shared container CPU: ~90 us measured) -- the GPU box's figure is in DESIGN.md."""
+    db = _config3_batch(rq)
+    us, words = db.host_plan_us(20)
+    nb = db.n_blocks
+    n_er, n_rep = int(db.n_erased.sum()), int(db.n_repair.sum())
+    assert words == nb + 2 * (nb + 1) + nb + n_er + n_rep + nb + 2 * nb
+    assert 0 < us < 2000, us
+
+
+def test_decode_host_plan_argument_errors(rq):
+    """Out-of-range ESIs fail before any status is written (checked over the whole arrays at once)."""
+    db = _config3_batch(rq, n_blocks=4)
+    db.repair_esi[3] = 5  # a repair ESI below K
+    with pytest.raises(rq.RaptorQError):
+        db.host_plan_us(1)
+    db = _config3_batch(rq, n_blocks=4)
+    db.erased[0] = 1024  # an erased ESI at K
+    with pytest.raises(rq.RaptorQError):
+        db.host_plan_us(1)
