@@ -91,6 +91,7 @@ struct ApplyArgs {
     uint64_t data_stride;
     uint32_t T;
     uint32_t max_e;             // largest e of the batch (slice sizing)
+    uint32_t out_sc1 = 0;       // 1: recovered rows stored sc1 (written through, not left dirty in L2)
 };
 
 // Launchers (rq_kernels.hip).  Return hipError_t as int.

@@ -121,6 +121,17 @@ struct HostBuf {
 
 // Per-stream workspaces: kernels of calls on different streams may run concurrently, so every
 // stream gets its own scratch / index / syndrome buffers (calls on one stream are ordered).
+// Flags of the engine's own device-side events (`last`, the side-stream `cpy`): nobody on the host reads
+// memory after them, so the marker needs no system-scope release (RQHIP_EV_NOFENCE=1 in experiments
+// builds; measured in profiles/r04e).
+unsigned internal_event_flags() {
+    static const unsigned f = [] {
+        const char* e = knob("RQHIP_EV_NOFENCE");
+        return hipEventDisableTiming | (e && e[0] == '1' ? hipEventDisableSystemFence : 0u);
+    }();
+    return f;
+}
+
 struct Workspace {
     DevBuf r0, xb, xp, gws, scratch;
     DevBuf pk;                      // host-memory decode: recovered rows, packed for the D2H
@@ -148,7 +159,7 @@ struct Workspace {
     // never synchronises the device while the context lock is held
     hipEvent_t last = nullptr;
     int mark(void* stream) {
-        if (!last && hipEventCreateWithFlags(&last, hipEventDisableTiming) != hipSuccess) {
+        if (!last && hipEventCreateWithFlags(&last, internal_event_flags()) != hipSuccess) {
             last = nullptr;
             return fail(RQ_ERR_DEVICE, "hipEventCreate failed");
         }
@@ -1126,8 +1137,8 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     if (side && !w->cs) {  // events first: a half-built pair is destroyed, never published
         hipEvent_t ev[2] = {nullptr, nullptr};
         hipStream_t cs = nullptr;
-        bool ok = hipEventCreateWithFlags(&ev[0], hipEventDisableTiming) == hipSuccess &&
-                  hipEventCreateWithFlags(&ev[1], hipEventDisableTiming) == hipSuccess &&
+        bool ok = hipEventCreateWithFlags(&ev[0], internal_event_flags()) == hipSuccess &&
+                  hipEventCreateWithFlags(&ev[1], internal_event_flags()) == hipSuccess &&
                   hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) == hipSuccess;
         if (!ok) {
             for (hipEvent_t e : ev)
@@ -1213,9 +1224,14 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     z.T = T; z.n = nz; z.pack = nullptr;
     // 2) per-block solve (after the side stream's descriptor upload): on the side stream, or after the
     //    syndrome program on the caller's
+    // The caller's stream waits for the upload either before the syndrome program (RQHIP_DESC_WAIT=1 in
+    // experiments builds: the upload has long finished by then, the wait is the queue's barrier packet)
+    // or between it and the solve (the default).
+    static const bool wait_early = [] { const char* e = knob("RQHIP_DESC_WAIT"); return e && e[0] == '1'; }();
+    if (side && !beside && wait_early) HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, w->cpy[set], 0));
     if (!beside && (rc = launch_col(ctx, k, T, n_blocks, data, data_stride, w->r0.p, (uint64_t)uni.size() * T, stream)))
         return rc;
-    if (side && !beside) HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, w->cpy[set], 0));
+    if (side && !beside && !wait_early) HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, w->cpy[set], 0));
     SolveArgs s;
     s.blk_map = di + o_map;
     s.erased_off = di + o_eoff;
@@ -1263,6 +1279,10 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     ap.data_stride = data_stride;
     ap.T = T;
     ap.max_e = max_e;
+    // recovered-row store policy (RQHIP_APPLY_SC1=1 in experiments builds: written through, so the
+    // kernel boundary after the apply has no dirty lines to write back)
+    static const uint32_t apply_sc1 = [] { const char* e = knob("RQHIP_APPLY_SC1"); return e && e[0] == '1' ? 1u : 0u; }();
+    ap.out_sc1 = apply_sc1;
     if (launch_apply(ap, (T / 4 + 63) / 64, nw, stream)) return fail(RQ_ERR_DEVICE, "k_apply launch failed");
     const size_t pack_bytes = (size_t)nz * T;
     if (po) {

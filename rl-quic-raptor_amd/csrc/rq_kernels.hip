@@ -1227,7 +1227,10 @@ k_apply(ApplyArgs a, uint32_t n_units, uint32_t np, uint32_t MC) {
             const int go = __builtin_amdgcn_readlane((int)erow, k);
 #pragma unroll
             for (int j = 0; j < CPL; ++j)
-                if (live[j]) __builtin_amdgcn_raw_buffer_store_b32(acc[k][j], rsD, (int)vo[j], go, 0);
+                if (live[j]) {
+                    if (a.out_sc1) __builtin_amdgcn_raw_buffer_store_b32(acc[k][j], rsD, (int)vo[j], go, 16);
+                    else __builtin_amdgcn_raw_buffer_store_b32(acc[k][j], rsD, (int)vo[j], go, 0);
+                }
         }
     }
 }
