@@ -811,7 +811,10 @@ static void emit_colprog_body(const MProg& mp, uint32_t W, std::string& s) {
     // extra outstanding scalar load.)
     const std::vector<uint32_t> src_rows = colprog_src_rows(mp);
     const uint32_t n_groups = (uint32_t)((src_rows.size() + 15) / 16);
-    if (n_groups) line("s_load_dwordx16 s[64:79], s[50:51], 0x0");
+    // experiments: RQHIP_SRC_SMUL=1 forms each source load's soffset with an s_mul (one SALU per load)
+    // instead (no lgkmcnt(0) per 16 loads, which also drains the LDS operations in flight)
+    static const bool src_smul = [] { const char* e = knob("RQHIP_SRC_SMUL"); return e && e[0] == '1'; }();
+    if (n_groups && !src_smul) line("s_load_dwordx16 s[64:79], s[50:51], 0x0");
     uint32_t src_j = 0;
     int sr = 0;
     // s40..s47 rotate as short-lived SALU temporaries; at W > 1, s41 holds the wave's LDS base for the
@@ -855,6 +858,15 @@ static void emit_colprog_body(const MProg& mp, uint32_t W, std::string& s) {
                 if (diag & 4) {
                     std::snprintf(buf, sizeof buf, is_agpr(m.d) ? "v_accvgpr_write_b32 %s, v%d" : "v_mov_b32_e32 %s, v%d",
                                   R(m.d), V_SRCOFF);
+                    line(buf);
+                    break;
+                }
+                if (src_smul) {
+                    ++src_j;
+                    const int q = srot();
+                    std::snprintf(buf, sizeof buf, "s_mul_i32 s%d, s12, %u", q, m.imm); line(buf);
+                    std::snprintf(buf, sizeof buf, "buffer_load_dword %s, v%d, s[24:27], s%d offen%s", R(m.d), V_SRCOFF, q,
+                                  pol.src.c_str());
                     line(buf);
                     break;
                 }
