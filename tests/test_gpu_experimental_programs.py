@@ -1,0 +1,52 @@
+"""The column-program variants the experiments library keeps behind knobs, on the GPU: the two-wave
+(pair) program with dword loads, with four-row staging of its load wave, with HDPC rows moved to the
+load wave, and the single-wave program with four-row staging (profiles/r04_pair).
+They are not the shipped programs (measured slower at K=1024), but they must stay bit-exact: each runs
+in its own process (the knobs are read once per process) through tools/colbench.py, which checks the
+first and last block of a batch against the oracle, or through bench.py, which checks a whole
+encode + decode step.  Skipped when the experiments library was not built (__graft_entry__.build()
+builds it)."""
+import os
+import re
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+EXP = ROOT / "rl-quic-raptor_amd" / "build_exp" / "librqhip.so"
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not EXP.exists(), reason="experiments library not built (tools/build_experiments.sh)")]
+
+VARIANTS = {
+    "pair_dword": {"RQHIP_PAIR": "1", "RQHIP_PAIR_CFG": "6,16,192,0"},
+    "pair_staged": {"RQHIP_PAIR": "1"},
+    "pair_hdpc3": {"RQHIP_PAIR": "1", "RQHIP_PAIR_CFG": "6,16,192,32,1200,3"},
+    "single_staged": {"RQHIP_PAIR": "0", "RQHIP_DMA4": "8"},
+}
+
+
+def _run(args, knobs, timeout=150):
+    env = dict(os.environ, RQHIP_LIB=str(EXP), **knobs)
+    r = subprocess.run([sys.executable] + args, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    return r.stdout
+
+
+@pytest.mark.parametrize("name", sorted(VARIANTS))
+@pytest.mark.parametrize("K,N,B", [(1024, 1100, 24), (2048, 2260, 6)])
+def test_variant_encode_matches_oracle(name, K, N, B):
+    out = _run(["tools/colbench.py", str(K), "1200", str(N), str(B), "1"], VARIANTS[name])
+    counts = [int(m) for m in re.findall(r"mismatching repairs: \[\] (\d+)", out)]
+    assert counts == [0, 0], out
+
+
+@pytest.mark.parametrize("name", ["pair_staged", "single_staged"])
+def test_variant_encode_decode_step(name):
+    """A full config-3 step (1 024 blocks) through bench.py on the experiments library: the decode's
+    syndrome program is the same variant; bench.py asserts every recovered block bit-exact and the
+    post-timing bytes + statuses."""
+    out = _run(["tools/experiments/bench_exp.py", "--steps", "1", "--warmup", "0", "--cpu-sample", "0"], VARIANTS[name])
+    assert '"decode_ok_fraction": 1.0' in out and '"post_timing_check": "bytes+statuses"' in out, out
