@@ -733,7 +733,8 @@ struct Policy {
 // 2 drops LDS spill traffic, 4 replaces source loads by register writes, 8 drops output stores,
 // 16 loads source rows in increasing row order (wrong rows; measures the cost of the random order),
 // 32 drops the XOR / xtime instructions (memory traffic and register moves only), 64 drops the vmcnt
-// waits (loads then race their uses: wrong bytes, but every address stays valid).
+// waits (loads then race their uses: wrong bytes, but every address stays valid), 128 drops the pair
+// programs' barriers (the two waves run decoupled: wrong bytes, same instructions, nothing waits).
 static uint32_t diag_mask() {
     const char* e = knob("RQHIP_DIAG");
     return e ? (uint32_t)std::atoi(e) : 0u;
@@ -972,6 +973,7 @@ static void emit_colprog_body(const MProg& mp, uint32_t W, std::string& s) {
                 break;
             }
             case MI_BAR:
+                if (diag & 128) break;
                 line("s_barrier");
                 break;
             case MI_WAITL:
@@ -1554,6 +1556,7 @@ bool emulate_pair(const PairProg& pp, const uint8_t* src, uint32_t T, uint8_t* o
 }
 
 std::string emit_pair_asm(const PairProg& pp, const std::string& kname) {
+    static const uint32_t diag = diag_mask();
     const MProg& A = pp.A;
     const MProg& B = pp.B;
     const Reserved rv(A.n_vgpr);
@@ -1651,13 +1654,13 @@ std::string emit_pair_asm(const PairProg& pp, const std::string& kname) {
             line(buf);
         }
         if (is_a && dma4) emit_dma4_prologue(A, rv, s);
-        if (!is_a)  // B trails A by `lag` transfers: its first `lag` barriers pair with A's first transfers
+        if (!is_a && !(diag & 128))  // B trails A by `lag` transfers: its first `lag` barriers pair with A's first
             for (uint32_t j = 0; j < pp.lag; ++j) line("s_barrier");
         s += std::string(".L") + tag + "_loop:\n";
         line("s_cmp_lt_u32 s52, s48");
         std::snprintf(buf, sizeof buf, "s_cbranch_scc1 .L%s_body", tag);
         line(buf);
-        if (is_a)  // A's last `lag` barriers pair with B's barriers of the last item's last transfers
+        if (is_a && !(diag & 128))  // A's last `lag` barriers pair with B's of the last item's last transfers
             for (uint32_t j = 0; j < pp.lag; ++j) line("s_barrier");
         line("s_endpgm");
         s += std::string(".L") + tag + "_body:\n";
