@@ -738,8 +738,14 @@ int launch_col(DevCtx* ctx, ColKernel* k, uint32_t T, uint32_t n_blocks, const v
     const uint32_t max_wg = std::min(max_iters, resident);
     const size_t spw = (size_t)std::max<uint32_t>(k->n_slots, 1) * 256;
     int rc;
-    Workspace* w = ctx->wsp(stream);
-    if ((rc = w->scratch.ensure(spw * max_wg * Wi))) return rc;  // a pair's wave A alone uses scratch
+    // A program with no global-scratch slot (K=1024 and below since round 3) touches no workspace: no
+    // scratch buffer, and no `last` marker on the stream after it (each marker costs the stream a few
+    // us between kernels, profiles/r04e).
+    Workspace* w = nullptr;
+    if (k->n_slots) {
+        w = ctx->wsp(stream);
+        if ((rc = w->scratch.ensure(spw * max_wg * Wi))) return rc;  // a pair's wave A alone uses scratch
+    }
     auto& tab = k->row_off[T];
     if (!tab) {  // once per (program, T): the source loads' soffsets, padded to whole 16-entry groups
         std::unique_ptr<DevBuf> b(new DevBuf());
@@ -759,7 +765,7 @@ int launch_col(DevCtx* ctx, ColKernel* k, uint32_t T, uint32_t n_blocks, const v
         std::memset(&a, 0, sizeof a);
         a.src = (uint64_t)(uintptr_t)src + (uint64_t)b0 * src_stride;
         a.out = (uint64_t)(uintptr_t)out + (uint64_t)b0 * out_stride;
-        a.scratch = (uint64_t)(uintptr_t)w->scratch.p;
+        a.scratch = w ? (uint64_t)(uintptr_t)w->scratch.p : 0;
         a.src_stride = (uint32_t)src_stride;
         // the source resource's size: the launch's rows, so a wrong offset reads 0 instead of faulting
         a.src_bytes = (uint32_t)std::min<uint64_t>(0xFFFFFFFFull, (uint64_t)(nb - 1) * src_stride + (uint64_t)k->row_end * T);
@@ -801,7 +807,7 @@ int launch_col(DevCtx* ctx, ColKernel* k, uint32_t T, uint32_t n_blocks, const v
         }
         HIP_TRY(hipModuleLaunchKernel(k->fn, wgs, 1, 1, 64 * Wg, 1, 1, 0, (hipStream_t)stream, nullptr, cfg));
     }
-    return w->mark(stream);
+    return w ? w->mark(stream) : RQ_OK;
 }
 
 // Encode `n_blocks` device-resident blocks: outputs esi[0..n_esi) of every block.
