@@ -752,6 +752,136 @@ __global__ void __launch_bounds__(64) k_solve_reg(SolveArgs a) {
     if (lane == 0) a.status[b] = 1;
 }
 
+// One wave per block, rows in registers, for e <= 64 on the first e + margin (<= 64) received
+// repairs: a lean first-pass solver (RQHIP_SOLVE_LEAN=1 in experiments builds).  Lane j owns received
+// repair j as 32 dwords (e coefficient bytes, then the identity part at byte e + j).  Each step k takes
+// the lowest unused row with a nonzero coefficient in column k (ballot); the pivot lane posts its live
+// dwords to LDS, every lane reads them back (one broadcast address per b128) and folds c_j times the
+// pivot row into its own (c_j = f_j / f_p, the pivot lane 1 ^ 1/f_p, which leaves row_p / f_p), with
+// c_j's v_perm tables read from an LDS copy of kPerm by log c_j and the pivot dwords made scalar, so
+// the selectors are SALU work.  Against k_solve_reg: no per-step table build (~70 VALU), no v_readlane
+// per pivot dword; against k_solve_pq: one wave and ~9 KB of LDS per block and no barrier, so blocks
+// also fit beside the syndrome program's waves.
+__global__ void __launch_bounds__(64) k_solve_lean(SolveArgs a) {
+    __shared__ __attribute__((aligned(4))) uint8_t ex[512], lg[256];
+    __shared__ uint8_t pivl[64];
+    __shared__ __attribute__((aligned(16))) uint4 prow_s[8];  // the pivot row's live dwords, by quad
+    // the coefficient tables and pivot infos during the elimination; the final rows after it
+    constexpr uint32_t RS = 33;  // final row stride (dwords; no bank conflicts)
+    __shared__ __attribute__((aligned(16))) uint32_t un[64 * RS];
+    uint4* tlA = reinterpret_cast<uint4*>(un);    // [255]
+    uint32_t* tlB = un + 4 * 255;                 // [255]
+    uint32_t* pinfo = tlB + 255;                  // [256]: log f | log(1 ^ 1/f) << 8 | (1 ^ 1/f != 0) << 16
+    const uint32_t lane = threadIdx.x;
+    if (a.status_init)  // the host-decided statuses (disjoint from the solver's blocks, ST_PENDING)
+        for (uint32_t i = blockIdx.x * 64 + lane; i < a.n_all; i += gridDim.x * 64)
+            if (a.status_init[i] != ST_PENDING) a.status[i] = a.status_init[i];
+    const uint32_t b = a.blk_map[blockIdx.x];
+    const uint32_t e = a.erased_off[b + 1] - a.erased_off[b];
+    const uint32_t nr = a.rep_cnt[b];
+    if (e > 64) {
+        if (lane == 0) a.status[b] = ST_FALLBACK;
+        return;
+    }
+    const uint32_t nrow = a.row_margin ? min(min(nr, 64u), e + a.row_margin) : min(nr, 64u);
+    const uint32_t* E = a.erased + a.erased_off[b];
+    const uint32_t* U = a.rep_uidx + a.rep_off[b];
+    gf_tables_copy(ex, lg);
+    for (uint32_t l = lane; l < 255; l += 64) {
+        tlA[l] = make_uint4(kPerm.A[l][0], kPerm.A[l][1], kPerm.A[l][2], kPerm.A[l][3]);
+        tlB[l] = kPerm.B[l];
+    }
+    uint32_t row[32];
+#pragma unroll
+    for (int w = 0; w < 32; ++w) row[w] = 0;
+    if (lane < nrow) {  // every byte load of the row in flight at once
+        const uint8_t* mr = a.mrep + (size_t)U[lane] * a.mrep_stride;
+#pragma unroll
+        for (int w = 0; w < 16; ++w)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if ((uint32_t)(4 * w + i) < e) row[w] |= (uint32_t)mr[E[4 * w + i]] << (8 * i);
+        const uint32_t pos = e + lane;
+#pragma unroll
+        for (int w = 0; w < 32; ++w)
+            if ((pos >> 2) == (uint32_t)w) row[w] |= 1u << (8 * (pos & 3));
+    }
+    __syncthreads();  // ex / lg
+    for (uint32_t x = lane; x < 256; x += 64) {
+        uint32_t v = 0;
+        if (x) {
+            const uint32_t lx = lg[x], cp = 1u ^ ex[255u - lx];
+            v = lx | (cp ? (uint32_t)lg[cp] << 8 | 1u << 16 : 0u);
+        }
+        pinfo[x] = v;
+    }
+    __syncthreads();  // tables and pinfo
+    bool used = lane >= nrow;
+    const uint32_t q1 = (e + nrow + 3) >> 2;  // live dwords
+    for (uint32_t k = 0; k < e; ++k) {
+        const uint32_t W = k >> 2;
+        uint32_t rw = 0;
+#pragma unroll
+        for (int w = 0; w < 16; ++w)
+            if ((uint32_t)w == W) rw = row[w];
+        const uint32_t f = (rw >> (8 * (k & 3))) & 0xFFu;
+        const uint64_t bal = __ballot(f != 0 && !used);
+        if (bal == 0) {  // rank-deficient on these rows (uniform)
+            if (lane == 0) a.status[b] = (nr > nrow) ? ST_FALLBACK : 0;
+            return;
+        }
+        const uint32_t p = (uint32_t)__ffsll((unsigned long long)bal) - 1;
+        const bool me = lane == p;
+        used |= me;
+        const uint32_t pif = pinfo[f];
+        // the pivot lane posts its live dwords (quads from W / 4; columns < k are zero there)
+        const uint32_t w4 = W >> 2, q4 = (q1 + 3) >> 2;
+        if (me) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if ((uint32_t)j >= w4 && (uint32_t)j < q4)
+                    prow_s[j] = make_uint4(row[4 * j], row[4 * j + 1], row[4 * j + 2], row[4 * j + 3]);
+        }
+        const uint32_t pip = (uint32_t)__builtin_amdgcn_readlane((int)pif, (int)p);
+        const uint32_t ilgp = 255u - (pip & 0xFFu);
+        uint32_t l = me ? (pif >> 8) & 0xFFu : (pif & 0xFFu) + ilgp;
+        l = l >= 255u ? l - 255u : l;
+        const bool act = me ? (pif >> 16) != 0 : f != 0;
+        const uint4 A = tlA[act ? l : 0];
+        const uint32_t B = tlB[act ? l : 0];
+        __builtin_amdgcn_wave_barrier();  // (LDS operations of one wave complete in order)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if ((uint32_t)j < w4 || (uint32_t)j >= q4) continue;  // uniform
+            const uint4 P = prow_s[j];
+            const uint32_t px[4] = {(uint32_t)__builtin_amdgcn_readfirstlane(P.x), (uint32_t)__builtin_amdgcn_readfirstlane(P.y),
+                                    (uint32_t)__builtin_amdgcn_readfirstlane(P.z), (uint32_t)__builtin_amdgcn_readfirstlane(P.w)};
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                const uint32_t m = act ? perm_mul(A, B, px[d]) : 0u;
+                row[4 * j + d] ^= m;
+            }
+        }
+        if (lane == 0) pivl[k] = (uint8_t)p;
+        __builtin_amdgcn_wave_barrier();
+    }
+    // the final rows into LDS (over the tables), X[k][m] = identity byte (e + piv_m) of pivot row piv_k
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < 32; ++w) un[lane * RS + w] = row[w];
+    __syncthreads();
+    uint8_t* xc = a.xcoef + 64ull * a.xoff[blockIdx.x];
+    const uint32_t xs = x_stride(e);
+    uint16_t* XP = a.xpiv + a.erased_off[b];
+    for (uint32_t m = lane; m < e; m += 64) XP[m] = pivl[m];
+    const uint8_t* rb = reinterpret_cast<const uint8_t*>(un);
+    for (uint32_t m = 0; m < e; ++m) {  // row m of X: one byte per lane, no index division
+        const uint32_t pm = pivl[m];
+        for (uint32_t k = lane; k < e; k += 64) xc[m * xs + k] = rb[pivl[k] * (RS * 4) + e + pm];
+    }
+    if (lane == 0) a.status[b] = 1;
+}
+
 // General solver for the blocks the fast solvers deferred: any e, every received repair.  The
 // received rows are taken in order and reduced against a Gauss-Jordan basis of the rows kept so far
 // (basis row i: pivot column pc[i], coefficients zero on every other pivot column, then the
@@ -907,6 +1037,16 @@ static bool solve_pq() {
 #endif
 }
 
+// the lean one-wave first-pass solver (k_solve_lean; RQHIP_SOLVE_LEAN=1 in experiments builds)
+static bool solve_lean() {
+#ifdef RQHIP_EXPERIMENTS
+    static const bool on = [] { const char* e = std::getenv("RQHIP_SOLVE_LEAN"); return e && e[0] == '1'; }();
+    return on;
+#else
+    return false;
+#endif
+}
+
 static int solve_nw() {
 #ifdef RQHIP_EXPERIMENTS
     static const int nw = [] {
@@ -931,12 +1071,14 @@ int launch_solve(const SolveArgs& a_in, uint32_t n_blocks, bool need_general, bo
 #endif
     SolveArgs a = first;
     a.status_init = nullptr;
-    const bool pm_first = solve_nw() == 8 || (solve_pm() && (solve_nw() == 1 || solve_nw() == 2 || solve_nw() == 4));
+    const bool pm_first = solve_lean() || solve_nw() == 8 ||
+                          (solve_pm() && (solve_nw() == 1 || solve_nw() == 2 || solve_nw() == 4));
     if (a_in.status_init && !pm_first &&
         hipMemcpyAsync(a.status, a_in.status_init, (size_t)a_in.n_all * 4, hipMemcpyHostToDevice,
                        (hipStream_t)stream) != hipSuccess)
         return (int)hipGetLastError();
-    switch (solve_nw()) {
+    if (solve_lean()) hipLaunchKernelGGL(k_solve_lean, dim3(n_blocks), dim3(64), 0, (hipStream_t)stream, first);
+    else switch (solve_nw()) {
         case 1:
             if (solve_pm() && solve_pq()) hipLaunchKernelGGL((k_solve_pq<1, 1>), dim3(n_blocks), dim3(64), 0, (hipStream_t)stream, first);
             else if (solve_pm()) hipLaunchKernelGGL((k_solve_pm<1, 1, true>), dim3(n_blocks), dim3(64), 0, (hipStream_t)stream, first);
