@@ -12,6 +12,7 @@
 // sum_k M[j][k] x_k with M[j][k] = mrep[j][E_k] (the same program run once on the identity
 // payload).  Rank(M) = |E| <=> the reference's system is full rank, and x_E is unique.
 #include <hip/hip_runtime.h>
+#include <type_traits>
 
 #include <algorithm>
 #include <cstdint>
@@ -500,7 +501,10 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pm(SolveArgs a) {
 // log is then a v_readlane of the pivot lane's entry), and loads all its pivot-row quads at once: a
 // step is three dependent LDS round trips (f, pinfo[f], the tables) plus the barrier, where the
 // quad-at-a-time loop had two more per quad.
-template <int RPL, int NW>
+// PF (experiments, RQHIP_SOLVE_PF=1): the column buffer carries each row's pinfo word instead of its
+// coefficient byte, looked up by the wave that writes it while it updates its other quads, so a step
+// starts one dependent LDS round trip later in its chain.
+template <int RPL, int NW, bool PF = false>
 __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
     constexpr uint32_t NT = 64 * NW;
     constexpr uint32_t NROWS = 64 * RPL, SW = 32 * RPL + 4;  // rows, row stride (dwords)
@@ -517,7 +521,8 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
     // updates the quad holding column k + 1 writes fcol[(k + 1) & 1] from its registers.  Reading
     // column k from `rows` instead would race with wave 0, which rewrites quad k / 16 in the same step
     // (a late wave then sees column k already eliminated: a wrong X with status 1).
-    __shared__ uint8_t fcol[2][NROWS];
+    using FC = typename std::conditional<PF, uint32_t, uint8_t>::type;
+    __shared__ FC fcol[2][NROWS];
     const uint32_t b = a.blk_map[blockIdx.x];
     const uint32_t tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
     if (a.status_init)
@@ -552,17 +557,20 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
             if (g == 0) myb[e + row] = 1;
         }
     }
-    // pinfo[f] = log f | log(1 ^ 1/f) << 8 | (1 ^ 1/f != 0) << 16; pinfo[0] = 0
+    // pinfo[f] = log f | log(1 ^ 1/f) << 8 | (1 ^ 1/f != 0) << 16 | (f != 0) << 17; pinfo[0] = 0
     for (uint32_t x = tid; x < 256; x += NT) {
         uint32_t v = 0;
         if (x) {
             const uint32_t lx = lg[x], cp = 1u ^ ex[255u - lx];
-            v = lx | (cp ? (uint32_t)lg[cp] << 8 | 1u << 16 : 0u);
+            v = lx | (cp ? (uint32_t)lg[cp] << 8 | 1u << 16 : 0u) | 1u << 17;
         }
         pinfo[x] = v;
     }
     __syncthreads();
-    for (uint32_t r = tid; r < NROWS; r += NT) fcol[0][r] = (uint8_t)(rows[r * SW] & 0xFFu);
+    for (uint32_t r = tid; r < NROWS; r += NT) {
+        const uint32_t f0 = rows[r * SW] & 0xFFu;
+        fcol[0][r] = PF ? (FC)pinfo[f0] : (FC)f0;
+    }
     __syncthreads();
     const uint32_t q1 = (e + nrow + 15) >> 4;  // quads holding live columns
     bool used[RPL];
@@ -582,11 +590,19 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
             for (int q = 0; q < RPL; ++q)
                 R[q][j] = reinterpret_cast<const uint4*>(rows + (lane + 64 * q) * SW)[min(w0 + NW * j, 8u * RPL)];
         uint32_t f[RPL], pif[RPL];
+        if constexpr (PF) {  // nonzero-ness from the pinfo word (bit 17)
 #pragma unroll
-        for (int q = 0; q < RPL; ++q) f[q] = fcol[k & 1][lane + 64 * q];
-        // (2) pinfo of every row's coefficient, beside the ballot
+            for (int q = 0; q < RPL; ++q) {
+                pif[q] = fcol[k & 1][lane + 64 * q];
+                f[q] = (pif[q] >> 17) & 1u;
+            }
+        } else {
 #pragma unroll
-        for (int q = 0; q < RPL; ++q) pif[q] = pinfo[f[q]];
+            for (int q = 0; q < RPL; ++q) f[q] = fcol[k & 1][lane + 64 * q];
+            // (2) pinfo of every row's coefficient, beside the ballot
+#pragma unroll
+            for (int q = 0; q < RPL; ++q) pif[q] = pinfo[f[q]];
+        }
         uint32_t p = 0xFFFFFFFFu;
 #pragma unroll
         for (int q = RPL - 1; q >= 0; --q) {
@@ -617,7 +633,7 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
 #pragma unroll
         for (int q = 0; q < RPL; ++q) {
             const bool piv = lane + 64 * q == p;
-            act[q] = piv ? (pif[q] >> 16) != 0 : f[q] != 0;
+            act[q] = piv ? ((pif[q] >> 16) & 1u) != 0 : f[q] != 0;
             const uint32_t l = piv ? (pif[q] >> 8) & 0xFFu : (pif[q] & 0xFFu) + ilgp;  // < 510
             A[q] = tlA[l];
             B[q] = tlB[l];
@@ -642,7 +658,8 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
                     const uint4 v = act[q] ? r : R[q][j];
                     const uint32_t d = (kn >> 2) & 3u;
                     const uint32_t dw = d == 0 ? v.x : d == 1 ? v.y : d == 2 ? v.z : v.w;
-                    fcol[kn & 1][lane + 64 * q] = (uint8_t)(dw >> ((kn & 3u) * 8));
+                    const uint32_t fb = (dw >> ((kn & 3u) * 8)) & 0xFFu;
+                    fcol[kn & 1][lane + 64 * q] = PF ? (FC)pinfo[fb] : (FC)fb;
                 }
             }
         }
@@ -1037,6 +1054,16 @@ static bool solve_pq() {
 #endif
 }
 
+// k_solve_pq's column buffer with pinfo words (RQHIP_SOLVE_PF=1 in experiments builds)
+static bool solve_pf() {
+#ifdef RQHIP_EXPERIMENTS
+    static const bool on = [] { const char* e = std::getenv("RQHIP_SOLVE_PF"); return e && e[0] == '1'; }();
+    return on;
+#else
+    return false;
+#endif
+}
+
 // the lean one-wave first-pass solver (k_solve_lean; RQHIP_SOLVE_LEAN=1 in experiments builds)
 static bool solve_lean() {
 #ifdef RQHIP_EXPERIMENTS
@@ -1092,7 +1119,9 @@ int launch_solve(const SolveArgs& a_in, uint32_t n_blocks, bool need_general, bo
             else hipLaunchKernelGGL((k_solve_pm<1, 2, true>), dim3(n_blocks), dim3(128), 0, (hipStream_t)stream, first);
             break;
         case 4:
-            if (solve_pm() && solve_lut() && solve_pq())
+            if (solve_pm() && solve_lut() && solve_pq() && solve_pf())
+                hipLaunchKernelGGL((k_solve_pq<1, 4, true>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, first);
+            else if (solve_pm() && solve_lut() && solve_pq())
                 hipLaunchKernelGGL((k_solve_pq<1, 4>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, first);
             else if (solve_pm() && solve_lut())
                 hipLaunchKernelGGL((k_solve_pm<1, 4, true>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, first);
