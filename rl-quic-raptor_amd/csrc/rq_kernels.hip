@@ -557,12 +557,12 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
             if (g == 0) myb[e + row] = 1;
         }
     }
-    // pinfo[f] = log f | log(1 ^ 1/f) << 8 | (1 ^ 1/f != 0) << 16 | (f != 0) << 17; pinfo[0] = 0
+    // pinfo[f] = log f | log(1 ^ 1/f) << 8 | (1 ^ 1/f != 0) << 16 [| (f != 0) << 17 with PF]; pinfo[0] = 0
     for (uint32_t x = tid; x < 256; x += NT) {
         uint32_t v = 0;
         if (x) {
             const uint32_t lx = lg[x], cp = 1u ^ ex[255u - lx];
-            v = lx | (cp ? (uint32_t)lg[cp] << 8 | 1u << 16 : 0u) | 1u << 17;
+            v = lx | (cp ? (uint32_t)lg[cp] << 8 | 1u << 16 : 0u) | (PF ? 1u << 17 : 0u);
         }
         pinfo[x] = v;
     }
