@@ -113,3 +113,50 @@ def test_large_k_decode_round_trip(gpu, rq):
     st = rq.DecodeBatch(K, T, er, rl).run(data, rep)
     torch.cuda.synchronize()
     assert (st == 1).all() and torch.equal(data, src)
+
+
+def _sparse_case(gpu, oracle, K, T, nb, seed, lo, hi, skip_block=None):
+    """Blocks with scattered received repair ESIs in [lo, hi); block `skip_block` loses nothing (its
+    status is decided on the host, so it is not solved)."""
+    rng = np.random.default_rng(seed)
+    src = _src(gpu, nb, K, T, seed)
+    src_h = src.cpu().numpy()
+    er, rl, rows = [], [], []
+    for b in range(nb):
+        e = [] if b == skip_block else sorted(rng.choice(K, 3 + b, replace=False).tolist())
+        esis = sorted(set(rng.integers(lo, hi, 10 + b).tolist()))
+        ref = oracle.OracleEncoder(src_h[b].tobytes(), T)
+        er.append(e)
+        rl.append(esis)
+        rows.extend(ref.gen_symbol(x) for x in esis)
+    rep = torch.from_numpy(np.stack(rows)).to(gpu)
+    data = src.clone()
+    for b in range(nb):
+        for i in er[b]:
+            data[b, i * T:(i + 1) * T] = 0xC3
+    return src, data, rep, er, rl
+
+
+def test_sparse_repair_esis_decode_async(gpu, rq, oracle):
+    """The async path over a sparse union (every block offers all its received repairs, so the host
+    plan bounds the union by the argument check's maximum; the union is the exact sorted set)."""
+    K, T, nb = 64, 256, 5
+    src, data, rep, er, rl = _sparse_case(gpu, oracle, K, T, nb, 21, K, K + (1 << 18))
+    db = rq.DecodeBatch(K, T, er, rl)
+    st = db.run_async(data, rep)
+    torch.cuda.synchronize()
+    assert (st == 1).all()
+    assert torch.equal(data, src)
+
+
+def test_far_repair_esis_decode_unmapped_union(gpu, rq, oracle):
+    """Received repairs near the top of the 24-bit ESI space (more than 2^22 past K: the host plan
+    builds the union by sorting, union indices by binary search), one block with nothing lost
+    (not solved: its status comes from the host), sync and async."""
+    K, T, nb = 64, 256, 4
+    for run in ("run", "run_async"):
+        src, data, rep, er, rl = _sparse_case(gpu, oracle, K, T, nb, 33, (1 << 24) - 4096, 1 << 24, skip_block=1)
+        st = getattr(rq.DecodeBatch(K, T, er, rl), run)(data, rep)
+        torch.cuda.synchronize()
+        assert (st == 1).all(), (run, st)
+        assert torch.equal(data, src), run
