@@ -2,6 +2,7 @@
 #include "rq_colasm.hpp"
 
 #include <algorithm>
+#include <array>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -647,7 +648,13 @@ bool compile_colprog(const Params& p, const uint32_t* esi, uint32_t n_out, const
     // global scratch and at most 1.5x the instructions (measured: K=128 4 waves -24 %, K=256 2 waves
     // -13 %, K=512 spills at 2 waves and loses, profiles/r02ab).
     const size_t ins1 = mp->ins.size();
-    static const uint32_t cap[3][3] = {{122, 128, 78}, {58, 64, 39}, {26, 32, 19}};  // VGPR, AGPR, LDS slots
+    // VGPR, AGPR, LDS slots for 2 / 4 / 8 waves per SIMD; experiments: RQHIP_W3=1 adds 3 (170 registers)
+    static const std::vector<std::array<uint32_t, 3>> cap = [] {
+        std::vector<std::array<uint32_t, 3>> c{{122, 128, 78}, {58, 64, 39}, {26, 32, 19}};
+        if (const char* e = knob("RQHIP_W3"))
+            if (e[0] == '1') c.insert(c.begin() + 1, {78, 86, 52});
+        return c;
+    }();
     for (const auto& c : cap) {
         AllocOpts w = o;
         w.n_vgpr = std::min(o.n_vgpr, c[0]);
