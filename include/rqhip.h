@@ -196,6 +196,17 @@ int rq_debug_colprog_emulate(uint32_t K, uint32_t T, const uint32_t* esi, uint32
                              size_t* asm_len);
 /* Assemble the column program in process (amd_comgr) and return the code object size. */
 int rq_debug_colprog_assemble(uint32_t K, const uint32_t* esi, uint32_t n_out, size_t* code_bytes);
+/* Tests of the round-4 code-generation guards (rq_comgr.cpp check_registers, ColKernArgs::src_bytes):
+ * rq_debug_assemble runs `len` bytes of gfx950 assembly text through the in-process assembler with the
+ * register check that precedes every generated program (an architectural VGPR at or above
+ * .amdhsa_accum_offset, or an AGPR past the allocation, is RQ_ERR_PLAN with the register named in
+ * rq_last_error).  rq_debug_colprog_bound emulates the (K, esi) program on one block with the source
+ * buffer resource bounded at src_bytes (dwords at or beyond it read 0, as on the GPU) and returns in
+ * row_end 1 + the largest source row the program reads (the engine sets src_bytes = (blocks - 1) *
+ * stride + row_end * T). */
+int rq_debug_assemble(const char* src, size_t len, size_t* code_bytes);
+int rq_debug_colprog_bound(uint32_t K, uint32_t T, const uint32_t* esi, uint32_t n_out, const uint8_t* src,
+                           uint8_t* out, uint64_t src_bytes, uint32_t* row_end);
 /* The two-wave (pair) split of the output program for (K, esi) -- wave A: source loads, forward pass,
  * pushes; wave B: HDPC bit accumulation, dense part, outputs; an LDS ring between them -- evaluated on
  * the host over two consecutive items of one block (the ring carries across items as on the GPU), every

@@ -1278,6 +1278,7 @@ struct WaveEmu {
     const MProg& mp;
     const uint8_t* src;
     uint32_t T, Td;
+    uint64_t src_bytes = UINT64_MAX;  // buffer-resource extent: source dwords at or beyond it read 0
     uint8_t* out;
     std::string* err;
     std::vector<std::vector<uint32_t>> R, scr, lds;
@@ -1305,6 +1306,15 @@ struct WaveEmu {
         return r < 0 || ((pend[r] == 0 || pend[r] <= retired) && (lpend[r] == 0 || lpend[r] <= lretired));
     }
     bool vmem() { return ++seq - retired <= 63; }
+    // source row `row` into dst (T/4 dwords) through the bounded buffer resource
+    void read_row(uint32_t row, uint32_t* dst) const {
+        const uint64_t base = (uint64_t)row * T;
+        for (uint32_t c = 0; c < Td; ++c) {
+            const uint64_t at = base + 4ull * c;
+            if (at + 4 <= src_bytes) std::memcpy(&dst[c], src + at, 4);
+            else dst[c] = 0;
+        }
+    }
 
     bool step(size_t i, const MInst& m) {
         if (!ready(m.a) || !ready(m.b) || !ready(m.c)) return bad(i, "operand read before its load completed");
@@ -1328,7 +1338,7 @@ struct WaveEmu {
                 break;
             case MI_LDSRC:
                 if (m.imm >= mp.K) return bad(i, "source row >= K");
-                std::memcpy(R[m.d].data(), src + (size_t)m.imm * T, (size_t)Td * 4);
+                read_row(m.imm, R[m.d].data());
                 if (!vmem()) return bad(i, "more than 63 vector-memory operations outstanding");
                 pend[m.d] = seq;
                 break;
@@ -1381,7 +1391,7 @@ struct WaveEmu {
                 if (m.imm >= mp.K) return bad(i, "source row >= K");
                 if (m.d < 0 || (uint32_t)m.d >= mp.n_lds_slots) return bad(i, "DMA slot out of range");
                 if (lds_dma[m.d] > retired) return bad(i, "DMA over a pending DMA");
-                std::memcpy(lds[m.d].data(), src + (size_t)m.imm * T, (size_t)Td * 4);
+                read_row(m.imm, lds[m.d].data());
                 if (!vmem()) return bad(i, "more than 63 vector-memory operations outstanding");
                 lds_dma[m.d] = seq;
                 break;
@@ -1419,7 +1429,7 @@ struct WaveEmu {
                     if (lds_dma[sl] > retired) return bad(i, "DMA over a pending DMA");
                     const uint32_t row = mp.dma4_rows[(size_t)m.imm * 4 + g];
                     if (row >= mp.K) return bad(i, "source row >= K");
-                    std::memcpy(lds[sl].data(), src + (size_t)row * T, (size_t)Td * 4);
+                    read_row(row, lds[sl].data());
                 }
                 if (!vmem()) return bad(i, "more than 63 vector-memory operations outstanding");
                 for (uint32_t g = 0; g < 4; ++g) lds_dma[mp.dma4_slot0 + 4u * (uint32_t)m.d + g] = seq;
@@ -1448,8 +1458,10 @@ struct WaveEmu {
 };
 }  // namespace
 
-bool emulate_colprog(const MProg& mp, const uint8_t* src, uint32_t T, uint8_t* out, std::string* err) {
+bool emulate_colprog(const MProg& mp, const uint8_t* src, uint32_t T, uint8_t* out, std::string* err,
+                     uint64_t src_bytes) {
     WaveEmu w(mp, src, T, out, err);
+    w.src_bytes = src_bytes;
     return w.run();
 }
 

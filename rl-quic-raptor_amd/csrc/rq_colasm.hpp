@@ -158,7 +158,10 @@ uint32_t colprog_acc_off(const MProg& mp);
 
 // Executes the machine program on the host for one block (T/4 lanes), checking vmcnt waits and
 // scratch ordering as it goes.  Test infrastructure for the allocator, not a product path.
-bool emulate_colprog(const MProg& mp, const uint8_t* src, uint32_t T, uint8_t* out, std::string* err);
+// src_bytes: the source buffer resource's extent as the kernel sets it (ColKernArgs::src_bytes); a
+// source dword at or beyond it reads 0, as a bounds-checked buffer load does on the GPU.
+bool emulate_colprog(const MProg& mp, const uint8_t* src, uint32_t T, uint8_t* out, std::string* err,
+                     uint64_t src_bytes = UINT64_MAX);
 
 // ---- two-wave (pair) column programs (split_pair in rq_colprog.hpp) ----
 struct PairProg {

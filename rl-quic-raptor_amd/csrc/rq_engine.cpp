@@ -1983,6 +1983,30 @@ int rq_debug_colprog_assemble(uint32_t K, const uint32_t* esi, uint32_t n_out, s
     return RQ_OK;
 }
 
+int rq_debug_assemble(const char* src, size_t len, size_t* code_bytes) {
+    if (!src) return fail(RQ_ERR_BAD_ARG, "no source");
+    std::vector<char> co;
+    std::string err;
+    if (!comgr_assemble(std::string(src, len), &co, &err)) return fail(RQ_ERR_PLAN, err);
+    if (code_bytes) *code_bytes = co.size();
+    return RQ_OK;
+}
+
+int rq_debug_colprog_bound(uint32_t K, uint32_t T, const uint32_t* esi, uint32_t n_out, const uint8_t* src,
+                           uint8_t* out, uint64_t src_bytes, uint32_t* row_end) {
+    Params p;
+    int rc = params_for_K(K, &p);
+    if (rc) return fail(rc, "k is too big");
+    if (T == 0 || T % 4) return fail(RQ_ERR_BAD_ARG, "T must be a positive multiple of 4");
+    ColIR ir;
+    MProg mp;
+    std::string err;
+    if (!debug_compile(p, esi, n_out, alloc_options(), &ir, &mp, &err)) return fail(RQ_ERR_PLAN, err);
+    if (row_end) *row_end = colprog_row_end(mp);
+    if (src && out && !emulate_colprog(mp, src, T, out, &err, src_bytes)) return fail(RQ_ERR_PLAN, err);
+    return RQ_OK;
+}
+
 int rq_debug_decode_plan(uint32_t T, uint32_t K, uint32_t n_blocks, const uint32_t* n_erased, const uint32_t* erased,
                          const uint32_t* n_repair, const uint32_t* repair_esi, uint32_t iters, double* us_per_call,
                          uint32_t* n_idx_words) {

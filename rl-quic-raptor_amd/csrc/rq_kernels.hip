@@ -12,6 +12,8 @@
 // sum_k M[j][k] x_k with M[j][k] = mrep[j][E_k] (the same program run once on the identity
 // payload).  Rank(M) = |E| <=> the reference's system is full rank, and x_E is unique.
 #include <hip/hip_runtime.h>
+
+#include <mutex>
 #include <type_traits>
 
 #include <algorithm>
@@ -1143,11 +1145,14 @@ int launch_solve(const SolveArgs& a_in, uint32_t n_blocks, bool need_general, bo
         else hipLaunchKernelGGL((k_solve_fast<2, 4>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a);
         if ((e = hipGetLastError()) != hipSuccess) return (int)e;
     }
-    static bool attr = false;
-    if (!attr) {
+    // k_solve's dynamic-LDS limit is a per-device attribute, and the host-memory API drives one host thread
+    // per device (run_sharded): set it once per device, race-free, on the device this thread launches on
+    static std::once_flag attr_once[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return (int)hipErrorInvalidDevice;
+    std::call_once(attr_once[dev], [] {
         (void)hipFuncSetAttribute((const void*)k_solve, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
-        attr = true;
-    }
+    });
     const size_t lds = solve_ws_bytes(std::min<uint32_t>(max_lds_e, a.lds_e));
     a.n_map = n_blocks;
     uint32_t grid = std::min<uint32_t>(n_blocks, 256);

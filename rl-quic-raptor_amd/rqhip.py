@@ -44,6 +44,7 @@ EXPORTED = (
     "rq_decode_blocks_host", "rq_host_alloc", "rq_host_free", "rq_debug_colprog_passes",
     "rq_debug_shard_plan", "rq_debug_virtual_shards", "rq_debug_tuple", "rq_stream_release", "rq_shutdown",
     "rq_launch_timing", "rq_launch_time", "rq_debug_pair_emulate", "rq_debug_dma4_emulate", "rq_debug_decode_plan",
+    "rq_debug_assemble", "rq_debug_colprog_bound",
 )
 
 
@@ -180,6 +181,9 @@ def lib():
                                       ctypes.POINTER(ctypes.c_double), u32p], ctypes.c_int),
             "rq_debug_dma4_emulate": ([ctypes.c_uint32, ctypes.c_uint32, u32p, ctypes.c_uint32, vp, vp, ctypes.c_uint32,
                                        ctypes.c_uint32, u32p, ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+            "rq_debug_assemble": ([ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+            "rq_debug_colprog_bound": ([ctypes.c_uint32, ctypes.c_uint32, u32p, ctypes.c_uint32, vp, vp, ctypes.c_uint64,
+                                        u32p], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -336,6 +340,29 @@ def colprog_assemble(K, esis):
     _check(lib().rq_debug_colprog_assemble(K, e.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), len(e),
                                            ctypes.byref(n)))
     return n.value
+
+
+def assemble(text):
+    """rq_debug_assemble: gfx950 assembly text through the engine's register check and amd_comgr;
+    returns the code object size (RaptorQError with the check's message otherwise)."""
+    b = text.encode()
+    n = ctypes.c_size_t(0)
+    _check(lib().rq_debug_assemble(b, len(b), ctypes.byref(n)))
+    return n.value
+
+
+def colprog_bound(K, T, esis, src, src_bytes):
+    """rq_debug_colprog_bound: the (K, esis) program emulated on one block with its source buffer resource
+    bounded at src_bytes; returns (outputs, row_end)."""
+    import numpy as np
+    src = np.ascontiguousarray(src, np.uint8)
+    e = np.asarray(esis, np.uint32)
+    out = np.zeros((len(e), T), np.uint8)
+    re_ = ctypes.c_uint32(0)
+    P32 = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+    _check(lib().rq_debug_colprog_bound(K, T, P32(e), len(e), src.ctypes.data, out.ctypes.data, src_bytes,
+                                        ctypes.byref(re_)))
+    return out, re_.value
 
 
 def shard_plan(device_mask, n_devices, n_blocks, virtual_shards=0):
