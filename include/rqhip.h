@@ -205,6 +205,10 @@ int rq_debug_colprog_assemble(uint32_t K, const uint32_t* esi, uint32_t n_out, s
  * row_end 1 + the largest source row the program reads (the engine sets src_bytes = (blocks - 1) *
  * stride + row_end * T). */
 int rq_debug_assemble(const char* src, size_t len, size_t* code_bytes);
+/* Tests: writes a synthetic column-program cache entry (n_rows source-load rows and n_dma4 four-row staging
+ * rows) at `path` in the on-disk cache format and reads it back through the engine's loader;
+ * RQ_OK when every byte survives (the loader hashes and returns both row lists). */
+int rq_debug_cache_roundtrip(const char* path, uint32_t n_rows, uint32_t n_dma4);
 int rq_debug_colprog_bound(uint32_t K, uint32_t T, const uint32_t* esi, uint32_t n_out, const uint8_t* src,
                            uint8_t* out, uint64_t src_bytes, uint32_t* row_end);
 /* The two-wave (pair) split of the output program for (K, esi) -- wave A: source loads, forward pass,

@@ -78,6 +78,7 @@ struct AllocOpts {
     uint32_t src_lds = 1;        // evicted source rows may take LDS slots (else dropped at once)
     uint32_t wait_age = 320;     // a vmcnt wait also covers operations issued this many instructions ago
     uint32_t lwait_age = 48;     // the same for lgkmcnt (LDS) waits
+    uint32_t load_batch = 1;     // source-row prefetches issued in groups of this many (experiments)
 };
 
 struct MProg {

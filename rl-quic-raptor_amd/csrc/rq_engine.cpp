@@ -179,6 +179,19 @@ struct Workspace {
     }
 };
 
+// Records a workspace's `last` event on every exit once armed: a call that fails after it
+// queued work touching the workspace still leaves the marker behind that work, so DevCtx::reap never
+// frees buffers a failed call's kernels may still read or write.  The success paths disarm it and call
+// mark() themselves (its error is theirs to return).
+struct MarkGuard {
+    Workspace* w = nullptr;
+    void* stream = nullptr;
+    bool armed = false;
+    ~MarkGuard() {
+        if (armed && w) (void)w->mark(stream);
+    }
+};
+
 // Host-memory batch API: device staging of one pipeline stage (one internal stream).
 struct Stage {
     hipStream_t s = nullptr;
@@ -364,6 +377,7 @@ const AllocOpts& alloc_options() {
         if (const char* h = knob("RQHIP_SRC_BIAS")) r.src_bias = (uint32_t)std::atoi(h);
         if (const char* h = knob("RQHIP_SRC_LDS")) r.src_lds = (uint32_t)std::atoi(h);
         if (const char* h = knob("RQHIP_WAIT_AGE")) std::sscanf(h, "%u,%u", &r.wait_age, &r.lwait_age);
+        if (const char* h = knob("RQHIP_LOAD_BATCH")) r.load_batch = (uint32_t)std::max(1, std::atoi(h));
         return r;
     }();
     return o;
@@ -421,7 +435,7 @@ struct CacheHdr {
     MProg::Stats st;
     uint64_t body_hash;  // FNV-1a of the name, code object and row table (checked on load)
 };
-constexpr char CACHE_MAGIC[9] = "RQCO0007";
+constexpr char CACHE_MAGIC[9] = "RQCO0008";
 
 uint64_t cache_body_hash(const std::string& name, const std::vector<char>& co, const std::vector<uint32_t>& rows) {
     uint64_t h = fnv1a(name.data(), name.size());
@@ -434,14 +448,15 @@ bool cache_load(const std::string& path, CacheHdr* h, std::string* name, std::ve
     FILE* f = std::fopen(path.c_str(), "rb");
     if (!f) return false;
     bool ok = std::fread(h, sizeof *h, 1, f) == 1 && std::memcmp(h->magic, CACHE_MAGIC, 8) == 0 && h->name_len < 256 &&
-              h->co_len < (1ull << 30) && h->n_rows < (1u << 24);
-    if (ok) {
+              h->co_len < (1ull << 30) && h->n_rows < (1u << 24) && h->n_dma4 < (1u << 24);
+    if (ok) {  // the source-load rows, then the four-row staging rows (cache_store writes both)
+        const size_t nr = (size_t)h->n_rows + h->n_dma4;
         name->resize(h->name_len);
         co->resize(h->co_len);
-        rows->resize(h->n_rows);
+        rows->resize(nr);
         ok = std::fread(&(*name)[0], 1, h->name_len, f) == h->name_len &&
              std::fread(co->data(), 1, h->co_len, f) == h->co_len &&
-             std::fread(rows->data(), 4, h->n_rows, f) == h->n_rows;
+             std::fread(rows->data(), 4, nr, f) == nr;
     }
     std::fclose(f);
     // a torn or corrupted entry (the lengths can still look right) is dropped and rebuilt
@@ -493,6 +508,7 @@ uint32_t colprog_launch_shape(MProg* mp) {
 }
 
 // ---------------- column programs (the encode hot path) ----------------
+#ifdef RQHIP_EXPERIMENTS
 // Two-wave (pair) column programs (rq_colasm.hpp compile_pair): wave A streams the source rows and runs
 // the forward pass and pushes, wave B the HDPC bit accumulation, dense part and outputs, handed over
 // through an LDS ring.  Taken for the bit-accumulation (SCHED_4R) programs, whose single wave is bound
@@ -543,6 +559,16 @@ const Dma4Cfg& dma4_cfg() {
     }();
     return c;
 }
+#endif  // RQHIP_EXPERIMENTS
+
+// Whether a column program may differ with the caller's 16-B alignment (four-row staging, experiments).
+bool staging_possible() {
+#ifdef RQHIP_EXPERIMENTS
+    return dma4_cfg().quads != 0 || pair_cfg().mode != 0;
+#else
+    return false;
+#endif
+}
 
 bool compile_engine_program(const Params& p, const uint32_t* esi, uint32_t n_esi, const AllocOpts& ao,
                             bool search_waves, bool aligned16, ColIR* ir, MProg* mp, PairProg* pp, bool* use_pair,
@@ -550,6 +576,10 @@ bool compile_engine_program(const Params& p, const uint32_t* esi, uint32_t n_esi
     uint32_t passes = 0;
     *use_pair = false;
     if (!compile_colprog(p, esi, n_esi, ao, ir, mp, err, &passes, search_waves)) return false;
+#ifndef RQHIP_EXPERIMENTS
+    (void)aligned16; (void)pp;
+    return true;
+#else
     const Dma4Cfg& d4 = dma4_cfg();
     if (d4.quads && aligned16 && (passes & SCHED_4R) && mp->wg_waves <= 1) {
         MProg m4;
@@ -579,6 +609,7 @@ bool compile_engine_program(const Params& p, const uint32_t* esi, uint32_t n_esi
     }
     *use_pair = true;
     return true;
+#endif
 }
 
 // Compile (once per device and (K', K, outputs)) the straight-line gfx950 program for the given
@@ -589,7 +620,11 @@ bool compile_engine_program(const Params& p, const uint32_t* esi, uint32_t n_esi
 // (the four-row staging of pair programs reads 16-B chunks); a separate program otherwise.
 int get_col_kernel(DevCtx* ctx, const Params& p, const uint32_t* esi, uint32_t n_esi, bool all_C, ColKernel** out,
                    bool aligned16 = false) {
-    std::string key = std::to_string(p.Kp) + ":" + std::to_string(p.K) + (all_C ? ":C" : ":E") + (aligned16 ? "a" : "");
+    // the 16-B-aligned variant is a different program only where four-row staging could be chosen
+    // (experiments builds with RQHIP_DMA4 / RQHIP_PAIR): elsewhere both alignments share one program
+    const bool staged = staging_possible();
+    std::string key = std::to_string(p.Kp) + ":" + std::to_string(p.K) + (all_C ? ":C" : ":E") + (aligned16 && staged ? "a" : "");
+    if (!staged) aligned16 = false;
     if (!all_C) {
         key.reserve(key.size() + n_esi * 6);
         for (uint32_t i = 0; i < n_esi; ++i) key += "," + std::to_string(esi[i]);
@@ -654,8 +689,10 @@ int get_col_kernel(DevCtx* ctx, const Params& p, const uint32_t* esi, uint32_t n
             uint32_t wpc = 0;
             co.clear();
             if (pair) {
+#ifdef RQHIP_EXPERIMENTS
                 wpc = 4;  // two workgroups of two 512-register waves per CU (pair_lds_bytes <= 80 KiB)
                 if (!comgr_assemble(emit_pair_asm(pp, kname), &co, &err)) { ctx->colk.erase(key); return fail(RQ_ERR_PLAN, err); }
+#endif
             } else {
                 wpc = colprog_launch_shape(&mp);
                 if (!comgr_assemble(emit_colprog_asm(mp, kname), &co, &err)) { ctx->colk.erase(key); return fail(RQ_ERR_PLAN, err); }
@@ -746,6 +783,7 @@ int launch_col(DevCtx* ctx, ColKernel* k, uint32_t T, uint32_t n_blocks, const v
         w = ctx->wsp(stream);
         if ((rc = w->scratch.ensure(spw * max_wg * Wi))) return rc;  // a pair's wave A alone uses scratch
     }
+    MarkGuard mg{w, stream};
     auto& tab = k->row_off[T];
     if (!tab) {  // once per (program, T): the source loads' soffsets, padded to whole 16-entry groups
         std::unique_ptr<DevBuf> b(new DevBuf());
@@ -801,12 +839,15 @@ int launch_col(DevCtx* ctx, ColKernel* k, uint32_t T, uint32_t n_blocks, const v
                 ctx->tev.push_back({e0, e1});
             }
             const auto& pr = ctx->tev[ctx->tev_used++];
+            mg.armed = w != nullptr;
             HIP_TRY(hipExtModuleLaunchKernel(k->fn, wgs * 64 * Wg, 1, 1, 64 * Wg, 1, 1, 0, (hipStream_t)stream, nullptr,
                                              cfg, pr.first, pr.second, 0));
             continue;
         }
+        mg.armed = w != nullptr;
         HIP_TRY(hipModuleLaunchKernel(k->fn, wgs, 1, 1, 64 * Wg, 1, 1, 0, (hipStream_t)stream, nullptr, cfg));
     }
+    mg.armed = false;
     return w ? w->mark(stream) : RQ_OK;
 }
 
@@ -1179,8 +1220,10 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
             (void)hipEventRecord(w->up[set], s);
         }
     } up_guard{w, (hipStream_t)stream, set, false};
+    MarkGuard mark_guard{w, stream};
     if (side) {
         if ((rc = w->dstatus.ensure((size_t)n_blocks * 4))) return rc;
+        mark_guard.armed = true;
         HIP_TRY(hipMemcpyAsync(w->idx[set].p, w->h_idx[set].p, n_idx * 4, hipMemcpyHostToDevice, w->cs));
         up_guard.armed = true;
         HIP_TRY(hipEventRecord(w->cpy[set], w->cs));
@@ -1198,6 +1241,7 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
         dst_status = reinterpret_cast<int32_t*>(w->idx[set].as<uint32_t>() + o_st);
     }
     if ((rc = w->r0.ensure((size_t)n_blocks * uni.size() * T))) return rc;
+    mark_guard.armed = true;  // the kernels below read and write this workspace's buffers
     if ((rc = w->xb.ensure((size_t)xo * 64))) return rc;
     if ((rc = w->xp.ensure(std::max<size_t>(n_er, 1) * 2))) return rc;
     if (go && (rc = w->gws.ensure((size_t)go * 64))) return rc;
@@ -1305,9 +1349,11 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     if (po) HIP_TRY(hipMemcpyAsync(w->h_pack.p, w->pk.p, pack_bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
     if (async) {  // statuses land in the caller's pinned array when the stream gets here
         HIP_TRY(hipMemcpyAsync(status, dst_status, n_blocks * 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
+        mark_guard.armed = false;
         return w->mark(stream);
     }
     HIP_TRY(hipMemcpyAsync(w->h_status.p, dst_status, n_blocks * 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
+    mark_guard.armed = false;
     if ((rc = w->mark(stream))) return rc;
     if (fin == Fin::Deferred) return RQ_OK;  // decode_collect after the caller's stream sync
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
@@ -1983,6 +2029,40 @@ int rq_debug_colprog_assemble(uint32_t K, const uint32_t* esi, uint32_t n_out, s
     return RQ_OK;
 }
 
+int rq_debug_cache_roundtrip(const char* path, uint32_t n_rows, uint32_t n_dma4) {
+    if (!path) return fail(RQ_ERR_BAD_ARG, "no path");
+    CacheHdr h;
+    std::memset(&h, 0, sizeof h);
+    std::memcpy(h.magic, CACHE_MAGIC, 8);
+    const std::string name = "rq_colprog_cache_test";
+    std::vector<char> co(4096);
+    for (size_t i = 0; i < co.size(); ++i) co[i] = (char)(i * 131 + 7);
+    std::vector<uint32_t> rows((size_t)n_rows + n_dma4);
+    for (size_t i = 0; i < rows.size(); ++i) rows[i] = (uint32_t)(i * 2654435761u);
+    h.n_rows = n_rows;
+    h.n_dma4 = n_dma4;
+    h.name_len = (uint32_t)name.size();
+    h.co_len = co.size();
+    h.body_hash = cache_body_hash(name, co, rows);
+    {  // cache_store writes through a temporary name in cache_dir(): write the entry directly here
+        FILE* f = std::fopen(path, "wb");
+        if (!f) return fail(RQ_ERR_BAD_ARG, "cannot write the entry");
+        const bool ok = std::fwrite(&h, sizeof h, 1, f) == 1 && std::fwrite(name.data(), 1, name.size(), f) == name.size() &&
+                        std::fwrite(co.data(), 1, co.size(), f) == co.size() &&
+                        std::fwrite(rows.data(), 4, rows.size(), f) == rows.size();
+        std::fclose(f);
+        if (!ok) return fail(RQ_ERR_BAD_ARG, "cannot write the entry");
+    }
+    CacheHdr g;
+    std::string n2;
+    std::vector<char> co2;
+    std::vector<uint32_t> r2;
+    if (!cache_load(path, &g, &n2, &co2, &r2)) return fail(RQ_ERR_PLAN, "cache entry rejected on load");
+    if (n2 != name || co2 != co || r2 != rows || g.n_rows != n_rows || g.n_dma4 != n_dma4)
+        return fail(RQ_ERR_PLAN, "cache entry differs after the round trip");
+    return RQ_OK;
+}
+
 int rq_debug_assemble(const char* src, size_t len, size_t* code_bytes) {
     if (!src) return fail(RQ_ERR_BAD_ARG, "no source");
     std::vector<char> co;
@@ -2040,6 +2120,10 @@ int rq_debug_decode_plan(uint32_t T, uint32_t K, uint32_t n_blocks, const uint32
 
 int rq_debug_dma4_emulate(uint32_t K, uint32_t T, const uint32_t* esi, uint32_t n_out, const uint8_t* src, uint8_t* out,
                           uint32_t quads, uint32_t la, uint32_t stats[8], size_t* code_bytes) {
+#ifndef RQHIP_EXPERIMENTS
+    (void)K; (void)T; (void)esi; (void)n_out; (void)src; (void)out; (void)quads; (void)la; (void)stats; (void)code_bytes;
+    return fail(RQ_ERR_BAD_ARG, "four-row staging is in the experiments build only (tools/build_experiments.sh)");
+#else
     Params p;
     int rc = params_for_K(K, &p);
     if (rc) return fail(rc, "k is too big");
@@ -2063,10 +2147,15 @@ int rq_debug_dma4_emulate(uint32_t K, uint32_t T, const uint32_t* esi, uint32_t 
         *code_bytes = co.size();
     }
     return RQ_OK;
+#endif
 }
 
 int rq_debug_pair_emulate(uint32_t K, uint32_t T, const uint32_t* esi, uint32_t n_out, const uint8_t* src,
                           uint8_t* out, const uint32_t cfg[5], uint32_t stats[16], size_t* code_bytes) {
+#ifndef RQHIP_EXPERIMENTS
+    (void)K; (void)T; (void)esi; (void)n_out; (void)src; (void)out; (void)cfg; (void)stats; (void)code_bytes;
+    return fail(RQ_ERR_BAD_ARG, "pair programs are in the experiments build only (tools/build_experiments.sh)");
+#else
     Params p;
     int rc = params_for_K(K, &p);
     if (rc) return fail(rc, "k is too big");
@@ -2105,6 +2194,7 @@ int rq_debug_pair_emulate(uint32_t K, uint32_t T, const uint32_t* esi, uint32_t 
         *code_bytes = co.size();
     }
     return RQ_OK;
+#endif
 }
 
 int rq_debug_shard_plan(uint32_t device_mask, int n_devices, uint32_t n_blocks, uint32_t virtual_shards, int* dev,

@@ -22,6 +22,7 @@
 
 #include "rfc6330_tables.h"
 #include "rq_device.hpp"
+#include "rq_kernels_common.hpp"
 
 namespace rq {
 
@@ -38,27 +39,6 @@ int upload_tables() {
     return (int)e;
 }
 
-// ------------------------------ GF(256) on packed dwords ------------------------------------
-// alpha * x per byte: v_perm's sign-replicating selectors turn the four top bits into 0x00/0xFF
-// byte masks (selector bytes 0x0a,0x08,0x0b,0x09 read bits 7,15,23,31 of {x<<8 : x}), no multiply.
-__device__ __forceinline__ uint32_t xtime4(uint32_t x) {
-    const uint32_t mask = __builtin_amdgcn_perm(x << 8, x, 0x090b080au);
-    return ((x << 1) & 0xFEFEFEFEu) ^ (mask & 0x1D1D1D1Du);
-}
-
-// a ^ (b & m) in one v_bitop3 (src0 a 0xF0, src1 b 0xCC, src2 m 0xAA -> 0x78)
-__device__ __forceinline__ uint32_t bitop_xand(uint32_t a, uint32_t b, uint32_t m) {
-    uint32_t d;
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x78" : "=v"(d) : "v"(a), "v"(b), "v"(m));
-    return d;
-}
-
-// a ^ b ^ c in one v_bitop3 (hipcc does not form it from three XORs)
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-    uint32_t d;
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(d) : "v"(a), "v"(b), "v"(c));
-    return d;
-}
 
 // ------------------------------ LT tuple on device (RQ/params.go:83-112) -------------------
 __device__ __forceinline__ uint32_t d_rand(uint32_t y, uint32_t i, uint32_t m) {
@@ -114,390 +94,14 @@ int launch_pack_rows(const PackArgs& a, void* stream) {
 // rank e <=> the reference's system is full rank.
 // Output: X (e x e) and the e received repairs it combines: x_k = sum_m X[k][m] s_{piv[m]}, stored
 // as xcoef[m * xc_stride + k] (one uniform 64-byte row per m for k_apply's scalar loads).
-__device__ __forceinline__ uint8_t gmul_t(const uint8_t* lg, const uint8_t* ex, uint8_t a, uint8_t b) {
-    return (a && b) ? ex[lg[a] + lg[b]] : (uint8_t)0;
-}
-
-// GF(256) exp/log tables (poly 0x11D, alpha = 2), constant-initialised in device memory and copied
-// into LDS by the blocks that need them.
-struct alignas(16) GfTabs {
-    uint8_t ex[512];
-    uint8_t lg[256];
-};
-constexpr GfTabs make_gf_tabs() {
-    GfTabs t{};
-    uint32_t x = 1;
-    for (int i = 0; i < 255; ++i) {
-        t.ex[i] = (uint8_t)x; t.ex[i + 255] = (uint8_t)x; t.lg[x] = (uint8_t)i;
-        x <<= 1; if (x & 0x100) x ^= 0x11D;
-    }
-    t.ex[510] = t.ex[0]; t.ex[511] = t.ex[1];
-    return t;
-}
-__device__ const GfTabs kGf = make_gf_tabs();
-
-__device__ __forceinline__ void gf_tables_copy(uint8_t* ex, uint8_t* lg) {
-    // as 192 dwords, one load per thread (no serialised byte-load loop)
-    const uint32_t* se = reinterpret_cast<const uint32_t*>(kGf.ex);
-    const uint32_t* sl = reinterpret_cast<const uint32_t*>(kGf.lg);
-    for (uint32_t i = threadIdx.x; i < 192; i += blockDim.x) {
-        if (i < 128) reinterpret_cast<uint32_t*>(ex)[i] = se[i];
-        else reinterpret_cast<uint32_t*>(lg)[i - 128] = sl[i - 128];
-    }
-}
-
-// Row gather of the solvers: wave g copies coefficient bytes k = g, g + NW, ... of one received
-// repair (mr[Es[k]], a byte gather from the program's identity-payload outputs) into its LDS row,
-// sixteen loads in flight per lane instead of one load-then-store round trip per byte.
-template <int NW>
-__device__ __forceinline__ void gather_row(uint8_t* myb, const uint8_t* mr, const uint32_t* Es, uint32_t e, uint32_t g) {
-    for (uint32_t k0 = g; k0 < e; k0 += 16 * NW) {
-        uint8_t v[16];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) {
-            const uint32_t k = k0 + NW * u;
-            v[u] = k < e ? mr[Es[k]] : (uint8_t)0;
-        }
-#pragma unroll
-        for (int u = 0; u < 16; ++u) {
-            const uint32_t k = k0 + NW * u;
-            if (k < e) myb[k] = v[u];
-        }
-    }
-}
-
-// Four waves per block, RPL rows per lane: lane j of every wave holds received repairs j + 64q
-// (q < RPL) as LDS rows of 128*RPL bytes: e coefficient bytes, then the identity part (byte e + row);
-// wave g updates the 16-byte quads g, g+4, ... of every row.  RPL = 1 takes blocks with e <= 64 on
-// their first 64 received repairs; RPL = 2 takes the blocks it deferred (e <= 128, first 128
-// repairs).  Each step picks the lowest unused row with a nonzero coefficient (ballot: every wave
-// sees all rows and picks the same one), scales it by the inverse and stores its eight alpha^b
-// multiples (one byte per thread, exp/log tables), and every other row XORs in the multiples its own
-// coefficient's bits select (one v_bitop3 per bit and dword).
-template <int RPL, int NW>
-__global__ void __launch_bounds__(64 * NW) k_solve_fast(SolveArgs a) {
-    constexpr uint32_t NT = 64 * NW;
-    constexpr uint32_t NROWS = 64 * RPL, WQ = 8 * RPL, SW = 32 * RPL + 4;  // quads per row, row stride
-    __shared__ __attribute__((aligned(16))) uint32_t rows[NROWS * SW];
-    __shared__ __attribute__((aligned(16))) uint4 mult[8][WQ];  // alpha^b * scaled pivot row
-    __shared__ __attribute__((aligned(4))) uint8_t ex[512], lg[256];
-    __shared__ uint8_t pivl[NROWS];
-    __shared__ uint32_t Es[NROWS];
-    const uint32_t b = a.blk_map[blockIdx.x];
-    const uint32_t tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
-    if (RPL > 1 && a.status[b] != ST_FALLBACK) return;  // the wide pass takes deferred blocks only
-    const uint32_t e = a.erased_off[b + 1] - a.erased_off[b];
-    const uint32_t nr = a.rep_cnt[b];
-    if (e > NROWS) {
-        if (tid == 0) a.status[b] = ST_FALLBACK;
-        return;
-    }
-    const uint32_t nrow = min(nr, NROWS);
-    const uint32_t* E = a.erased + a.erased_off[b];
-    const uint32_t* U = a.rep_uidx + a.rep_off[b];
-    for (uint32_t i = tid; i < e; i += NT) Es[i] = E[i];
-    gf_tables_copy(ex, lg);
-    for (uint32_t i = tid; i < NROWS * SW; i += NT) rows[i] = 0;
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < RPL; ++q) {
-        const uint32_t row = lane + 64 * q;
-        if (row < nrow) {  // row gather: wave g takes columns g, g+4, ...
-            uint8_t* myb = reinterpret_cast<uint8_t*>(rows + row * SW);
-            const uint8_t* mr = a.mrep + (size_t)U[row] * a.mrep_stride;
-            gather_row<NW>(myb, mr, Es, e, g);
-            if (g == 0) myb[e + row] = 1;
-        }
-    }
-    __syncthreads();
-    const uint32_t q1 = (e + nrow + 15) >> 4;  // quads holding live columns
-    bool used[RPL];
-#pragma unroll
-    for (int q = 0; q < RPL; ++q) used[q] = lane + 64 * q >= nrow;
-    uint8_t* mb = reinterpret_cast<uint8_t*>(mult);
-    const uint8_t* rb = reinterpret_cast<const uint8_t*>(rows);
-    for (uint32_t k = 0; k < e; ++k) {
-        uint32_t f[RPL];
-        uint32_t p = 0xFFFFFFFFu;
-#pragma unroll
-        for (int q = RPL - 1; q >= 0; --q) {
-            f[q] = (rows[(lane + 64 * q) * SW + (k >> 2)] >> ((k & 3) * 8)) & 0xFFu;
-            const uint64_t bal = __ballot(f[q] != 0 && !used[q]);
-            if (bal) p = 64 * q + (uint32_t)__ffsll((unsigned long long)bal) - 1;
-        }
-        if (p == 0xFFFFFFFFu) {  // uniform over the block: every wave saw the same rows
-            if (tid == 0) a.status[b] = (nr > nrow) ? ST_FALLBACK : 0;
-            return;
-        }
-#pragma unroll
-        for (int q = 0; q < RPL; ++q)
-            if (lane + 64 * q == p) used[q] = true;
-        if (tid == 0) pivl[k] = (uint8_t)p;
-        // scaled pivot row and its alpha multiples: alpha^bt * x / x_k = exp(log x - log x_k + bt)
-        const uint32_t lginv = 255u - lg[rb[p * SW * 4 + k]];
-        for (uint32_t pos = tid; pos < 128 * RPL; pos += NT) {
-            const uint32_t x = rb[p * SW * 4 + pos];
-            uint32_t t = lg[x] + lginv;
-            t = t >= 255u ? t - 255u : t;
-#pragma unroll
-            for (int bt = 0; bt < 8; ++bt) mb[bt * WQ * 16 + pos] = x ? ex[t + bt] : (uint8_t)0;
-        }
-        __syncthreads();
-        // columns < k are zero in the pivot row (all are earlier pivot columns): start at quad k/16
-        const uint32_t q0 = k >> 4;
-#pragma unroll
-        for (int q = 0; q < RPL; ++q) {
-            uint4* my4 = reinterpret_cast<uint4*>(rows + (lane + 64 * q) * SW);
-            if (lane + 64 * q == p) {
-                for (uint32_t w = q0 + g; w < q1; w += NW) my4[w] = mult[0][w];
-            } else if (f[q]) {
-                uint32_t msk[8];
-#pragma unroll
-                for (int bt = 0; bt < 8; ++bt) msk[bt] = 0u - ((f[q] >> bt) & 1u);
-                for (uint32_t w = q0 + g; w < q1; w += NW) {
-                    uint4 r = my4[w];
-#pragma unroll
-                    for (int bt = 0; bt < 8; ++bt) {
-                        const uint4 m = mult[bt][w];
-                        r.x = bitop_xand(r.x, m.x, msk[bt]);
-                        r.y = bitop_xand(r.y, m.y, msk[bt]);
-                        r.z = bitop_xand(r.z, m.z, msk[bt]);
-                        r.w = bitop_xand(r.w, m.w, msk[bt]);
-                    }
-                    my4[w] = r;
-                }
-            }
-        }
-        __syncthreads();
-    }
-    // X[k][m] = identity byte (e + piv_m) of pivot row piv_k
-    uint8_t* xc = a.xcoef + 64ull * a.xoff[blockIdx.x];
-    const uint32_t xs = x_stride(e);
-    uint16_t* XP = a.xpiv + a.erased_off[b];
-    for (uint32_t m = tid; m < e; m += NT) XP[m] = pivl[m];
-    for (uint32_t idx = tid; idx < e * e; idx += NT) {
-        const uint32_t m = idx / e, k = idx - m * e;
-        xc[m * xs + k] = rb[pivl[k] * SW * 4 + e + pivl[m]];
-    }
-    if (tid == 0) a.status[b] = 1;
-}
-
-// The five v_perm tables of a coefficient c (byte lanes): c*{0..3}, c*{4..7}, c*{0,8,16,24},
-// c*{32,40,48,56}, c*{0,64,128,192}, from the eight alpha^i multiples of c.
-__device__ __forceinline__ uint8_t xtime1(uint32_t x) { return (uint8_t)((x << 1) ^ ((x & 0x80u) ? 0x1Du : 0u)); }
-
-__device__ __forceinline__ void perm_tables(uint32_t c, uint4* A, uint32_t* B) {
-    uint32_t m[8];
-    m[0] = c;
-#pragma unroll
-    for (int i = 1; i < 8; ++i) m[i] = xtime1(m[i - 1]);
-    auto lo = [&](uint32_t x) { return ((x & 1u) ? m[0] : 0u) ^ ((x & 2u) ? m[1] : 0u) ^ ((x & 4u) ? m[2] : 0u); };
-    auto pack = [](uint32_t a, uint32_t b, uint32_t c2, uint32_t d) { return a | (b << 8) | (c2 << 16) | (d << 24); };
-    A->x = pack(0, lo(1), lo(2), lo(3));
-    A->y = pack(lo(4), lo(5), lo(6), lo(7));
-    A->z = pack(0, m[3], m[4], m[3] ^ m[4]);
-    A->w = pack(m[5], m[5] ^ m[3], m[5] ^ m[4], m[5] ^ m[4] ^ m[3]);
-    *B = pack(0, m[6], m[7], m[6] ^ m[7]);
-}
-
-// perm_tables of every nonzero coefficient alpha^l (l < 255), constant-initialised in device memory:
-// the solvers copy them into LDS (five dword loads per entry) instead of building 255 table sets per
-// block (~70 VALU each).
-struct alignas(16) PermTabs {
-    uint32_t A[255][4];
-    uint32_t B[255];
-};
-constexpr PermTabs make_perm_tabs() {
-    PermTabs t{};
-    const GfTabs g = make_gf_tabs();
-    for (int l = 0; l < 255; ++l) {
-        uint32_t m[8] = {g.ex[l], 0, 0, 0, 0, 0, 0, 0};
-        for (int i = 1; i < 8; ++i) m[i] = ((m[i - 1] << 1) ^ ((m[i - 1] & 0x80u) ? 0x1Du : 0u)) & 0xFFu;
-        auto lo = [&](uint32_t x) { return ((x & 1u) ? m[0] : 0u) ^ ((x & 2u) ? m[1] : 0u) ^ ((x & 4u) ? m[2] : 0u); };
-        auto pack = [](uint32_t a, uint32_t b, uint32_t c2, uint32_t d) { return a | (b << 8) | (c2 << 16) | (d << 24); };
-        t.A[l][0] = pack(0, lo(1), lo(2), lo(3));
-        t.A[l][1] = pack(lo(4), lo(5), lo(6), lo(7));
-        t.A[l][2] = pack(0, m[3], m[4], m[3] ^ m[4]);
-        t.A[l][3] = pack(m[5], m[5] ^ m[3], m[5] ^ m[4], m[5] ^ m[4] ^ m[3]);
-        t.B[l] = pack(0, m[6], m[7], m[6] ^ m[7]);
-    }
-    return t;
-}
-__device__ const PermTabs kPerm = make_perm_tabs();
-
-// c * x on four bytes with c's perm_tables: three v_perm lookups (3 + 3 + 2 bits of each byte).
-__device__ __forceinline__ uint32_t perm_mul(const uint4& A, uint32_t B, uint32_t x) {
-    const uint32_t s0 = x & 0x07070707u, s1 = (x >> 3) & 0x07070707u, s2 = (x >> 6) & 0x03030303u;
-    return xor3(__builtin_amdgcn_perm(A.y, A.x, s0), __builtin_amdgcn_perm(A.w, A.z, s1),
-                __builtin_amdgcn_perm(B, B, s2));
-}
-
-// k_solve_fast's layout (four waves, RPL rows per lane as LDS rows, wave g on the quads g, g+4, ...)
-// with the elimination done by GF(256) multiplication instead of alpha-multiple tables: each lane
-// turns its coefficient c_j = f_j / f_p into v_perm tables (perm_tables) and folds c_j times the
-// pivot row into its row, the pivot row's dwords read once per quad (one broadcast b128) and made
-// scalar, so the lookups' selectors are SGPRs.  The pivot lane uses c = 1 ^ 1/f_p, which leaves
-// row_p / f_p (each wave reads the pivot quad before its pivot lane rewrites it).  One barrier per
-// step (the alpha-multiple tables, their byte stores and the second barrier are gone) and an eighth
-// of the LDS reads.
-template <int RPL, int NW, bool LUT>
-__global__ void __launch_bounds__(64 * NW) k_solve_pm(SolveArgs a) {
-    constexpr uint32_t NT = 64 * NW;
-    constexpr uint32_t NROWS = 64 * RPL, SW = 32 * RPL + 4;  // rows, row stride (dwords)
-    __shared__ __attribute__((aligned(16))) uint32_t rows[NROWS * SW];
-    __shared__ __attribute__((aligned(4))) uint8_t ex[512], lg[256];
-    __shared__ uint8_t pivl[NROWS];
-    __shared__ uint32_t Es[NROWS];
-    // LUT: the v_perm tables of every nonzero coefficient, indexed by its log (built once per block)
-    __shared__ __attribute__((aligned(16))) uint4 tlA[LUT ? 255 : 1];
-    __shared__ uint32_t tlB[LUT ? 255 : 1];
-    // LUT: per pivot value f (!= 0), log f | log(1 ^ 1/f) << 8 | (1 ^ 1/f != 0) << 16: one lookup per
-    // step instead of three dependent ones (lg[f_p], ex[255 - lg f_p], lg[c_p])
-    __shared__ uint32_t pinfo[LUT ? 256 : 1];
-    __shared__ uint8_t fcol[2][NROWS];  // column k of every row by step parity (see k_solve_pq)
-    const uint32_t b = a.blk_map[blockIdx.x];
-    const uint32_t tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
-    if (a.status_init)  // the host-decided statuses (disjoint from the solver's blocks, ST_PENDING)
-        for (uint32_t i = blockIdx.x * NT + tid; i < a.n_all; i += gridDim.x * NT)
-            if (a.status_init[i] != ST_PENDING) a.status[i] = a.status_init[i];
-    if (RPL > 1 && a.status[b] != ST_FALLBACK) return;  // the wide pass takes deferred blocks only
-    const uint32_t e = a.erased_off[b + 1] - a.erased_off[b];
-    const uint32_t nr = a.rep_cnt[b];
-    if (e > NROWS) {
-        if (tid == 0) a.status[b] = ST_FALLBACK;
-        return;
-    }
-    const uint32_t nrow = (RPL == 1 && a.row_margin) ? min(min(nr, NROWS), e + a.row_margin) : min(nr, NROWS);
-    const uint32_t* E = a.erased + a.erased_off[b];
-    const uint32_t* U = a.rep_uidx + a.rep_off[b];
-    for (uint32_t i = tid; i < e; i += NT) Es[i] = E[i];
-    gf_tables_copy(ex, lg);
-    if (LUT)
-        for (uint32_t l = tid; l < 255; l += NT) perm_tables(kGf.ex[l], &tlA[l], &tlB[l]);
-    for (uint32_t i = tid; i < NROWS * SW; i += NT) rows[i] = 0;
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < RPL; ++q) {
-        const uint32_t row = lane + 64 * q;
-        if (row < nrow) {  // row gather: wave g takes columns g, g+4, ...
-            uint8_t* myb = reinterpret_cast<uint8_t*>(rows + row * SW);
-            const uint8_t* mr = a.mrep + (size_t)U[row] * a.mrep_stride;
-            gather_row<NW>(myb, mr, Es, e, g);
-            if (g == 0) myb[e + row] = 1;
-        }
-    }
-    if (LUT)
-        for (uint32_t x = 1 + tid; x < 256; x += NT) {
-            const uint32_t lx = lg[x], cp = 1u ^ ex[255u - lx];
-            pinfo[x] = lx | (cp ? (uint32_t)lg[cp] << 8 | 1u << 16 : 0u);
-        }
-    __syncthreads();
-    for (uint32_t r = tid; r < NROWS; r += NT) fcol[0][r] = (uint8_t)(rows[r * SW] & 0xFFu);
-    __syncthreads();
-    const uint32_t q1 = (e + nrow + 15) >> 4;  // quads holding live columns
-    bool used[RPL];
-#pragma unroll
-    for (int q = 0; q < RPL; ++q) used[q] = lane + 64 * q >= nrow;
-    const uint8_t* rb = reinterpret_cast<const uint8_t*>(rows);
-    for (uint32_t k = 0; k < e; ++k) {
-        uint32_t f[RPL];
-        uint32_t p = 0xFFFFFFFFu;
-#pragma unroll
-        for (int q = RPL - 1; q >= 0; --q) {
-            f[q] = fcol[k & 1][lane + 64 * q];
-            const uint64_t bal = __ballot(f[q] != 0 && !used[q]);
-            if (bal) p = 64 * q + (uint32_t)__ffsll((unsigned long long)bal) - 1;
-        }
-        if (p == 0xFFFFFFFFu) {  // uniform over the block: every wave saw the same rows
-            if (tid == 0) a.status[b] = (nr > nrow) ? ST_FALLBACK : 0;
-            return;
-        }
-#pragma unroll
-        for (int q = 0; q < RPL; ++q)
-            if (lane + 64 * q == p) used[q] = true;
-        if (tid == 0) pivl[k] = (uint8_t)p;
-        // f_p from the pivot lane's register (no LDS round trip); lg[f] issued beside lg[f_p]
-        uint32_t fp = 0;
-#pragma unroll
-        for (int q = 0; q < RPL; ++q)
-            if ((p >> 6) == (uint32_t)q) fp = __builtin_amdgcn_readlane(f[q], p & 63);
-        uint4 A[RPL];
-        uint32_t B[RPL];
-        bool act[RPL];
-        if (LUT) {
-            const uint32_t pi = pinfo[fp];
-            const uint32_t lgp = pi & 0xFFu, lcp = (pi >> 8) & 0xFFu;  // the pivot lane's coefficient 1 ^ 1/f_p
-#pragma unroll
-            for (int q = 0; q < RPL; ++q) {
-                uint32_t l = 0;
-                if (lane + 64 * q == p) {
-                    act[q] = (pi >> 16) != 0;
-                    l = lcp;
-                } else {
-                    act[q] = f[q] != 0;
-                    l = lg[f[q]] + 255u - lgp;
-                    l = l >= 255u ? l - 255u : l;
-                }
-                A[q] = tlA[act[q] ? l : 0];
-                B[q] = tlB[act[q] ? l : 0];
-            }
-        } else {
-            const uint32_t lgp = lg[fp];
-            const uint32_t inv = ex[255u - lgp];
-#pragma unroll
-            for (int q = 0; q < RPL; ++q) {
-                uint32_t c = 0;
-                if (lane + 64 * q == p) {
-                    c = 1u ^ inv;
-                } else if (f[q]) {
-                    uint32_t t = lg[f[q]] + 255u - lgp;
-                    t = t >= 255u ? t - 255u : t;
-                    c = ex[t];
-                }
-                act[q] = c != 0;
-                perm_tables(c, &A[q], &B[q]);
-            }
-        }
-        // columns < k are zero in the pivot row (all are earlier pivot columns): start at quad k/16
-        const uint4* prow = reinterpret_cast<const uint4*>(rows + p * SW);
-        const uint32_t kn = k + 1;
-        for (uint32_t w = (k >> 4) + g; w < q1; w += NW) {
-            const uint4 P = prow[w];
-            const uint32_t px = __builtin_amdgcn_readfirstlane(P.x), py = __builtin_amdgcn_readfirstlane(P.y);
-            const uint32_t pz = __builtin_amdgcn_readfirstlane(P.z), pw = __builtin_amdgcn_readfirstlane(P.w);
-#pragma unroll
-            for (int q = 0; q < RPL; ++q) {
-                uint4* my4 = reinterpret_cast<uint4*>(rows + (lane + 64 * q) * SW);
-                uint4 r = my4[w];
-                if (act[q]) {
-                    r.x ^= perm_mul(A[q], B[q], px);
-                    r.y ^= perm_mul(A[q], B[q], py);
-                    r.z ^= perm_mul(A[q], B[q], pz);
-                    r.w ^= perm_mul(A[q], B[q], pw);
-                    my4[w] = r;
-                }
-                if (kn < e && w == (kn >> 4)) {  // wave-uniform: this wave owns column k + 1
-                    const uint32_t d = (kn >> 2) & 3u;
-                    const uint32_t dw = d == 0 ? r.x : d == 1 ? r.y : d == 2 ? r.z : r.w;
-                    fcol[kn & 1][lane + 64 * q] = (uint8_t)(dw >> ((kn & 3u) * 8));
-                }
-            }
-        }
-        __syncthreads();
-    }
-    // X[k][m] = identity byte (e + piv_m) of pivot row piv_k
-    uint8_t* xc = a.xcoef + 64ull * a.xoff[blockIdx.x];
-    const uint32_t xs = x_stride(e);
-    uint16_t* XP = a.xpiv + a.erased_off[b];
-    for (uint32_t m = tid; m < e; m += NT) XP[m] = pivl[m];
-    for (uint32_t idx = tid; idx < e * e; idx += NT) {
-        const uint32_t m = idx / e, k = idx - m * e;
-        xc[m * xs + k] = rb[pivl[k] * SW * 4 + e + pivl[m]];
-    }
-    if (tid == 0) a.status[b] = 1;
-}
-
-// k_solve_pm (LUT) with a shorter dependent chain per pivot step: each wave issues the loads of its
+// The shipped solvers are k_solve_pq<1, 4> (e <= 64), k_solve_pq<2, 4> (e <= 128) and k_solve (any e);
+// the variants measured slower live in rq_kernels_exp.hip (experiments builds only).
+//
+// Four waves per block, RPL rows per lane (lane j of every wave holds received repairs j + 64q as LDS
+// rows: e coefficient bytes, then the identity part at byte e + row); each step picks the lowest unused
+// row with a nonzero coefficient (ballot) and every other row folds c_j = f_j / f_p times the pivot
+// row in (GF(256) multiplication by three v_perm lookups against c_j's tables, the pivot row's dwords
+// made scalar so the selectors are SGPRs).  Round-2 k_solve_pm with a shorter dependent chain per pivot step: each wave issues the loads of its
 // row quads for the step (at most QW per row) at the step's start, reads pinfo[f] of its own
 // coefficient (log f, and the pivot-lane coefficient's log) instead of lg[f] after pinfo[f_p] (f_p's
 // log is then a v_readlane of the pivot lane's entry), and loads all its pivot-row quads at once: a
@@ -683,223 +287,7 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
     if (tid == 0) a.status[b] = 1;
 }
 
-// One wave per block for e <= 64 on the first <= 64 received repairs, the rows held in registers:
-// lane j owns received repair j as 32 dwords (e coefficient bytes, then the identity part at byte
-// e + j).  Each step k takes the lowest unused row with a nonzero coefficient in column k (ballot),
-// and every lane folds the pivot row (read dword by dword with v_readlane: uniform, so the v_perm
-// selectors are scalar) scaled by its own coefficient c_j = f_j / f_p into its row -- one GF(256)
-// multiply per dword as three v_perm lookups against per-lane tables of c_j (perm_tables).  The
-// pivot lane uses c = 1 ^ 1/f_p, which leaves row_p / f_p.  No barrier inside the elimination.
-__global__ void __launch_bounds__(64) k_solve_reg(SolveArgs a) {
-    __shared__ __attribute__((aligned(4))) uint8_t ex[512], lg[256];
-    __shared__ uint8_t pivl[64];
-    __shared__ uint32_t rows[64 * 33];  // final rows, stride 33 dwords (no bank conflicts)
-    const uint32_t b = a.blk_map[blockIdx.x];
-    const uint32_t lane = threadIdx.x;
-    const uint32_t e = a.erased_off[b + 1] - a.erased_off[b];
-    const uint32_t nr = a.rep_cnt[b];
-    if (e > 64) {
-        if (lane == 0) a.status[b] = ST_FALLBACK;
-        return;
-    }
-    const uint32_t nrow = min(nr, 64u);
-    const uint32_t* E = a.erased + a.erased_off[b];
-    const uint32_t* U = a.rep_uidx + a.rep_off[b];
-    gf_tables_copy(ex, lg);
-    uint32_t row[32];
-#pragma unroll
-    for (int w = 0; w < 32; ++w) row[w] = 0;
-    if (lane < nrow) {
-        const uint8_t* mr = a.mrep + (size_t)U[lane] * a.mrep_stride;
-#pragma unroll
-        for (int w = 0; w < 16; ++w)
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                if ((uint32_t)(4 * w + i) < e) row[w] |= (uint32_t)mr[E[4 * w + i]] << (8 * i);
-        const uint32_t pos = e + lane;
-#pragma unroll
-        for (int w = 0; w < 32; ++w)
-            if ((pos >> 2) == (uint32_t)w) row[w] |= 1u << (8 * (pos & 3));
-    }
-    bool used = lane >= nrow;
-    const uint32_t q1 = (e + nrow + 3) >> 2;  // live dwords
-    __syncthreads();                          // GF tables
-    for (uint32_t k = 0; k < e; ++k) {
-        const uint32_t W = k >> 2;
-        uint32_t rw = 0;
-#pragma unroll
-        for (int w = 0; w < 16; ++w)
-            if ((uint32_t)w == W) rw = row[w];
-        const uint32_t f = (rw >> (8 * (k & 3))) & 0xFFu;
-        const uint64_t bal = __ballot(f != 0 && !used);
-        if (bal == 0) {  // rank-deficient on these rows (uniform)
-            if (lane == 0) a.status[b] = (nr > nrow) ? ST_FALLBACK : 0;
-            return;
-        }
-        const uint32_t p = (uint32_t)__ffsll((unsigned long long)bal) - 1;
-        const bool me = lane == p;
-        used |= me;
-        const uint32_t fp = (uint32_t)__builtin_amdgcn_readlane((int)f, (int)p);
-        const uint32_t lginv = 255u - lg[fp];
-        uint32_t c = f ? ex[lg[f] + lginv] : 0u;
-        if (me) c = ex[lginv] ^ 1u;
-        uint4 A;
-        uint32_t B;
-        perm_tables(c, &A, &B);
-#pragma unroll
-        for (int w = 0; w < 32; ++w) {
-            if ((uint32_t)w >= W && (uint32_t)w < q1) {
-                const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)row[w], (int)p);
-                row[w] ^= perm_mul(A, B, x);
-            }
-        }
-        if (lane == 0) pivl[k] = (uint8_t)p;
-    }
-#pragma unroll
-    for (int w = 0; w < 32; ++w) rows[lane * 33 + w] = row[w];
-    __syncthreads();
-    // X[k][m] = identity byte (e + piv_m) of pivot row piv_k
-    uint8_t* xc = a.xcoef + 64ull * a.xoff[blockIdx.x];
-    const uint32_t xs = x_stride(e);
-    uint16_t* XP = a.xpiv + a.erased_off[b];
-    for (uint32_t m = lane; m < e; m += 64) XP[m] = pivl[m];
-    const uint8_t* rb = reinterpret_cast<const uint8_t*>(rows);
-    for (uint32_t idx = lane; idx < e * e; idx += 64) {
-        const uint32_t m = idx / e, k = idx - m * e;
-        xc[m * xs + k] = rb[pivl[k] * 132 + e + pivl[m]];
-    }
-    if (lane == 0) a.status[b] = 1;
-}
 
-// One wave per block, rows in registers, for e <= 64 on the first e + margin (<= 64) received
-// repairs: a lean first-pass solver (RQHIP_SOLVE_LEAN=1 in experiments builds).  Lane j owns received
-// repair j as 32 dwords (e coefficient bytes, then the identity part at byte e + j).  Each step k takes
-// the lowest unused row with a nonzero coefficient in column k (ballot); the pivot lane posts its live
-// dwords to LDS, every lane reads them back (one broadcast address per b128) and folds c_j times the
-// pivot row into its own (c_j = f_j / f_p, the pivot lane 1 ^ 1/f_p, which leaves row_p / f_p), with
-// c_j's v_perm tables read from an LDS copy of kPerm by log c_j and the pivot dwords made scalar, so
-// the selectors are SALU work.  Against k_solve_reg: no per-step table build (~70 VALU), no v_readlane
-// per pivot dword; against k_solve_pq: one wave and ~9 KB of LDS per block and no barrier, so blocks
-// also fit beside the syndrome program's waves.
-__global__ void __launch_bounds__(64) k_solve_lean(SolveArgs a) {
-    __shared__ __attribute__((aligned(4))) uint8_t ex[512], lg[256];
-    __shared__ uint8_t pivl[64];
-    __shared__ __attribute__((aligned(16))) uint4 prow_s[8];  // the pivot row's live dwords, by quad
-    // the coefficient tables and pivot infos during the elimination; the final rows after it
-    constexpr uint32_t RS = 33;  // final row stride (dwords; no bank conflicts)
-    __shared__ __attribute__((aligned(16))) uint32_t un[64 * RS];
-    uint4* tlA = reinterpret_cast<uint4*>(un);    // [255]
-    uint32_t* tlB = un + 4 * 255;                 // [255]
-    uint32_t* pinfo = tlB + 255;                  // [256]: log f | log(1 ^ 1/f) << 8 | (1 ^ 1/f != 0) << 16
-    const uint32_t lane = threadIdx.x;
-    if (a.status_init)  // the host-decided statuses (disjoint from the solver's blocks, ST_PENDING)
-        for (uint32_t i = blockIdx.x * 64 + lane; i < a.n_all; i += gridDim.x * 64)
-            if (a.status_init[i] != ST_PENDING) a.status[i] = a.status_init[i];
-    const uint32_t b = a.blk_map[blockIdx.x];
-    const uint32_t e = a.erased_off[b + 1] - a.erased_off[b];
-    const uint32_t nr = a.rep_cnt[b];
-    if (e > 64) {
-        if (lane == 0) a.status[b] = ST_FALLBACK;
-        return;
-    }
-    const uint32_t nrow = a.row_margin ? min(min(nr, 64u), e + a.row_margin) : min(nr, 64u);
-    const uint32_t* E = a.erased + a.erased_off[b];
-    const uint32_t* U = a.rep_uidx + a.rep_off[b];
-    gf_tables_copy(ex, lg);
-    for (uint32_t l = lane; l < 255; l += 64) {
-        tlA[l] = make_uint4(kPerm.A[l][0], kPerm.A[l][1], kPerm.A[l][2], kPerm.A[l][3]);
-        tlB[l] = kPerm.B[l];
-    }
-    uint32_t row[32];
-#pragma unroll
-    for (int w = 0; w < 32; ++w) row[w] = 0;
-    if (lane < nrow) {  // every byte load of the row in flight at once
-        const uint8_t* mr = a.mrep + (size_t)U[lane] * a.mrep_stride;
-#pragma unroll
-        for (int w = 0; w < 16; ++w)
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                if ((uint32_t)(4 * w + i) < e) row[w] |= (uint32_t)mr[E[4 * w + i]] << (8 * i);
-        const uint32_t pos = e + lane;
-#pragma unroll
-        for (int w = 0; w < 32; ++w)
-            if ((pos >> 2) == (uint32_t)w) row[w] |= 1u << (8 * (pos & 3));
-    }
-    __syncthreads();  // ex / lg
-    for (uint32_t x = lane; x < 256; x += 64) {
-        uint32_t v = 0;
-        if (x) {
-            const uint32_t lx = lg[x], cp = 1u ^ ex[255u - lx];
-            v = lx | (cp ? (uint32_t)lg[cp] << 8 | 1u << 16 : 0u);
-        }
-        pinfo[x] = v;
-    }
-    __syncthreads();  // tables and pinfo
-    bool used = lane >= nrow;
-    const uint32_t q1 = (e + nrow + 3) >> 2;  // live dwords
-    for (uint32_t k = 0; k < e; ++k) {
-        const uint32_t W = k >> 2;
-        uint32_t rw = 0;
-#pragma unroll
-        for (int w = 0; w < 16; ++w)
-            if ((uint32_t)w == W) rw = row[w];
-        const uint32_t f = (rw >> (8 * (k & 3))) & 0xFFu;
-        const uint64_t bal = __ballot(f != 0 && !used);
-        if (bal == 0) {  // rank-deficient on these rows (uniform)
-            if (lane == 0) a.status[b] = (nr > nrow) ? ST_FALLBACK : 0;
-            return;
-        }
-        const uint32_t p = (uint32_t)__ffsll((unsigned long long)bal) - 1;
-        const bool me = lane == p;
-        used |= me;
-        const uint32_t pif = pinfo[f];
-        // the pivot lane posts its live dwords (quads from W / 4; columns < k are zero there)
-        const uint32_t w4 = W >> 2, q4 = (q1 + 3) >> 2;
-        if (me) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                if ((uint32_t)j >= w4 && (uint32_t)j < q4)
-                    prow_s[j] = make_uint4(row[4 * j], row[4 * j + 1], row[4 * j + 2], row[4 * j + 3]);
-        }
-        const uint32_t pip = (uint32_t)__builtin_amdgcn_readlane((int)pif, (int)p);
-        const uint32_t ilgp = 255u - (pip & 0xFFu);
-        uint32_t l = me ? (pif >> 8) & 0xFFu : (pif & 0xFFu) + ilgp;
-        l = l >= 255u ? l - 255u : l;
-        const bool act = me ? (pif >> 16) != 0 : f != 0;
-        const uint4 A = tlA[act ? l : 0];
-        const uint32_t B = tlB[act ? l : 0];
-        __builtin_amdgcn_wave_barrier();  // (LDS operations of one wave complete in order)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            if ((uint32_t)j < w4 || (uint32_t)j >= q4) continue;  // uniform
-            const uint4 P = prow_s[j];
-            const uint32_t px[4] = {(uint32_t)__builtin_amdgcn_readfirstlane(P.x), (uint32_t)__builtin_amdgcn_readfirstlane(P.y),
-                                    (uint32_t)__builtin_amdgcn_readfirstlane(P.z), (uint32_t)__builtin_amdgcn_readfirstlane(P.w)};
-#pragma unroll
-            for (int d = 0; d < 4; ++d) {
-                const uint32_t m = act ? perm_mul(A, B, px[d]) : 0u;
-                row[4 * j + d] ^= m;
-            }
-        }
-        if (lane == 0) pivl[k] = (uint8_t)p;
-        __builtin_amdgcn_wave_barrier();
-    }
-    // the final rows into LDS (over the tables), X[k][m] = identity byte (e + piv_m) of pivot row piv_k
-    __syncthreads();
-#pragma unroll
-    for (int w = 0; w < 32; ++w) un[lane * RS + w] = row[w];
-    __syncthreads();
-    uint8_t* xc = a.xcoef + 64ull * a.xoff[blockIdx.x];
-    const uint32_t xs = x_stride(e);
-    uint16_t* XP = a.xpiv + a.erased_off[b];
-    for (uint32_t m = lane; m < e; m += 64) XP[m] = pivl[m];
-    const uint8_t* rb = reinterpret_cast<const uint8_t*>(un);
-    for (uint32_t m = 0; m < e; ++m) {  // row m of X: one byte per lane, no index division
-        const uint32_t pm = pivl[m];
-        for (uint32_t k = lane; k < e; k += 64) xc[m * xs + k] = rb[pivl[k] * (RS * 4) + e + pm];
-    }
-    if (lane == 0) a.status[b] = 1;
-}
 
 // General solver for the blocks the fast solvers deferred: any e, every received repair.  The
 // received rows are taken in order and reduced against a Gauss-Jordan basis of the rows kept so far
@@ -1017,134 +405,71 @@ size_t solve_ws_bytes(uint32_t e) {
     return W2 + ((e + 15) & ~15u) + 4 * ((e + 7) & ~7u) + (size_t)e * W2;
 }
 
-// The e <= 64 solver: k_solve_fast<1> with four waves per block; experiments builds select one wave
-// (RQHIP_SOLVE_NW=1) or the register-resident k_solve_reg (RQHIP_SOLVE_NW=0; measured 111 us against
-// 94 us for the four-wave solver at 1 024 blocks, e = 55: profiles/r02r).
-// Elimination by GF(256) multiplication (k_solve_pm, the default) or by alpha-multiple tables
-// (k_solve_fast: RQHIP_SOLVE_PM=0 in experiments builds).  Measured at 1 024 blocks K=1024, e ~ 52:
-// decode 0.810 against 0.820 ms per step; the e ~ 113 wide pass at K=2048: 192 against 237 us
-// (profiles/r02ag).
-static bool solve_pm() {
 #ifdef RQHIP_EXPERIMENTS
-    static const bool on = [] { const char* e = std::getenv("RQHIP_SOLVE_PM"); return !(e && e[0] == '0'); }();
-    return on;
-#else
-    return true;
-#endif
+// Experiments builds: the solver variants measured and not shipped (rq_kernels_exp.hip) behind knobs.
+// RQHIP_SOLVE_PM=0: alpha-multiple tables (k_solve_fast) instead of GF(256) multiplication; RQHIP_SOLVE_LUT=0:
+// per-step table builds (k_solve_pm<..., false>); RQHIP_SOLVE_PQ=0: k_solve_pm instead of k_solve_pq;
+// RQHIP_SOLVE_PF=1: k_solve_pq's pinfo column buffer; RQHIP_SOLVE_LEAN=1: k_solve_lean; RQHIP_SOLVE_NW:
+// waves per block (1, 2, 4, 8; 0 = k_solve_reg).  Measurements: profiles/r02ag, r02r, r03_solve2, r04j, r04l.
+int launch_solve_exp_first(const SolveArgs& first, const SolveArgs& a, uint32_t n_blocks, bool pm, bool lut, bool pq,
+                           bool lean, int nw, void* stream);
+int launch_solve_exp_wide(const SolveArgs& a, uint32_t n_blocks, bool pm, bool lut, bool pq, void* stream);
+static bool knob_on(const char* name, bool dflt) {
+    const char* e = std::getenv(name);
+    return e ? e[0] != '0' : dflt;
 }
-
-// k_solve_pm's coefficient tables from a per-block log-indexed LUT (the default; RQHIP_SOLVE_LUT=0 in
-// experiments builds builds them per step): the solve is VALU-bound at four blocks per CU, and the
-// per-step perm_tables were ~40 VALU per lane.  Decode 0.806 -> 0.790 ms, wide pass 194 -> 182 us
-// (profiles/r02ag/lut).
-static bool solve_lut() {
-#ifdef RQHIP_EXPERIMENTS
-    static const bool on = [] { const char* e = std::getenv("RQHIP_SOLVE_LUT"); return !(e && e[0] == '0'); }();
-    return on;
-#else
-    return true;
 #endif
-}
-
-// k_solve_pq (the default) against k_solve_pm (RQHIP_SOLVE_PQ=0 in experiments builds)
-static bool solve_pq() {
-#ifdef RQHIP_EXPERIMENTS
-    static const bool on = [] { const char* e = std::getenv("RQHIP_SOLVE_PQ"); return !(e && e[0] == '0'); }();
-    return on;
-#else
-    return true;
-#endif
-}
-
-// k_solve_pq's column buffer with pinfo words (RQHIP_SOLVE_PF=1 in experiments builds)
-static bool solve_pf() {
-#ifdef RQHIP_EXPERIMENTS
-    static const bool on = [] { const char* e = std::getenv("RQHIP_SOLVE_PF"); return e && e[0] == '1'; }();
-    return on;
-#else
-    return false;
-#endif
-}
-
-// the lean one-wave first-pass solver (k_solve_lean; RQHIP_SOLVE_LEAN=1 in experiments builds)
-static bool solve_lean() {
-#ifdef RQHIP_EXPERIMENTS
-    static const bool on = [] { const char* e = std::getenv("RQHIP_SOLVE_LEAN"); return e && e[0] == '1'; }();
-    return on;
-#else
-    return false;
-#endif
-}
-
-static int solve_nw() {
-#ifdef RQHIP_EXPERIMENTS
-    static const int nw = [] {
-        const char* e = std::getenv("RQHIP_SOLVE_NW");
-        return e ? std::atoi(e) : 4;
-    }();
-    return nw;
-#else
-    return 4;
-#endif
-}
 
 int launch_solve(const SolveArgs& a_in, uint32_t n_blocks, bool need_general, bool wide, uint32_t max_lds_e,
                  void* stream) {
-    // the first k_solve_pm launch copies the host-decided statuses (a_in.status_init); the other
-    // solvers get them uploaded first, and later launches never copy
-    SolveArgs first = a_in;  // the first pass copies the host-decided statuses
+    // the first solver launch copies the host-decided statuses (a_in.status_init); later launches never do
+    SolveArgs first = a_in;
     first.diag_steps = 0;
+    const hipStream_t st = (hipStream_t)stream;
 #ifdef RQHIP_EXPERIMENTS
     static const uint32_t dsteps = [] { const char* e = std::getenv("RQHIP_SOLVE_STEPS"); return e ? (uint32_t)std::atoi(e) : 0u; }();
     first.diag_steps = dsteps;
 #endif
     SolveArgs a = first;
     a.status_init = nullptr;
-    const bool pm_first = solve_lean() || solve_nw() == 8 ||
-                          (solve_pm() && (solve_nw() == 1 || solve_nw() == 2 || solve_nw() == 4));
-    if (a_in.status_init && !pm_first &&
-        hipMemcpyAsync(a.status, a_in.status_init, (size_t)a_in.n_all * 4, hipMemcpyHostToDevice,
-                       (hipStream_t)stream) != hipSuccess)
+#ifdef RQHIP_EXPERIMENTS
+    static const bool pm = knob_on("RQHIP_SOLVE_PM", true), lut = knob_on("RQHIP_SOLVE_LUT", true),
+                      pq = knob_on("RQHIP_SOLVE_PQ", true), pf = knob_on("RQHIP_SOLVE_PF", false),
+                      lean = knob_on("RQHIP_SOLVE_LEAN", false);
+    static const int nw = [] { const char* e = std::getenv("RQHIP_SOLVE_NW"); return e ? std::atoi(e) : 4; }();
+    // solvers that take `a` (statuses uploaded first): k_solve_fast and k_solve_reg
+    const bool takes_a = !lean && ((nw == 1 && !pm) || (nw == 4 && !pm) || (nw != 1 && nw != 2 && nw != 4 && nw != 8));
+    if (a_in.status_init && takes_a &&
+        hipMemcpyAsync(a.status, a_in.status_init, (size_t)a_in.n_all * 4, hipMemcpyHostToDevice, st) != hipSuccess)
         return (int)hipGetLastError();
-    if (solve_lean()) hipLaunchKernelGGL(k_solve_lean, dim3(n_blocks), dim3(64), 0, (hipStream_t)stream, first);
-    else switch (solve_nw()) {
-        case 1:
-            if (solve_pm() && solve_pq()) hipLaunchKernelGGL((k_solve_pq<1, 1>), dim3(n_blocks), dim3(64), 0, (hipStream_t)stream, first);
-            else if (solve_pm()) hipLaunchKernelGGL((k_solve_pm<1, 1, true>), dim3(n_blocks), dim3(64), 0, (hipStream_t)stream, first);
-            else hipLaunchKernelGGL((k_solve_fast<1, 1>), dim3(n_blocks), dim3(64), 0, (hipStream_t)stream, a);
-            break;
-        case 8:  // experiments: eight waves per block
-            hipLaunchKernelGGL((k_solve_pq<1, 8>), dim3(n_blocks), dim3(512), 0, (hipStream_t)stream, first);
-            break;
-        case 2:
-            if (solve_pq()) hipLaunchKernelGGL((k_solve_pq<1, 2>), dim3(n_blocks), dim3(128), 0, (hipStream_t)stream, first);
-            else hipLaunchKernelGGL((k_solve_pm<1, 2, true>), dim3(n_blocks), dim3(128), 0, (hipStream_t)stream, first);
-            break;
-        case 4:
-            if (solve_pm() && solve_lut() && solve_pq() && solve_pf())
-                hipLaunchKernelGGL((k_solve_pq<1, 4, true>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, first);
-            else if (solve_pm() && solve_lut() && solve_pq())
-                hipLaunchKernelGGL((k_solve_pq<1, 4>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, first);
-            else if (solve_pm() && solve_lut())
-                hipLaunchKernelGGL((k_solve_pm<1, 4, true>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, first);
-            else if (solve_pm())
-                hipLaunchKernelGGL((k_solve_pm<1, 4, false>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, first);
-            else hipLaunchKernelGGL((k_solve_fast<1, 4>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a);
-            break;
-        default: hipLaunchKernelGGL(k_solve_reg, dim3(n_blocks), dim3(64), 0, (hipStream_t)stream, a); break;
+    int rx = launch_solve_exp_first(first, a, n_blocks, pm, lut, pq, lean, nw, stream);
+    if (rx == -1) {
+        if (nw == 1) hipLaunchKernelGGL((k_solve_pq<1, 1>), dim3(n_blocks), dim3(64), 0, st, first);
+        else if (nw == 2) hipLaunchKernelGGL((k_solve_pq<1, 2>), dim3(n_blocks), dim3(128), 0, st, first);
+        else if (nw == 8) hipLaunchKernelGGL((k_solve_pq<1, 8>), dim3(n_blocks), dim3(512), 0, st, first);
+        else if (pf) hipLaunchKernelGGL((k_solve_pq<1, 4, true>), dim3(n_blocks), dim3(256), 0, st, first);
+        else hipLaunchKernelGGL((k_solve_pq<1, 4>), dim3(n_blocks), dim3(256), 0, st, first);
+        rx = (int)hipGetLastError();
     }
+    if (rx != hipSuccess || !need_general) return rx;
+    if (wide) {  // blocks with 64 < e <= 128; the rare rank-deficient-on-64-rows block goes to k_solve
+        int rw = launch_solve_exp_wide(a, n_blocks, pm, lut, pq, stream);
+        if (rw == -1) {
+            hipLaunchKernelGGL((k_solve_pq<2, 4>), dim3(n_blocks), dim3(256), 0, st, a);
+            rw = (int)hipGetLastError();
+        }
+        if (rw != hipSuccess) return rw;
+    }
+#else
+    // e <= 64 on the first e + margin received repairs (statuses copied in by this launch)
+    hipLaunchKernelGGL((k_solve_pq<1, 4>), dim3(n_blocks), dim3(256), 0, st, first);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !need_general) return (int)e;
     if (wide) {  // blocks with 64 < e <= 128; the rare rank-deficient-on-64-rows block goes to k_solve
-        if (solve_pm() && solve_lut() && solve_pq())
-            hipLaunchKernelGGL((k_solve_pq<2, 4>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a);
-        else if (solve_pm() && solve_lut())
-            hipLaunchKernelGGL((k_solve_pm<2, 4, true>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a);
-        else if (solve_pm())
-            hipLaunchKernelGGL((k_solve_pm<2, 4, false>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a);
-        else hipLaunchKernelGGL((k_solve_fast<2, 4>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, a);
+        hipLaunchKernelGGL((k_solve_pq<2, 4>), dim3(n_blocks), dim3(256), 0, st, a);
         if ((e = hipGetLastError()) != hipSuccess) return (int)e;
     }
+#endif
     // k_solve's dynamic-LDS limit is a per-device attribute, and the host-memory API drives one host thread
     // per device (run_sharded): set it once per device, race-free, on the device this thread launches on
     static std::once_flag attr_once[64];
@@ -1426,27 +751,28 @@ static void launch_apply_cpl(const ApplyArgs& a, uint32_t kc, dim3 g, uint32_t e
     // one-at-a-time loop): 185 -> 178 us at 1 024 blocks K=1024, two interleaved rounds on one box
     // (profiles/r03_apply2).  The look-ahead of a chunk's last pair reads up to 2 KC table entries past
     // it, hence the slack.
-#ifdef RQHIP_EXPERIMENTS
-    static const bool pair = [] { const char* e = std::getenv("RQHIP_APPLY_PAIR"); return !(e && e[0] == '0'); }();
+#ifndef RQHIP_EXPERIMENTS
+    // the shipped shapes: syndromes in pairs, KC = 4 at four waves per SIMD, KC = 8 at three (under four's
+    // 128 VGPRs the KC = 8 pair loop spills 11 at CPL 5: 170.9 against 177.1 us, profiles/r03_apply2/occ).
+    // launch_apply's cap keeps kc at 4 or 8.
+    static_assert(PD == 2 && KCMAX == 8, "release k_apply shape");
+    if (kc <= 4) hipLaunchKernelGGL((k_apply<4, CPL, 2, OCC, true>), g, dim3(64), lds + 40 * 4, st, a, nu, np, mc);
+    else hipLaunchKernelGGL((k_apply<8, CPL, 2, 3, true>), g, dim3(64), lds + 40 * 8, st, a, nu, np, mc);
 #else
-    constexpr bool pair = true;
-#endif
+    // experiments: RQHIP_APPLY_PAIR=0 restores the one-syndrome-at-a-time loop, RQHIP_APPLY_PAIROCC=4 the
+    // KC = 8 pair loop at four waves per SIMD, RQHIP_APPLY_KC the wider slices (KC 12..24)
+    static const bool pair = [] { const char* e = std::getenv("RQHIP_APPLY_PAIR"); return !(e && e[0] == '0'); }();
     if constexpr (PD == 2 && KCMAX == 8) {
         if (pair && kc <= 4) {
             hipLaunchKernelGGL((k_apply<4, CPL, 2, OCC, true>), g, dim3(64), lds + 40 * 4, st, a, nu, np, mc);
             return;
         }
         if (pair && kc == 8) {
-            // the KC = 8 pair loop at three waves per SIMD: under four's 128 VGPRs it spills 11 (CPL 5);
-            // 170.9 against 177.1 us, three interleaved rounds (profiles/r03_apply2/occ);
-            // RQHIP_APPLY_PAIROCC=4 in experiments builds restores four
-#ifdef RQHIP_EXPERIMENTS
             static const bool occ4p = [] { const char* e = std::getenv("RQHIP_APPLY_PAIROCC"); return e && e[0] == '4'; }();
             if (occ4p) {
                 hipLaunchKernelGGL((k_apply<8, CPL, 2, OCC, true>), g, dim3(64), lds + 40 * 8, st, a, nu, np, mc);
                 return;
             }
-#endif
             hipLaunchKernelGGL((k_apply<8, CPL, 2, 3, true>), g, dim3(64), lds + 40 * 8, st, a, nu, np, mc);
             return;
         }
@@ -1462,6 +788,7 @@ static void launch_apply_cpl(const ApplyArgs& a, uint32_t kc, dim3 g, uint32_t e
         }
     }
     hipLaunchKernelGGL((k_apply<8, CPL, PD, OCC>), g, dim3(64), lds, st, a, nu, np, mc);
+#endif
 }
 
 #ifdef RQHIP_EXPERIMENTS

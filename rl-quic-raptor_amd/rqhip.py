@@ -23,7 +23,10 @@ from pathlib import Path
 _HERE = Path(__file__).resolve().parent
 # RQHIP_LIB names an alternative build of the same library (tools/build_experiments.sh) for tuning runs
 LIB_PATH = Path(os.environ["RQHIP_LIB"]).resolve() if os.environ.get("RQHIP_LIB") else _HERE / "build" / "librqhip.so"
+# the experiments variant (RQHIP_* knobs; the pair and four-row-staging programs, the unshipped solvers)
+EXP_LIB_PATH = _HERE / "build_exp" / "librqhip.so"
 _lib = None
+_exp_lib = None
 
 RQ_OK = 0
 RQ_ERR_SYMBOL_SIZE_ZERO = -1
@@ -44,7 +47,7 @@ EXPORTED = (
     "rq_decode_blocks_host", "rq_host_alloc", "rq_host_free", "rq_debug_colprog_passes",
     "rq_debug_shard_plan", "rq_debug_virtual_shards", "rq_debug_tuple", "rq_stream_release", "rq_shutdown",
     "rq_launch_timing", "rq_launch_time", "rq_debug_pair_emulate", "rq_debug_dma4_emulate", "rq_debug_decode_plan",
-    "rq_debug_assemble", "rq_debug_colprog_bound",
+    "rq_debug_assemble", "rq_debug_colprog_bound", "rq_debug_cache_roundtrip",
 )
 
 
@@ -117,80 +120,103 @@ def lib():
     global _lib
     if _lib is None:
         ensure_built()
-        # One HIP runtime per process: PyTorch-ROCm bundles its own libamdhip64.so.7 (same soname as
-        # /opt/rocm's).  Loaded first, torch's copy also serves librqhip.so's NEEDED entry; loaded after
-        # librqhip.so, a second runtime initialises the device beside the first and the library's
-        # hipGetDeviceCount then fails (seen on the GPU box, r03h).  The Python mirror exchanges device
-        # tensors and streams with torch, so it loads torch's runtime first when torch is present.
-        try:
-            import torch  # noqa: F401
-        except ImportError:
-            pass
-        L = ctypes.CDLL(str(LIB_PATH))
-        u8p = ctypes.POINTER(ctypes.c_uint8)
-        u16p = ctypes.POINTER(ctypes.c_uint16)
-        u32p = ctypes.POINTER(ctypes.c_uint32)
-        ip = ctypes.POINTER(ctypes.c_int)
-        vp = ctypes.c_void_p
-        sig = {
-            "rq_strerror": ([ctypes.c_int], ctypes.c_char_p),
-            "rq_last_error": ([], ctypes.c_char_p),
-            "rq_params": ([ctypes.c_uint64, ctypes.c_uint32, u32p], ctypes.c_int),
-            "rq_encoder_create": ([u8p, ctypes.c_size_t, ctypes.c_uint32, ip], vp),
-            "rq_encoder_k": ([vp], ctypes.c_uint32),
-            "rq_encoder_symbol_size": ([vp], ctypes.c_uint32),
-            "rq_encoder_symbol": ([vp, ctypes.c_uint32, u8p], ctypes.c_int),
-            "rq_encoder_symbols": ([vp, ctypes.c_uint32, ctypes.c_uint32, u8p], ctypes.c_int),
-            "rq_encoder_free": ([vp], None),
-            "rq_decoder_create": ([ctypes.c_uint64, ctypes.c_uint32, ip], vp),
-            "rq_decoder_k": ([vp], ctypes.c_uint32),
-            "rq_decoder_add": ([vp, ctypes.c_uint32, u8p, ctypes.c_size_t, ip], ctypes.c_int),
-            "rq_decoder_decode": ([vp, u8p, ip], ctypes.c_int),
-            "rq_decoder_free": ([vp], None),
-            "rq_encode_batch": ([ctypes.POINTER(EncodeDesc)], ctypes.c_int),
-            "rq_decode_batch": ([ctypes.POINTER(DecodeDesc)], ctypes.c_int),
-            "rq_decode_batch_async": ([ctypes.POINTER(DecodeDesc)], ctypes.c_int),
-            "rq_encode_batch_host": ([ctypes.POINTER(EncodeDesc), ctypes.c_uint32], ctypes.c_int),
-            "rq_decode_batch_host": ([ctypes.POINTER(DecodeDesc), ctypes.c_uint32], ctypes.c_int),
-            "rq_device_count": ([], ctypes.c_int),
-            "rq_set_device": ([ctypes.c_int], ctypes.c_int),
-            "rq_debug_colprog_eval": ([ctypes.c_uint32, ctypes.c_uint32, u32p, ctypes.c_uint32, vp, vp, u32p],
-                                      ctypes.c_int),
-            "rq_debug_colprog_emulate": ([ctypes.c_uint32, ctypes.c_uint32, u32p, ctypes.c_uint32, vp, vp, u32p, u32p,
-                                          ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)],
-                                         ctypes.c_int),
-            "rq_debug_colprog_assemble": ([ctypes.c_uint32, u32p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_size_t)],
-                                          ctypes.c_int),
-            "rq_debug_decode_margin": ([ctypes.c_uint32], ctypes.c_uint32),
-            "rq_decode_blocks_host": ([ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(BlockIO), ctypes.c_uint32,
-                                       ctypes.c_uint32], ctypes.c_int),
-            "rq_host_alloc": ([ctypes.c_size_t], vp),
-            "rq_host_free": ([vp], None),
-            "rq_debug_colprog_passes": ([ctypes.c_int], ctypes.c_int),
-            "rq_debug_shard_plan": ([ctypes.c_uint32, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ip, u32p, u32p,
-                                     ctypes.c_uint32], ctypes.c_int),
-            "rq_debug_virtual_shards": ([ctypes.c_uint32], ctypes.c_uint32),
-            "rq_debug_tuple": ([ctypes.c_uint32, ctypes.c_uint32, u32p], ctypes.c_int),
-            "rq_stream_release": ([vp], ctypes.c_int),
-            "rq_shutdown": ([], ctypes.c_int),
-            "rq_launch_timing": ([ctypes.c_int], ctypes.c_int),
-            "rq_launch_time": ([ctypes.POINTER(ctypes.c_double), u32p, ctypes.c_int], ctypes.c_int),
-            "rq_debug_pair_emulate": ([ctypes.c_uint32, ctypes.c_uint32, u32p, ctypes.c_uint32, vp, vp, u32p, u32p,
-                                       ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
-            "rq_debug_decode_plan": ([ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, u32p, u32p, u32p, u32p, ctypes.c_uint32,
-                                      ctypes.POINTER(ctypes.c_double), u32p], ctypes.c_int),
-            "rq_debug_dma4_emulate": ([ctypes.c_uint32, ctypes.c_uint32, u32p, ctypes.c_uint32, vp, vp, ctypes.c_uint32,
-                                       ctypes.c_uint32, u32p, ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
-            "rq_debug_assemble": ([ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
-            "rq_debug_colprog_bound": ([ctypes.c_uint32, ctypes.c_uint32, u32p, ctypes.c_uint32, vp, vp, ctypes.c_uint64,
-                                        u32p], ctypes.c_int),
-        }
-        for name, (args, res) in sig.items():
-            f = getattr(L, name)
-            f.argtypes = args
-            f.restype = res
-        _lib = L
+        _lib = _load(LIB_PATH)
     return _lib
+
+
+def exp_lib():
+    """The experiments library (tools/build_experiments.sh), built on first use; its own ctypes handle
+    beside the release library's.  The pair / four-row-staging debug entry points work only here."""
+    global _exp_lib
+    if _exp_lib is None:
+        if EXP_LIB_PATH == LIB_PATH:
+            _exp_lib = lib()
+            return _exp_lib
+        if not EXP_LIB_PATH.exists():
+            try:
+                subprocess.run(["bash", str(_HERE.parent / "tools" / "build_experiments.sh")], check=True)
+            except (OSError, subprocess.CalledProcessError) as ex:
+                raise RaptorQError(RQ_ERR_DEVICE, "experiments library could not be built: %s" % ex) from ex
+        _exp_lib = _load(EXP_LIB_PATH)
+    return _exp_lib
+
+
+def _load(path):
+    """dlopen one build of librqhip.so and set its ctypes signatures."""
+    # One HIP runtime per process: PyTorch-ROCm bundles its own libamdhip64.so.7 (same soname as
+    # /opt/rocm's).  Loaded first, torch's copy also serves librqhip.so's NEEDED entry; loaded after
+    # librqhip.so, a second runtime initialises the device beside the first and the library's
+    # hipGetDeviceCount then fails (seen on the GPU box, r03h).  The Python mirror exchanges device
+    # tensors and streams with torch, so it loads torch's runtime first when torch is present.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    L = ctypes.CDLL(str(path))
+    u8p = ctypes.POINTER(ctypes.c_uint8)
+    u16p = ctypes.POINTER(ctypes.c_uint16)
+    u32p = ctypes.POINTER(ctypes.c_uint32)
+    ip = ctypes.POINTER(ctypes.c_int)
+    vp = ctypes.c_void_p
+    sig = {
+        "rq_strerror": ([ctypes.c_int], ctypes.c_char_p),
+        "rq_last_error": ([], ctypes.c_char_p),
+        "rq_params": ([ctypes.c_uint64, ctypes.c_uint32, u32p], ctypes.c_int),
+        "rq_encoder_create": ([u8p, ctypes.c_size_t, ctypes.c_uint32, ip], vp),
+        "rq_encoder_k": ([vp], ctypes.c_uint32),
+        "rq_encoder_symbol_size": ([vp], ctypes.c_uint32),
+        "rq_encoder_symbol": ([vp, ctypes.c_uint32, u8p], ctypes.c_int),
+        "rq_encoder_symbols": ([vp, ctypes.c_uint32, ctypes.c_uint32, u8p], ctypes.c_int),
+        "rq_encoder_free": ([vp], None),
+        "rq_decoder_create": ([ctypes.c_uint64, ctypes.c_uint32, ip], vp),
+        "rq_decoder_k": ([vp], ctypes.c_uint32),
+        "rq_decoder_add": ([vp, ctypes.c_uint32, u8p, ctypes.c_size_t, ip], ctypes.c_int),
+        "rq_decoder_decode": ([vp, u8p, ip], ctypes.c_int),
+        "rq_decoder_free": ([vp], None),
+        "rq_encode_batch": ([ctypes.POINTER(EncodeDesc)], ctypes.c_int),
+        "rq_decode_batch": ([ctypes.POINTER(DecodeDesc)], ctypes.c_int),
+        "rq_decode_batch_async": ([ctypes.POINTER(DecodeDesc)], ctypes.c_int),
+        "rq_encode_batch_host": ([ctypes.POINTER(EncodeDesc), ctypes.c_uint32], ctypes.c_int),
+        "rq_decode_batch_host": ([ctypes.POINTER(DecodeDesc), ctypes.c_uint32], ctypes.c_int),
+        "rq_device_count": ([], ctypes.c_int),
+        "rq_set_device": ([ctypes.c_int], ctypes.c_int),
+        "rq_debug_colprog_eval": ([ctypes.c_uint32, ctypes.c_uint32, u32p, ctypes.c_uint32, vp, vp, u32p],
+                                  ctypes.c_int),
+        "rq_debug_colprog_emulate": ([ctypes.c_uint32, ctypes.c_uint32, u32p, ctypes.c_uint32, vp, vp, u32p, u32p,
+                                      ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)],
+                                     ctypes.c_int),
+        "rq_debug_colprog_assemble": ([ctypes.c_uint32, u32p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_size_t)],
+                                      ctypes.c_int),
+        "rq_debug_decode_margin": ([ctypes.c_uint32], ctypes.c_uint32),
+        "rq_decode_blocks_host": ([ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(BlockIO), ctypes.c_uint32,
+                                   ctypes.c_uint32], ctypes.c_int),
+        "rq_host_alloc": ([ctypes.c_size_t], vp),
+        "rq_host_free": ([vp], None),
+        "rq_debug_colprog_passes": ([ctypes.c_int], ctypes.c_int),
+        "rq_debug_shard_plan": ([ctypes.c_uint32, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ip, u32p, u32p,
+                                 ctypes.c_uint32], ctypes.c_int),
+        "rq_debug_virtual_shards": ([ctypes.c_uint32], ctypes.c_uint32),
+        "rq_debug_tuple": ([ctypes.c_uint32, ctypes.c_uint32, u32p], ctypes.c_int),
+        "rq_stream_release": ([vp], ctypes.c_int),
+        "rq_shutdown": ([], ctypes.c_int),
+        "rq_launch_timing": ([ctypes.c_int], ctypes.c_int),
+        "rq_launch_time": ([ctypes.POINTER(ctypes.c_double), u32p, ctypes.c_int], ctypes.c_int),
+        "rq_debug_pair_emulate": ([ctypes.c_uint32, ctypes.c_uint32, u32p, ctypes.c_uint32, vp, vp, u32p, u32p,
+                                   ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+        "rq_debug_decode_plan": ([ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, u32p, u32p, u32p, u32p, ctypes.c_uint32,
+                                  ctypes.POINTER(ctypes.c_double), u32p], ctypes.c_int),
+        "rq_debug_dma4_emulate": ([ctypes.c_uint32, ctypes.c_uint32, u32p, ctypes.c_uint32, vp, vp, ctypes.c_uint32,
+                                   ctypes.c_uint32, u32p, ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+        "rq_debug_assemble": ([ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+        "rq_debug_cache_roundtrip": ([ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32], ctypes.c_int),
+        "rq_debug_colprog_bound": ([ctypes.c_uint32, ctypes.c_uint32, u32p, ctypes.c_uint32, vp, vp, ctypes.c_uint64,
+                                    u32p], ctypes.c_int),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    return L
 
 
 def launch_timing(enable):
@@ -207,9 +233,10 @@ def launch_time(reset=True):
     return ms.value, n.value
 
 
-def _check(rc):
+def _check(rc, L=None):
     if rc != RQ_OK:
-        detail = lib().rq_last_error().decode() or lib().rq_strerror(rc).decode()
+        L = L or lib()
+        detail = L.rq_last_error().decode() or L.rq_strerror(rc).decode()
         raise RaptorQError(rc, detail)
     return rc
 
@@ -288,9 +315,11 @@ PAIR_STATS = ("a_ins", "a_valu", "a_loads", "a_agpr_moves", "a_ring_stores", "a_
               "b_ring_loads", "b_stores", "ring", "transfers", "handed", "lds_bytes", "a_dma4", "sched_4r")
 
 
-def pair_emulate(K, T, esis, src=None, cfg=(0, 0, 0, 0, 0), assemble=False):
+def pair_emulate(K, T, esis, src=None, cfg=(0, 0, 0, 0, 0), assemble=False, L=None):
     """rq_debug_pair_emulate: the two-wave split of the (K, esis) program, run on the host over two items
-    of one block (src: K*T bytes, or None for statistics only).  Returns (outputs or None, stats dict)."""
+    of one block (src: K*T bytes, or None for statistics only).  Returns (outputs or None, stats dict).
+    The pair programs live in the experiments library (L defaults to exp_lib())."""
+    L = L or exp_lib()
     import numpy as np
     e = np.asarray(esis, np.uint32)
     c = np.asarray(tuple(cfg) + (0,) * (5 - len(cfg)), np.uint32)
@@ -303,7 +332,7 @@ def pair_emulate(K, T, esis, src=None, cfg=(0, 0, 0, 0, 0), assemble=False):
         sp, op = s.ctypes.data, out.ctypes.data
     n = ctypes.c_size_t(0)
     P = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
-    _check(lib().rq_debug_pair_emulate(K, T, P(e), len(e), sp, op, P(c), P(st), ctypes.byref(n) if assemble else None))
+    _check(L.rq_debug_pair_emulate(K, T, P(e), len(e), sp, op, P(c), P(st), ctypes.byref(n) if assemble else None), L)
     d = dict(zip(PAIR_STATS, (int(x) for x in st)))
     d["code_bytes"] = n.value
     return (out.reshape(len(esis), T) if out is not None else None), d
@@ -312,9 +341,11 @@ def pair_emulate(K, T, esis, src=None, cfg=(0, 0, 0, 0, 0), assemble=False):
 DMA4_STATS = ("ins", "valu", "dma4", "scratch_slots", "tbl_slots", "lds_slots", "ins_plain", "sched_4r")
 
 
-def dma4_emulate(K, T, esis, src=None, quads=8, la=0, assemble=False):
+def dma4_emulate(K, T, esis, src=None, quads=8, la=0, assemble=False, L=None):
     """rq_debug_dma4_emulate: the single-wave program with four-row staging, run on the host over one
-    item (src: K*T bytes, or None for statistics only).  Returns (outputs or None, stats dict)."""
+    item (src: K*T bytes, or None for statistics only).  Returns (outputs or None, stats dict).
+    Four-row staging lives in the experiments library (L defaults to exp_lib())."""
+    L = L or exp_lib()
     import numpy as np
     e = np.asarray(esis, np.uint32)
     st = np.zeros(8, np.uint32)
@@ -326,7 +357,7 @@ def dma4_emulate(K, T, esis, src=None, quads=8, la=0, assemble=False):
         sp, op = s.ctypes.data, out.ctypes.data
     n = ctypes.c_size_t(0)
     P = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
-    _check(lib().rq_debug_dma4_emulate(K, T, P(e), len(e), sp, op, quads, la, P(st), ctypes.byref(n) if assemble else None))
+    _check(L.rq_debug_dma4_emulate(K, T, P(e), len(e), sp, op, quads, la, P(st), ctypes.byref(n) if assemble else None), L)
     d = dict(zip(DMA4_STATS, (int(x) for x in st)))
     d["code_bytes"] = n.value
     return (out.reshape(len(esis), T) if out is not None else None), d

@@ -98,3 +98,12 @@ def test_source_bound_reads_zero():
     none, _ = rqhip.colprog_bound(K, T, ESIS, src, 0)
     zero_src, _ = rqhip.colprog_bound(K, T, ESIS, np.zeros_like(src), 1 << 62)
     assert np.array_equal(none, zero_src)
+
+
+@pytest.mark.parametrize("n_rows,n_dma4", [(1024, 0), (1024, 1040), (0, 0)])
+def test_program_cache_entry_round_trip(tmp_path, n_rows, n_dma4):
+    """The on-disk program cache keeps both row lists: cache_load reads the n_rows source-load rows and
+    the n_dma4 four-row staging rows that cache_store writes, and its body hash covers both (ADVICE r4:
+    the loader used to read n_rows only, so a staged entry never matched)."""
+    p = str(tmp_path / "entry.co").encode()
+    rqhip._check(rqhip.lib().rq_debug_cache_roundtrip(p, n_rows, n_dma4))
