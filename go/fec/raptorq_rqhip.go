@@ -33,6 +33,9 @@ var (
 	errBadKL    = errors.New("bad K or L")
 	errBadSizeL = errors.New("bad dataSize or L")
 	errBadNKL   = errors.New("bad N/K/L")
+	// batch-path argument errors (this shim's own API, not the reference's)
+	errBadBatch = errors.New("decode blocks: data, repair, erased and repairESI differ in length")
+	errShortBuf = errors.New("decode blocks: a block's data or repair slice is shorter than its symbols")
 )
 
 type RaptorQEncoder struct {
@@ -239,6 +242,19 @@ func DecodeBlocks(K, L int, data [][]byte, repair [][]byte, erased, repairESI []
 	n := len(data)
 	if n == 0 {
 		return nil, nil
+	}
+	if K <= 0 || L <= 0 {
+		return nil, errBadKL
+	}
+	// the library reads K*L bytes of data[b] and len(repairESI[b])*L of repair[b] and writes the
+	// recovered rows into data[b]: check every length before a pointer is taken
+	if len(repair) != n || len(erased) != n || len(repairESI) != n {
+		return nil, errBadBatch
+	}
+	for b := 0; b < n; b++ {
+		if len(data[b]) < K*L || len(repair[b]) < len(repairESI[b])*L {
+			return nil, errShortBuf
+		}
 	}
 	ioBytes := C.size_t(n) * C.size_t(unsafe.Sizeof(C.rq_block_io{}))
 	ioMem := C.malloc(ioBytes)
