@@ -99,8 +99,11 @@ struct Allocator {
         retire_to(seq - n);
     }
     uint64_t issue_vmem() {  // call before emitting a VMEM instruction; returns its seq
-        if (seq - retired >= o.max_vmem) {
-            const uint64_t n = o.max_vmem - 1;
+        if (seq - retired >= o.max_vmem) {  // full: also retire what was issued wait_age instructions ago
+            const size_t now = mp->ins.size();
+            uint64_t s = retired + 1;
+            while (s < seq && vm_ins[s + 1] + o.wait_age <= now) ++s;
+            const uint64_t n = std::min<uint64_t>(seq - s, o.max_vmem - 1);
             emit(MI_WAIT, -1, -1, -1, -1, (uint32_t)n);
             mp->st.wait++;
             retire_to(seq - n);
@@ -128,10 +131,16 @@ struct Allocator {
         retire_l(lseq - n);
     }
     uint64_t issue_lgkm() {
+        // full (15 outstanding): retire everything issued lwait_age instructions ago or more at once, so
+        // the next LDS operations do not each need a wait of their own (-106 waits per item at K=1024)
         if (lseq - lretired >= 15) {
-            emit(MI_WAITL, -1, -1, -1, -1, 14);
+            const size_t now = mp->ins.size();
+            uint64_t s = lretired + 1;
+            while (s < lseq && l_ins[s + 1] + o.lwait_age <= now) ++s;
+            const uint64_t n = std::min<uint64_t>(lseq - s, 14);
+            emit(MI_WAITL, -1, -1, -1, -1, (uint32_t)n);
             mp->st.waitl++;
-            retire_l(lseq - 14);
+            retire_l(lseq - n);
         }
         l_ins.push_back(mp->ins.size());
         return ++lseq;
