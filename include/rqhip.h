@@ -240,6 +240,15 @@ int rq_debug_dma4_emulate(uint32_t K, uint32_t T, const uint32_t* esi, uint32_t 
  * and re-solve on all of them only if that subset is rank-deficient.  Sets the margin (tests force
  * the second pass with 0) and returns the previous one.  Results never depend on it. */
 uint32_t rq_debug_decode_margin(uint32_t margin);
+/* The decode's apply step: 1 (default) = the register-table kernel (k_xbits + the generated
+ * rq_apply_gi kernel, rq_applygi.cpp), 0 = k_apply's v_perm byte tables.  Sets the mode (values > 1
+ * leave it) and returns the previous one; both give the same bytes. */
+uint32_t rq_debug_apply_mode(uint32_t mode);
+/* The register-table apply kernel's assembly for shape (KC outputs per wave, groups of G syndromes,
+ * loads PDG groups ahead): copied into text (cap bytes, NUL-terminated) when given, its length in
+ * *text_len, and, when code_bytes is given, assembled in process (its code object size). */
+int rq_debug_apply_gi_asm(uint32_t kc, uint32_t g, uint32_t pdg, char* text, size_t cap, size_t* text_len,
+                          size_t* code_bytes);
 /* The engine's LT tuple of ISI X at library K (rq_core.hpp tuple_of; RQ/params.go:83-112):
  * out = {d, a, b, d1, a1, b1}. */
 int rq_debug_tuple(uint32_t K, uint32_t X, uint32_t out[6]);

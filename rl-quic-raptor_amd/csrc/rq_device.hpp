@@ -94,7 +94,78 @@ struct ApplyArgs {
     uint32_t out_sc1 = 0;       // 1: recovered rows stored sc1 (written through, not left dirty in L2)
 };
 
+// The register-table apply (rq_applygi.cpp): x_E = g_E ^ X s as 8 GF(2) bit planes.  Shape: KC outputs
+// per wave (8 or 16), syndromes in groups of G (4..6) whose 2^G subset XORs form a table in VGPRs,
+// syndrome loads PDG groups ahead (1..2).
+struct GiShape {
+    uint32_t KC = 8, G = 5, PDG = 2;
+    uint32_t diag = 0;  // experiments (timing only, wrong bytes): 1 no index loads, 2 no syndrome loads, 4 no lookups
+};
+
+// Per block bi of the solve list, the dword stream k_xbits writes at gi + bi * block and the apply kernel
+// reads with scalar loads.  The layout is fixed by the batch's largest e (every address follows from
+// (bi, slice) and the kernel arguments, so a wave needs one round of scalar loads before its first
+// syndrome load); for the block's own e: ngr = ceil(e / G) groups, nsl = ceil(e / KC) slices.
+//   header (16 dwords): status (1 = solved), e, ngr, 0, then the 64-bit base addresses of the block's
+//            received repair rows, r0 rows and data rows
+//   er:      nslm records of 16 dwords: slice s's output row byte offsets (E[s KC + k] * T, 0 past e)
+//   of:      ngrm + PDG + 1 records of 16 dwords; record q: (received row, r0 row) byte offsets of
+//            syndrome m = G q + t at dwords 2t, 2t + 1 (0 past e: row 0, loaded and never looked up)
+//   ix:      per slice ngrm records of 8 KC dwords: record g, output k, bit b = the G-bit subset of group
+//            g's syndromes whose coefficients in X[s KC + k] have bit b set
+struct GiLayout {
+    uint32_t nslm, ngrm;        // slices / groups of the batch's largest e
+    uint32_t er, of, ix, ix_slice, block;  // dwords
+};
+__host__ __device__ inline GiLayout gi_layout(uint32_t max_e, const GiShape& s) {
+    GiLayout L;
+    L.nslm = (max_e + s.KC - 1) / s.KC;
+    L.ngrm = (max_e + s.G - 1) / s.G;
+    L.er = 16;
+    L.of = L.er + 16 * L.nslm;
+    L.ix = L.of + 16 * (L.ngrm + s.PDG + 1);
+    L.ix_slice = 8 * s.KC * L.ngrm;
+    L.block = L.ix + L.nslm * L.ix_slice;
+    return L;
+}
+
+struct XbitsArgs {
+    const uint32_t* blk_map;
+    const int32_t* status;
+    const uint32_t* erased_off;
+    const uint32_t* erased;
+    const uint32_t* rep_off;
+    const uint32_t* rep_uidx;
+    const uint8_t* xcoef;
+    const uint32_t* xoff;
+    const uint16_t* xpiv;
+    const uint8_t* recv;
+    const uint8_t* r0;
+    uint8_t* data;
+    uint64_t data_stride;
+    uint32_t* gi;
+    GiLayout L;
+    uint32_t T, n_union;
+};
+
+// Kernel arguments of the generated apply kernel; its prologue loads them at these byte offsets.
+struct ApplyGiArgs {
+    const uint32_t* gi;         // 0
+    uint32_t block_bytes;       // 8: 4 * GiLayout::block
+    uint32_t of_bytes;          // 12
+    uint32_t ix_bytes;          // 16
+    uint32_t ix_slice_bytes;    // 20
+    uint32_t n_blocks;          // 24: entries of the solve list
+    uint32_t T;                 // 28
+    uint32_t strips;            // 32: ceil(T / 256)
+    uint32_t nsg;               // 36: strip groups of ws waves (one workgroup each)
+    uint32_t sg_magic;          // 40: ceil(2^31 / nsg) (y / nsg = (2y * magic) >> 32)
+    uint32_t ws;                // 44: waves per workgroup
+};
+static_assert(sizeof(ApplyGiArgs) == 48, "apply kernel argument layout");
+
 // Launchers (rq_kernels.hip).  Return hipError_t as int.
+int launch_xbits(const XbitsArgs& a, uint32_t n_blocks, const GiShape& s, void* stream);
 // Host-memory decode: copy the recovered rows (the same (blk, row) list) into a dense buffer so only
 // e*T bytes per block travel back over PCIe.
 int launch_pack_rows(const PackArgs& a, void* stream);

@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "../../include/rqhip.h"
+#include "rq_applygi.hpp"
 #include "rq_colasm.hpp"
 #include "rq_colprog.hpp"
 #include "rq_device.hpp"
@@ -134,6 +135,7 @@ unsigned internal_event_flags() {
 
 struct Workspace {
     DevBuf r0, xb, xp, gws, scratch;
+    DevBuf gi;                      // the register-table apply's index stream (k_xbits)
     DevBuf pk;                      // host-memory decode: recovered rows, packed for the D2H
     HostBuf h_status, h_pack;
     // decode descriptors, double-buffered so that rq_decode_batch_async can return before its upload
@@ -220,6 +222,10 @@ struct DevCtx {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> tev;
     size_t tev_used = 0;
     hipStream_t obj_stream = nullptr;  // per-object API: its own stream, pinned staging, device buffer
+    // the register-table apply kernel (rq_applygi.cpp), assembled on first use for `gi_shape`
+    hipModule_t gi_mod = nullptr;
+    hipFunction_t gi_fn = nullptr;
+    GiShape gi_shape;
     HostBuf obj_h;
     DevBuf obj_d;
     // Per-stream workspaces are bounded: a caller that uses a fresh stream per window would otherwise
@@ -270,6 +276,7 @@ struct DevCtx {
         ws.clear();
         dead.clear();
         colk.clear();
+        if (gi_mod) (void)hipModuleUnload(gi_mod);
         for (Stage& st : stage)
             if (st.s) (void)hipStreamDestroy(st.s);
         for (hipEvent_t e : kdone)
@@ -1136,6 +1143,54 @@ bool solve_beside() {
     return on;
 }
 
+// The decode's apply: 1 = the register-table kernel (rq_applygi.cpp, k_xbits + the generated kernel),
+// 0 = k_apply's v_perm byte tables.  rq_debug_apply_mode switches it (tests compare the two).
+uint32_t g_apply_mode = 1;
+
+// The register-table apply's shape: KC = 8 outputs per wave, groups of G = 5 syndromes, loads two groups
+// ahead (124 VGPRs: four waves per SIMD); RQHIP_APPLY_GI="KC,G,PDG" in experiments builds.
+const GiShape& apply_gi_shape() {
+    static const GiShape sh = [] {
+        GiShape g;
+        if (const char* e = knob("RQHIP_APPLY_GI")) {
+            unsigned kc = 0, gg = 0, pd = 0;
+            if (std::sscanf(e, "%u,%u,%u", &kc, &gg, &pd) == 3) {
+                GiShape t;
+                t.KC = kc; t.G = gg; t.PDG = pd;
+                if (gi_shape_ok(t)) g = t;
+            }
+        }
+        if (const char* d = knob("RQHIP_APPLY_DIAG")) g.diag = (uint32_t)std::atoi(d);
+        return g;
+    }();
+    return sh;
+}
+
+// The apply kernel of this device, assembled (amd_comgr, in process) on first use.  Caller holds ctx->mu.
+int get_gi_kernel(DevCtx* ctx, const GiShape& sh, hipFunction_t* fn) {
+    if (ctx->gi_fn && ctx->gi_shape.KC == sh.KC && ctx->gi_shape.G == sh.G && ctx->gi_shape.PDG == sh.PDG &&
+        ctx->gi_shape.diag == sh.diag) {
+        *fn = ctx->gi_fn;
+        return RQ_OK;
+    }
+    std::vector<char> co;
+    std::string err;
+    if (!comgr_assemble(emit_apply_gi_asm(sh), &co, &err)) return fail(RQ_ERR_PLAN, err);
+    hipModule_t mod = nullptr;
+    hipFunction_t f = nullptr;
+    if (hipModuleLoadData(&mod, co.data()) != hipSuccess ||
+        hipModuleGetFunction(&f, mod, gi_kernel_name(sh).c_str()) != hipSuccess) {
+        if (mod) (void)hipModuleUnload(mod);
+        return fail(RQ_ERR_DEVICE, "apply kernel load failed");
+    }
+    if (ctx->gi_mod) (void)hipModuleUnload(ctx->gi_mod);  // a shape change (experiments): idle by then
+    ctx->gi_mod = mod;
+    ctx->gi_fn = f;
+    ctx->gi_shape = sh;
+    *fn = f;
+    return RQ_OK;
+}
+
 int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, void* data, uint64_t data_stride,
                 const std::vector<uint32_t>& eoff, const uint32_t* erased, const std::vector<uint32_t>& roff,
                 const uint32_t* repair_esi, const std::vector<uint32_t>& cnt, const std::vector<uint32_t>& blk_map,
@@ -1143,7 +1198,11 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     int rc;
     const bool async = fin == Fin::Async;
     DecodePlan& pl = decode_plan_scratch();
+    const bool gi = g_apply_mode == 1;
+    const GiShape& gsh = apply_gi_shape();
     if ((rc = plan_decode(p, n_blocks, eoff, roff, repair_esi, cnt, blk_map, po != nullptr, &pl, mx_hint))) return rc;
+    hipFunction_t gi_fn = nullptr;
+    if (gi && (rc = get_gi_kernel(ctx, gsh, &gi_fn))) return rc;
     const uint32_t nw = pl.nw, max_e = pl.max_e, max_lds_e = pl.max_lds_e;
     const bool need_general = pl.need_general, wide = pl.wide;
     const uint64_t xo = pl.xo, go = pl.go;
@@ -1245,6 +1304,10 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     if ((rc = w->xb.ensure((size_t)xo * 64))) return rc;
     if ((rc = w->xp.ensure(std::max<size_t>(n_er, 1) * 2))) return rc;
     if (go && (rc = w->gws.ensure((size_t)go * 64))) return rc;
+    // the apply's stream (fixed layout by the largest e) + slack: a slice's last group prefetches one
+    // index pair past its records
+    const GiLayout gl = gi_layout(max_e, gsh);
+    if (gi && (rc = w->gi.ensure((size_t)nw * gl.block * 4 + 4096))) return rc;
     // The solve reads only the descriptors and M (the program's repair-coefficient matrix), not the
     // syndromes: it can run on the side stream beside the syndrome program, which leaves SIMDs and
     // LDS free (960 one-wave workgroups on 1 024 SIMDs at K=1024).  The side stream first waits for
@@ -1333,7 +1396,46 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     // kernel boundary after the apply has no dirty lines to write back)
     static const uint32_t apply_sc1 = [] { const char* e = knob("RQHIP_APPLY_SC1"); return e && e[0] == '1' ? 1u : 0u; }();
     ap.out_sc1 = apply_sc1;
-    if (launch_apply(ap, (T / 4 + 63) / 64, nw, stream)) return fail(RQ_ERR_DEVICE, "k_apply launch failed");
+    if (gi && nw && max_e) {
+        XbitsArgs xa;
+        xa.blk_map = ap.blk_map;
+        xa.status = ap.status;
+        xa.erased_off = ap.erased_off;
+        xa.erased = ap.erased;
+        xa.rep_off = ap.rep_off;
+        xa.rep_uidx = ap.rep_uidx;
+        xa.xcoef = ap.xcoef;
+        xa.xoff = ap.xoff;
+        xa.xpiv = ap.xpiv;
+        xa.recv = ap.recv;
+        xa.r0 = ap.r0;
+        xa.data = ap.data;
+        xa.data_stride = data_stride;
+        xa.gi = w->gi.as<uint32_t>();
+        xa.L = gl;
+        xa.T = T;
+        xa.n_union = ap.n_union;
+        if (launch_xbits(xa, nw, gsh, stream)) return fail(RQ_ERR_DEVICE, "k_xbits launch failed");
+        ApplyGiArgs ga{};
+        ga.gi = xa.gi;
+        ga.block_bytes = gl.block * 4;
+        ga.of_bytes = gl.of * 4;
+        ga.ix_bytes = gl.ix * 4;
+        ga.ix_slice_bytes = gl.ix_slice * 4;
+        ga.n_blocks = nw;
+        ga.T = T;
+        ga.strips = (T / 4 + 63) / 64;
+        // one wave per workgroup: the strips of a (block, slice) as one workgroup (sharing the CU's scalar
+        // cache, RQHIP_APPLY_WS=8 in experiments builds) measured 152 against 112 us
+        static const uint32_t ws_cap = [] { const char* e = knob("RQHIP_APPLY_WS"); return e ? (uint32_t)std::max(1, std::atoi(e)) : 1u; }();
+        ga.ws = std::min<uint32_t>(ga.strips, std::min<uint32_t>(ws_cap, 8));
+        ga.nsg = (ga.strips + ga.ws - 1) / ga.ws;
+        ga.sg_magic = (uint32_t)((0x80000000ull + ga.nsg - 1) / ga.nsg);
+        size_t asz = sizeof ga;
+        void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &ga, HIP_LAUNCH_PARAM_BUFFER_SIZE, &asz, HIP_LAUNCH_PARAM_END};
+        HIP_TRY(hipModuleLaunchKernel(gi_fn, 8, gl.nslm * ga.nsg, (nw + 7) / 8, 64 * ga.ws, 1, 1, 0, (hipStream_t)stream,
+                                      nullptr, cfg));
+    } else if (launch_apply(ap, (T / 4 + 63) / 64, nw, stream)) return fail(RQ_ERR_DEVICE, "k_apply launch failed");
     const size_t pack_bytes = (size_t)nz * T;
     if (po) {
         if ((rc = w->pk.ensure(pack_bytes)) || (rc = w->h_pack.ensure(pack_bytes))) return rc;
@@ -2213,6 +2315,33 @@ int rq_debug_shard_plan(uint32_t device_mask, int n_devices, uint32_t n_blocks, 
 uint32_t rq_debug_virtual_shards(uint32_t n) {
     const uint32_t old = g_virtual_shards;
     g_virtual_shards = n;
+    return old;
+}
+
+int rq_debug_apply_gi_asm(uint32_t kc, uint32_t g, uint32_t pdg, char* text, size_t cap, size_t* text_len,
+                          size_t* code_bytes) {
+    GiShape sh;
+    sh.KC = kc; sh.G = g; sh.PDG = pdg;
+    if (!gi_shape_ok(sh)) return fail(RQ_ERR_BAD_ARG, "apply shape: KC 8 or 16, G 4..6, PDG 1..3");
+    const std::string src = emit_apply_gi_asm(sh);
+    if (text_len) *text_len = src.size();
+    if (text && cap) {
+        const size_t n = std::min(cap - 1, src.size());
+        std::memcpy(text, src.data(), n);
+        text[n] = 0;
+    }
+    if (code_bytes) {
+        std::vector<char> co;
+        std::string err;
+        if (!comgr_assemble(src, &co, &err)) return fail(RQ_ERR_PLAN, err);
+        *code_bytes = co.size();
+    }
+    return RQ_OK;
+}
+
+uint32_t rq_debug_apply_mode(uint32_t mode) {
+    const uint32_t old = g_apply_mode;
+    if (mode <= 1) g_apply_mode = mode;
     return old;
 }
 

@@ -88,6 +88,91 @@ int launch_pack_rows(const PackArgs& a, void* stream) {
     return (int)hipGetLastError();
 }
 
+// ------------------------------ decode: X -> the register-table apply's stream ---------------
+// One workgroup per block of the solve list: X (bytes, row m = syndrome in pivot order, byte k =
+// output) becomes the dword stream of rq_device.hpp GiLayout: a header (status, e, the block's row
+// bases), per slice of KC outputs their row offsets, per group of G syndromes their row offsets, and per
+// slice, group and output the eight G-bit subsets idx_b = sum_t bit_b(X[k][G g + t]) << t, so that
+// sum_m X[k][m] s_m = sum_b alpha^b sum_g Tab_g[idx_b], where Tab_g holds the 2^G XORs of group g's
+// syndromes (the apply kernel, rq_applygi.cpp).  Unsolved blocks get a header with status 0 only.
+template <int KC, int G, int PDG>
+__global__ void __launch_bounds__(256) k_xbits(XbitsArgs a) {
+    const uint32_t bi = blockIdx.x, tid = threadIdx.x;
+    const uint32_t b = a.blk_map[bi];
+    const GiLayout& L = a.L;
+    uint32_t* base = a.gi + (size_t)bi * L.block;
+    const bool solved = a.status[b] == 1;
+    const uint32_t e = a.erased_off[b + 1] - a.erased_off[b];
+    const uint32_t ngr = (e + G - 1) / G, nsl = (e + KC - 1) / KC;
+    if (tid < 16) {
+        uint64_t v = 0;
+        if (tid >= 4 && tid < 10) {
+            const uint32_t w = (tid - 4) >> 1;
+            const uint64_t addr = w == 0 ? (uint64_t)(a.recv + (size_t)a.rep_off[b] * a.T)
+                                : w == 1 ? (uint64_t)(a.r0 + (size_t)b * a.n_union * a.T)
+                                         : (uint64_t)(a.data + (size_t)b * a.data_stride);
+            v = (tid & 1) ? addr >> 32 : addr & 0xFFFFFFFFu;
+        }
+        base[tid] = tid == 0 ? (uint32_t)solved : tid == 1 ? e : tid == 2 ? ngr : (uint32_t)v;
+    }
+    if (!solved) return;
+    const uint32_t* E = a.erased + a.erased_off[b];
+    const uint16_t* XP = a.xpiv + a.erased_off[b];
+    const uint32_t* RU = a.rep_uidx + a.rep_off[b];
+    const uint8_t* xc = a.xcoef + 64ull * a.xoff[bi];
+    const uint32_t xs = x_stride(e), T = a.T;
+    for (uint32_t i = tid; i < nsl * 16; i += 256) {
+        const uint32_t sl = i >> 4, k = i & 15, ko = sl * KC + k;
+        base[L.er + i] = (k < (uint32_t)KC && ko < e) ? E[ko] * T : 0u;
+    }
+    for (uint32_t i = tid; i < (ngr + PDG + 1) * 16; i += 256) {
+        const uint32_t q = i >> 4, w = i & 15, t = w >> 1, m = G * q + t;
+        uint32_t v = 0;
+        if (t < (uint32_t)G && m < e) {
+            const uint32_t j = XP[m];
+            v = (w & 1) ? RU[j] * T : j * T;
+        }
+        base[L.of + i] = v;
+    }
+    for (uint32_t i = tid; i < nsl * ngr * KC; i += 256) {
+        const uint32_t k = i % KC, r = i / KC, g = r % ngr, sl = r / ngr, ko = sl * KC + k;
+        uint32_t x[G];
+#pragma unroll
+        for (int t = 0; t < G; ++t) {
+            const uint32_t m = G * g + t;
+            x[t] = (ko < e && m < e) ? xc[(size_t)m * xs + ko] : 0u;
+        }
+        uint32_t v[8];
+#pragma unroll
+        for (int bit = 0; bit < 8; ++bit) {
+            uint32_t s = 0;
+#pragma unroll
+            for (int t = 0; t < G; ++t) s |= ((x[t] >> bit) & 1u) << t;
+            v[bit] = s;
+        }
+        uint4* d = reinterpret_cast<uint4*>(base + L.ix + sl * L.ix_slice + g * 8 * KC + k * 8);
+        d[0] = make_uint4(v[0], v[1], v[2], v[3]);
+        d[1] = make_uint4(v[4], v[5], v[6], v[7]);
+    }
+}
+
+int launch_xbits(const XbitsArgs& a, uint32_t n_blocks, const GiShape& s, void* stream) {
+    if (!n_blocks) return 0;
+    const hipStream_t st = (hipStream_t)stream;
+#define RQ_XB(kc, g, p)                                                                                   \
+    if (s.KC == kc && s.G == g && s.PDG == p) {                                                           \
+        hipLaunchKernelGGL((k_xbits<kc, g, p>), dim3(n_blocks), dim3(256), 0, st, a);                     \
+        return (int)hipGetLastError();                                                                    \
+    }
+    RQ_XB(8, 5, 2)
+#ifdef RQHIP_EXPERIMENTS
+    RQ_XB(16, 6, 1) RQ_XB(16, 6, 2) RQ_XB(16, 5, 2) RQ_XB(8, 6, 2) RQ_XB(8, 5, 1) RQ_XB(8, 4, 1) RQ_XB(16, 4, 2)
+    RQ_XB(8, 4, 2) RQ_XB(8, 6, 1)
+#endif
+#undef RQ_XB
+    return (int)hipErrorInvalidValue;
+}
+
 // ------------------------------ decode: per-block GF(256) solve ------------------------------
 // M[j][k] = mrep[uidx_j][e_k] (received repair j, erased source e_k); Gauss-Jordan on [M | I]
 // (replaces GaussianElimination, RQ/discmath/gauss.go:7-45, on the e erased columns only):

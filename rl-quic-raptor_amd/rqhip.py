@@ -44,6 +44,7 @@ EXPORTED = (
     "rq_decoder_create", "rq_decoder_k", "rq_decoder_add", "rq_decoder_decode", "rq_decoder_free",
     "rq_encode_batch", "rq_decode_batch", "rq_decode_batch_async", "rq_encode_batch_host", "rq_decode_batch_host", "rq_device_count", "rq_set_device",
     "rq_debug_colprog_eval", "rq_debug_colprog_emulate", "rq_debug_colprog_assemble", "rq_debug_decode_margin",
+    "rq_debug_apply_mode", "rq_debug_apply_gi_asm",
     "rq_decode_blocks_host", "rq_host_alloc", "rq_host_free", "rq_debug_colprog_passes",
     "rq_debug_shard_plan", "rq_debug_virtual_shards", "rq_debug_tuple", "rq_stream_release", "rq_shutdown",
     "rq_launch_timing", "rq_launch_time", "rq_debug_pair_emulate", "rq_debug_dma4_emulate", "rq_debug_decode_plan",
@@ -188,6 +189,9 @@ def _load(path):
         "rq_debug_colprog_assemble": ([ctypes.c_uint32, u32p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_size_t)],
                                       ctypes.c_int),
         "rq_debug_decode_margin": ([ctypes.c_uint32], ctypes.c_uint32),
+        "rq_debug_apply_mode": ([ctypes.c_uint32], ctypes.c_uint32),
+        "rq_debug_apply_gi_asm": ([ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t,
+                                   ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
         "rq_decode_blocks_host": ([ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(BlockIO), ctypes.c_uint32,
                                    ctypes.c_uint32], ctypes.c_int),
         "rq_host_alloc": ([ctypes.c_size_t], vp),
@@ -380,6 +384,21 @@ def assemble(text):
     n = ctypes.c_size_t(0)
     _check(lib().rq_debug_assemble(b, len(b), ctypes.byref(n)))
     return n.value
+
+
+def apply_gi_asm(kc=16, g=6, pdg=2, assemble=True):
+    """rq_debug_apply_gi_asm: (assembly text, code object size or None) of the register-table apply kernel."""
+    n = ctypes.c_size_t(0)
+    _check(lib().rq_debug_apply_gi_asm(kc, g, pdg, None, 0, ctypes.byref(n), None))
+    buf = ctypes.create_string_buffer(n.value + 1)
+    co = ctypes.c_size_t(0)
+    _check(lib().rq_debug_apply_gi_asm(kc, g, pdg, buf, n.value + 1, None, ctypes.byref(co) if assemble else None))
+    return buf.value.decode(), (co.value if assemble else None)
+
+
+def apply_mode(mode):
+    """rq_debug_apply_mode: 1 = register-table apply, 0 = v_perm k_apply; returns the previous mode."""
+    return lib().rq_debug_apply_mode(mode)
 
 
 def colprog_bound(K, T, esis, src, src_bytes):
