@@ -245,9 +245,9 @@ uint32_t rq_debug_decode_margin(uint32_t margin);
  * leave it) and returns the previous one; both give the same bytes. */
 uint32_t rq_debug_apply_mode(uint32_t mode);
 /* The register-table apply kernel's assembly for shape (KC outputs per wave, groups of G syndromes,
- * loads PDG groups ahead): copied into text (cap bytes, NUL-terminated) when given, its length in
+ * loads PDG groups ahead, CPL dword columns per lane): copied into text (cap bytes, NUL-terminated) when given, its length in
  * *text_len, and, when code_bytes is given, assembled in process (its code object size). */
-int rq_debug_apply_gi_asm(uint32_t kc, uint32_t g, uint32_t pdg, char* text, size_t cap, size_t* text_len,
+int rq_debug_apply_gi_asm(uint32_t kc, uint32_t g, uint32_t pdg, uint32_t cpl, char* text, size_t cap, size_t* text_len,
                           size_t* code_bytes);
 /* The engine's LT tuple of ISI X at library K (rq_core.hpp tuple_of; RQ/params.go:83-112):
  * out = {d, a, b, d1, a1, b1}. */

@@ -22,6 +22,8 @@
 #include <algorithm>
 #include <cstdio>
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "rq_applygi.hpp"
 
@@ -41,34 +43,43 @@ struct Asm {
 }  // namespace
 
 bool gi_shape_ok(const GiShape& sh) {
-    return (sh.KC == 8 || sh.KC == 16) && sh.G >= 4 && sh.G <= 6 && sh.PDG >= 1 && sh.PDG <= 2;
+    return sh.KC >= 4 && sh.KC <= 16 && sh.KC % 4 == 0 && sh.G >= 4 && sh.G <= 6 && sh.PDG >= 1 && sh.PDG <= 2 &&
+           sh.CPL >= 1 && sh.CPL <= 2 && gi_vgprs(sh) <= 256;
 }
 
-// VGPRs: v0 lane, v1 the lane's byte offset in a row, v2..v7 Horner temporaries, the syndrome ring
-// (PDG slots of G received-row + G r0-row values) from v8, the table (2^G entries, entry 0 = 0), then
-// the KC x 8 bit planes (plane 0 starts as g_E).
-uint32_t gi_vgprs(const GiShape& sh) {
-    const uint32_t tb = (8 + 2 * sh.G * sh.PDG + 3) & ~3u;
-    return tb + (1u << sh.G) + 8 * sh.KC;
-}
+// VGPRs: v0 lane (prologue only), v1 the lane's byte offset in a row (column c at + 256 c), the syndrome
+// ring from v2 (per column, PDG slots of G received-row + G r0-row values; v2..v7 double as Horner
+// temporaries at the end), per column a table of 2^G entries (entry 0 = 0), then per column the KC x 8
+// bit planes (plane 0 starts as g_E).
+namespace {
+uint32_t gi_tb(const GiShape& sh) { return (2 + 2 * sh.G * sh.PDG * sh.CPL + 3) & ~3u; }
+}  // namespace
+
+uint32_t gi_vgprs(const GiShape& sh) { return gi_tb(sh) + sh.CPL * ((1u << sh.G) + 8 * sh.KC); }
 
 std::string gi_kernel_name(const GiShape& sh) {
     return "rq_apply_gi_k" + std::to_string(sh.KC) + "_g" + std::to_string(sh.G) + "_p" + std::to_string(sh.PDG) +
-           (sh.diag ? "_d" + std::to_string(sh.diag) : std::string());
+           "_c" + std::to_string(sh.CPL) + (sh.diag ? "_d" + std::to_string(sh.diag) : std::string());
 }
 
 std::string emit_apply_gi_asm(const GiShape& sh) {
-    const uint32_t KC = sh.KC, G = sh.G, PDG = sh.PDG, NT = 1u << G;
-    const uint32_t RING = 8, TB = (8 + 2 * G * PDG + 3) & ~3u, AC = TB + NT, NV = AC + 8 * KC;
-    const uint32_t PAIRS = KC / 4;  // 32 index dwords per pair of 16-dword pieces, 8 per output
+    const uint32_t KC = sh.KC, G = sh.G, PDG = sh.PDG, CPL = sh.CPL, NT = 1u << G;
+    const uint32_t RING = 2, TB = gi_tb(sh), AC = TB + CPL * NT, NV = gi_vgprs(sh);
+    const uint32_t PAIRS = KC / 4;                       // 32 index dwords per pair of 16-dword pieces
+    const uint32_t UNR = (PDG * PAIRS) % 2 ? 2 * PDG : PDG;  // groups per loop body: ring slots, and pieces A/B alternate
     const std::string kname = gi_kernel_name(sh);
-    auto RA = [&](uint32_t p, uint32_t t) { return RING + p * 2 * G + t; };
-    auto RB = [&](uint32_t p, uint32_t t) { return RING + p * 2 * G + G + t; };
-    auto ACC = [&](uint32_t k, uint32_t b) { return AC + 8 * k + b; };
+    auto RA = [&](uint32_t c, uint32_t p, uint32_t t) { return RING + (c * PDG + p) * 2 * G + t; };
+    auto RB = [&](uint32_t c, uint32_t p, uint32_t t) { return RING + (c * PDG + p) * 2 * G + G + t; };
+    auto TBC = [&](uint32_t c) { return TB + c * NT; };
+    auto ACC = [&](uint32_t c, uint32_t k, uint32_t b) { return AC + (c * KC + k) * 8 + b; };
+    // column c's memory operations: the row offset + 256 c, under column c's exec mask (s[96:97] for c = 1)
+    auto col_exec = [&](Asm& a, uint32_t c, bool on) {
+        if (c) a.line(on ? "s_mov_b64 exec, s[96:97]" : "s_mov_b64 exec, s[98:99]");
+    };
     Asm a;
     a.s += "\t.amdgcn_target \"amdgcn-amd-amdhsa--gfx950\"\n\t.amdhsa_code_object_version 6\n\t.text\n";
     a.s += "\t.globl " + kname + "\n\t.p2align 8\n\t.type " + kname + ",@function\n" + kname + ":\n";
-    // ---- prologue: which block / slice / strip, and whether it has work.  Round 1: the arguments;
+    // ---- prologue: which block / slice / column group, and whether it has work.  Round 1: the arguments;
     // round 2: the block's header, the slice's output rows and the first PDG groups' row offsets.
     a.line("s_load_dwordx8 s[8:15], s[0:1], 0x0");     // gi(8:9) block_bytes of_bytes ix_bytes ix_slice n_blocks T
     a.line("s_load_dwordx4 s[16:19], s[0:1], 0x20");   // strips nsg sg_magic ws
@@ -86,15 +97,21 @@ std::string emit_apply_gi_asm(const GiShape& sh) {
     a.line("s_mul_i32 s35, s34, s17");
     a.line("s_sub_u32 s35, s3, s35");                  // strip group
     a.line("s_mul_i32 s35, s35, s19");
-    a.line("s_add_u32 s35, s35, s36");                 // strip
+    a.line("s_add_u32 s35, s35, s36");                 // strip: CPL x 64 dword columns
     a.line("s_cmp_ge_u32 s35, s16");
     a.line("s_cbranch_scc1 .Lend");
-    // the lane's dword column; lanes past T / 4 run with exec off
-    a.line("s_lshl_b32 s36, s35, 6");
+    // the lane's dword column(s); lanes past T / 4 run with exec off (column 1: its own mask s[96:97])
+    a.f("s_lshl_b32 s36, s35, %u", CPL == 2 ? 7 : 6);
     a.line("v_add_u32_e32 v1, s36, v0");
     a.line("s_lshr_b32 s36, s15, 2");
     a.line("v_cmp_gt_u32_e64 s[42:43], s36, v1");
     a.line("s_and_b64 exec, exec, s[42:43]");
+    if (CPL == 2) {
+        a.line("s_sub_u32 s37, s36, 64");
+        a.line("v_cmp_gt_i32_e64 s[96:97], s37, v1");  // (signed: T / 4 < 64 leaves it empty)
+        a.line("s_and_b64 s[96:97], s[96:97], exec");
+        a.line("s_mov_b64 s[98:99], exec");
+    }
     a.line("v_lshlrev_b32_e32 v1, 2, v1");
     // the block's stream at gi + bi * block_bytes: offsets -> s[62:63], this slice's index records ->
     // s[44:45], its output rows -> s[60:61]
@@ -138,16 +155,23 @@ std::string emit_apply_gi_asm(const GiShape& sh) {
     a.line("s_and_b32 s57, s73, 0xffff");
     a.line("s_mov_b32 s58, -1");
     a.line("s_mov_b32 s59, 0x20000");
-    a.f("v_mov_b32_e32 v%u, 0", TB);
-    for (uint32_t k = 0; k < KC; ++k)
-        for (uint32_t b = 1; b < 8; ++b) a.f("v_mov_b32_e32 v%u, 0", ACC(k, b));
+    for (uint32_t c = 0; c < CPL; ++c) {
+        a.f("v_mov_b32_e32 v%u, 0", TBC(c));
+        for (uint32_t k = 0; k < KC; ++k)
+            for (uint32_t b = 1; b < 8; ++b) a.f("v_mov_b32_e32 v%u, 0", ACC(c, k, b));
+    }
     // g_E (the erased rows as they are) into plane 0; then the first PDG groups' syndrome rows
-    for (uint32_t k = 0; k < KC; ++k) a.f("buffer_load_dword v%u, v1, s[56:59], s%u offen", ACC(k, 0), 80 + k);
-    for (uint32_t p = 0; p < PDG; ++p)
-        for (uint32_t t = 0; t < G; ++t) {
-            a.f("buffer_load_dword v%u, v1, s[48:51], s%u offen", RA(p, t), 16 * p + 2 * t);
-            a.f("buffer_load_dword v%u, v1, s[52:55], s%u offen", RB(p, t), 16 * p + 2 * t + 1);
-        }
+    for (uint32_t c = 0; c < CPL; ++c) {
+        col_exec(a, c, true);
+        for (uint32_t k = 0; k < KC; ++k)
+            a.f("buffer_load_dword v%u, v1, s[56:59], s%u offen offset:%u", ACC(c, k, 0), 80 + k, 256 * c);
+        for (uint32_t p = 0; p < PDG; ++p)
+            for (uint32_t t = 0; t < G; ++t) {
+                a.f("buffer_load_dword v%u, v1, s[48:51], s%u offen offset:%u", RA(c, p, t), 16 * p + 2 * t, 256 * c);
+                a.f("buffer_load_dword v%u, v1, s[52:55], s%u offen offset:%u", RB(c, p, t), 16 * p + 2 * t + 1, 256 * c);
+            }
+        col_exec(a, c, false);
+    }
     a.f("s_add_u32 s62, s62, 0x%x", 64 * PDG);
     a.line("s_addc_u32 s63, s63, 0");
     // C = s[32:43]: the offsets of the group PDG ahead; pieces A = s[0:31], B = s[64:95]
@@ -169,24 +193,34 @@ std::string emit_apply_gi_asm(const GiShape& sh) {
         a.line("s_waitcnt lgkmcnt(0)");
         for (uint32_t r = 64; r < 96; r += 2) a.f("s_mov_b64 s[%u:%u], 0", r, r + 1);
     }
-    // ---- the groups: PDG copies of the body (ring slot p = g mod PDG), each ending in the exit test
+    // ---- the groups: UNR copies of the body (ring slot p = u mod PDG), each ending in the exit test
+    const uint32_t loads_per_group = 2 * G * CPL;
     a.s += ".Lgroup:\n";
-    for (uint32_t p = 0; p < PDG; ++p) {
-        a.f("s_waitcnt vmcnt(%u)", 2 * G * (PDG - 1));
-        for (uint32_t t = 0; t < G; ++t) a.f("v_xor_b32_e32 v%u, v%u, v%u", TB + (1u << t), RA(p, t), RB(p, t));
-        for (uint32_t i = 3; i < NT; ++i) {
-            if ((i & (i - 1)) == 0) continue;
-            const uint32_t lo = i & (0u - i);
-            a.f("v_xor_b32_e32 v%u, v%u, v%u", TB + i, TB + (i ^ lo), TB + lo);
+    uint32_t pair_no = 0;  // pieces alternate A, B over the whole body
+    for (uint32_t u = 0; u < UNR; ++u) {
+        const uint32_t p = u % PDG;
+        a.f("s_waitcnt vmcnt(%u)", loads_per_group * (PDG - 1));
+        for (uint32_t c = 0; c < CPL; ++c) {
+            for (uint32_t t = 0; t < G; ++t)
+                a.f("v_xor_b32_e32 v%u, v%u, v%u", TBC(c) + (1u << t), RA(c, p, t), RB(c, p, t));
+            for (uint32_t i = 3; i < NT; ++i) {
+                if ((i & (i - 1)) == 0) continue;
+                const uint32_t lo = i & (0u - i);
+                a.f("v_xor_b32_e32 v%u, v%u, v%u", TBC(c) + i, TBC(c) + (i ^ lo), TBC(c) + lo);
+            }
         }
         a.line("s_waitcnt lgkmcnt(0)");  // C and this group's first pair
         if (!(sh.diag & 2))
-            for (uint32_t t = 0; t < G; ++t) {  // the group PDG ahead into the slot just consumed
-                a.f("buffer_load_dword v%u, v1, s[48:51], s%u offen", RA(p, t), 32 + 2 * t);
-                a.f("buffer_load_dword v%u, v1, s[52:55], s%u offen", RB(p, t), 33 + 2 * t);
+            for (uint32_t c = 0; c < CPL; ++c) {  // the group PDG ahead into the slot just consumed
+                col_exec(a, c, true);
+                for (uint32_t t = 0; t < G; ++t) {
+                    a.f("buffer_load_dword v%u, v1, s[48:51], s%u offen offset:%u", RA(c, p, t), 32 + 2 * t, 256 * c);
+                    a.f("buffer_load_dword v%u, v1, s[52:55], s%u offen offset:%u", RB(c, p, t), 33 + 2 * t, 256 * c);
+                }
+                col_exec(a, c, false);
             }
-        for (uint32_t j = 0; j < PAIRS; ++j) {
-            const uint32_t cur = (j & 1) ? 64 : 0, nxt = (j & 1) ? 0 : 64;
+        for (uint32_t j = 0; j < PAIRS; ++j, ++pair_no) {
+            const uint32_t cur = (pair_no & 1) ? 64 : 0, nxt = (pair_no & 1) ? 0 : 64;
             if (!(sh.diag & 1)) {
                 if (j == 0) load_c();
                 else a.line("s_waitcnt lgkmcnt(0)");
@@ -197,7 +231,7 @@ std::string emit_apply_gi_asm(const GiShape& sh) {
                 const uint32_t k = 4 * j + q / 8, b = q % 8;
                 if (j == 0 && q == 0) a.f("s_set_gpr_idx_on s%u, gpr_idx(SRC0)", cur + q);
                 else a.f("s_set_gpr_idx_idx s%u", cur + q);
-                a.f("v_xor_b32_e32 v%u, v%u, v%u", ACC(k, b), TB, ACC(k, b));
+                for (uint32_t c = 0; c < CPL; ++c) a.f("v_xor_b32_e32 v%u, v%u, v%u", ACC(c, k, b), TBC(c), ACC(c, k, b));
             }
         }
         if (!(sh.diag & 4)) a.line("s_set_gpr_idx_off");
@@ -213,17 +247,20 @@ std::string emit_apply_gi_asm(const GiShape& sh) {
     a.line("s_mov_b32 s36, 0x090b080a");
     a.line("s_mov_b32 s37, 0xfefefefe");
     a.line("s_mov_b32 s38, 0x1d1d1d1d");
-    for (uint32_t k0 = 0; k0 < KC; k0 += 3) {
-        const uint32_t n = std::min<uint32_t>(3, KC - k0);
+    std::vector<std::pair<uint32_t, uint32_t>> outs;  // (column, output)
+    for (uint32_t c = 0; c < CPL; ++c)
+        for (uint32_t k = 0; k < KC; ++k) outs.push_back({c, k});
+    for (size_t o0 = 0; o0 < outs.size(); o0 += 3) {
+        const uint32_t n = (uint32_t)std::min<size_t>(3, outs.size() - o0);
+        auto P = [&](uint32_t u, uint32_t b) { return ACC(outs[o0 + u].first, outs[o0 + u].second, b); };
         for (int b = 6; b >= 0; --b) {
-            for (uint32_t u = 0; u < n; ++u) a.f("v_lshlrev_b32_e32 v%u, 8, v%u", 2 + 2 * u, ACC(k0 + u, b + 1));
+            for (uint32_t u = 0; u < n; ++u) a.f("v_lshlrev_b32_e32 v%u, 8, v%u", 2 + 2 * u, P(u, b + 1));
+            for (uint32_t u = 0; u < n; ++u) a.f("v_perm_b32 v%u, v%u, v%u, s36", 2 + 2 * u, 2 + 2 * u, P(u, b + 1));
             for (uint32_t u = 0; u < n; ++u)
-                a.f("v_perm_b32 v%u, v%u, v%u, s36", 2 + 2 * u, 2 + 2 * u, ACC(k0 + u, b + 1));
+                a.f("v_bitop3_b32 v%u, v%u, v%u, s38 bitop3:0x6c", 2 + 2 * u, 2 + 2 * u, P(u, b));
+            for (uint32_t u = 0; u < n; ++u) a.f("v_lshlrev_b32_e32 v%u, 1, v%u", 3 + 2 * u, P(u, b + 1));
             for (uint32_t u = 0; u < n; ++u)
-                a.f("v_bitop3_b32 v%u, v%u, v%u, s38 bitop3:0x6c", 2 + 2 * u, 2 + 2 * u, ACC(k0 + u, b));
-            for (uint32_t u = 0; u < n; ++u) a.f("v_lshlrev_b32_e32 v%u, 1, v%u", 3 + 2 * u, ACC(k0 + u, b + 1));
-            for (uint32_t u = 0; u < n; ++u)
-                a.f("v_bitop3_b32 v%u, v%u, v%u, s37 bitop3:0x6c", ACC(k0 + u, b), 3 + 2 * u, 2 + 2 * u);
+                a.f("v_bitop3_b32 v%u, v%u, v%u, s37 bitop3:0x6c", P(u, b), 3 + 2 * u, 2 + 2 * u);
         }
     }
     a.line("s_load_dwordx16 s[64:79], s[60:61], 0x0");
@@ -231,7 +268,11 @@ std::string emit_apply_gi_asm(const GiShape& sh) {
     for (uint32_t k = 0; k < KC; ++k) {
         a.f("s_cmp_le_u32 s47, %u", k);
         a.line("s_cbranch_scc1 .Lend");
-        a.f("buffer_store_dword v%u, v1, s[56:59], s%u offen", ACC(k, 0), 64 + k);
+        for (uint32_t c = 0; c < CPL; ++c) {
+            col_exec(a, c, true);
+            a.f("buffer_store_dword v%u, v1, s[56:59], s%u offen offset:%u", ACC(c, k, 0), 64 + k, 256 * c);
+            col_exec(a, c, false);
+        }
     }
     a.s += ".Lend:\n\ts_endpgm\n";
     a.s += ".Lfunc_end:\n\t.size " + kname + ", .Lfunc_end-" + kname + "\n";
@@ -241,13 +282,13 @@ std::string emit_apply_gi_asm(const GiShape& sh) {
     a.s += "\t\t.amdhsa_user_sgpr_kernarg_segment_ptr 1\n\t\t.amdhsa_system_sgpr_workgroup_id_x 1\n";
     a.s += "\t\t.amdhsa_system_sgpr_workgroup_id_y 1\n\t\t.amdhsa_system_sgpr_workgroup_id_z 1\n";
     a.s += "\t\t.amdhsa_system_vgpr_workitem_id 0\n\t\t.amdhsa_next_free_vgpr " + std::to_string(NV) + "\n";
-    a.s += "\t\t.amdhsa_next_free_sgpr 96\n\t\t.amdhsa_accum_offset " + std::to_string((NV + 3) & ~3u) + "\n";
+    a.s += "\t\t.amdhsa_next_free_sgpr 100\n\t\t.amdhsa_accum_offset " + std::to_string((NV + 3) & ~3u) + "\n";
     a.s += "\t\t.amdhsa_reserve_vcc 0\n\t\t.amdhsa_ieee_mode 0\n\t\t.amdhsa_dx10_clamp 0\n\t.end_amdhsa_kernel\n\t.text\n";
     a.s += "\t.amdgpu_metadata\n---\namdhsa.kernels:\n  - .agpr_count: 0\n    .args:\n";
     a.s += "      - .offset: 0\n        .size: 48\n        .value_kind: by_value\n";
     a.s += "    .group_segment_fixed_size: 0\n    .kernarg_segment_align: 8\n    .kernarg_segment_size: 48\n";
     a.s += "    .max_flat_workgroup_size: 512\n    .name: " + kname + "\n    .private_segment_fixed_size: 0\n";
-    a.s += "    .sgpr_count: 96\n    .symbol: " + kname + ".kd\n    .vgpr_count: " + std::to_string(NV) +
+    a.s += "    .sgpr_count: 100\n    .symbol: " + kname + ".kd\n    .vgpr_count: " + std::to_string(NV) +
            "\n    .wavefront_size: 64\n";
     a.s += "amdhsa.target: amdgcn-amd-amdhsa--gfx950\namdhsa.version:\n  - 1\n  - 2\n...\n\t.end_amdgpu_metadata\n";
     return a.s;

@@ -99,6 +99,7 @@ struct ApplyArgs {
 // syndrome loads PDG groups ahead (1..2).
 struct GiShape {
     uint32_t KC = 8, G = 5, PDG = 2;
+    uint32_t CPL = 1;   // dword columns per lane (64-column strips per wave), 1 or 2
     uint32_t diag = 0;  // experiments (timing only, wrong bytes): 1 no index loads, 2 no syndrome loads, 4 no lookups
 };
 

@@ -1148,15 +1148,16 @@ bool solve_beside() {
 uint32_t g_apply_mode = 1;
 
 // The register-table apply's shape: KC = 8 outputs per wave, groups of G = 5 syndromes, loads two groups
-// ahead (124 VGPRs: four waves per SIMD); RQHIP_APPLY_GI="KC,G,PDG" in experiments builds.
+// ahead, one dword column per lane (120 VGPRs: four waves per SIMD); RQHIP_APPLY_GI="KC,G,PDG[,CPL]" in
+// experiments builds.
 const GiShape& apply_gi_shape() {
     static const GiShape sh = [] {
         GiShape g;
         if (const char* e = knob("RQHIP_APPLY_GI")) {
-            unsigned kc = 0, gg = 0, pd = 0;
-            if (std::sscanf(e, "%u,%u,%u", &kc, &gg, &pd) == 3) {
+            unsigned kc = 0, gg = 0, pd = 0, cpl = 1;
+            if (std::sscanf(e, "%u,%u,%u,%u", &kc, &gg, &pd, &cpl) >= 3) {
                 GiShape t;
-                t.KC = kc; t.G = gg; t.PDG = pd;
+                t.KC = kc; t.G = gg; t.PDG = pd; t.CPL = cpl;
                 if (gi_shape_ok(t)) g = t;
             }
         }
@@ -1169,7 +1170,7 @@ const GiShape& apply_gi_shape() {
 // The apply kernel of this device, assembled (amd_comgr, in process) on first use.  Caller holds ctx->mu.
 int get_gi_kernel(DevCtx* ctx, const GiShape& sh, hipFunction_t* fn) {
     if (ctx->gi_fn && ctx->gi_shape.KC == sh.KC && ctx->gi_shape.G == sh.G && ctx->gi_shape.PDG == sh.PDG &&
-        ctx->gi_shape.diag == sh.diag) {
+        ctx->gi_shape.CPL == sh.CPL && ctx->gi_shape.diag == sh.diag) {
         *fn = ctx->gi_fn;
         return RQ_OK;
     }
@@ -1424,7 +1425,7 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
         ga.ix_slice_bytes = gl.ix_slice * 4;
         ga.n_blocks = nw;
         ga.T = T;
-        ga.strips = (T / 4 + 63) / 64;
+        ga.strips = (T / 4 + 64 * gsh.CPL - 1) / (64 * gsh.CPL);  // waves per (block, slice)
         // one wave per workgroup: the strips of a (block, slice) as one workgroup (sharing the CU's scalar
         // cache, RQHIP_APPLY_WS=8 in experiments builds) measured 152 against 112 us
         static const uint32_t ws_cap = [] { const char* e = knob("RQHIP_APPLY_WS"); return e ? (uint32_t)std::max(1, std::atoi(e)) : 1u; }();
@@ -2318,11 +2319,11 @@ uint32_t rq_debug_virtual_shards(uint32_t n) {
     return old;
 }
 
-int rq_debug_apply_gi_asm(uint32_t kc, uint32_t g, uint32_t pdg, char* text, size_t cap, size_t* text_len,
+int rq_debug_apply_gi_asm(uint32_t kc, uint32_t g, uint32_t pdg, uint32_t cpl, char* text, size_t cap, size_t* text_len,
                           size_t* code_bytes) {
     GiShape sh;
-    sh.KC = kc; sh.G = g; sh.PDG = pdg;
-    if (!gi_shape_ok(sh)) return fail(RQ_ERR_BAD_ARG, "apply shape: KC 8 or 16, G 4..6, PDG 1..3");
+    sh.KC = kc; sh.G = g; sh.PDG = pdg; sh.CPL = cpl;
+    if (!gi_shape_ok(sh)) return fail(RQ_ERR_BAD_ARG, "apply shape: KC 4..16 (a multiple of 4), G 4..6, PDG 1..2, CPL 1..2, <= 256 VGPRs");
     const std::string src = emit_apply_gi_asm(sh);
     if (text_len) *text_len = src.size();
     if (text && cap) {

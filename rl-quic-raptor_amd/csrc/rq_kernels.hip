@@ -167,7 +167,8 @@ int launch_xbits(const XbitsArgs& a, uint32_t n_blocks, const GiShape& s, void* 
     RQ_XB(8, 5, 2)
 #ifdef RQHIP_EXPERIMENTS
     RQ_XB(16, 6, 1) RQ_XB(16, 6, 2) RQ_XB(16, 5, 2) RQ_XB(8, 6, 2) RQ_XB(8, 5, 1) RQ_XB(8, 4, 1) RQ_XB(16, 4, 2)
-    RQ_XB(8, 4, 2) RQ_XB(8, 6, 1)
+    RQ_XB(8, 4, 2) RQ_XB(8, 6, 1) RQ_XB(12, 5, 1) RQ_XB(12, 5, 2) RQ_XB(4, 5, 1) RQ_XB(4, 4, 1) RQ_XB(4, 5, 2)
+    RQ_XB(12, 4, 2) RQ_XB(16, 5, 1)
 #endif
 #undef RQ_XB
     return (int)hipErrorInvalidValue;

@@ -190,7 +190,8 @@ def _load(path):
                                       ctypes.c_int),
         "rq_debug_decode_margin": ([ctypes.c_uint32], ctypes.c_uint32),
         "rq_debug_apply_mode": ([ctypes.c_uint32], ctypes.c_uint32),
-        "rq_debug_apply_gi_asm": ([ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t,
+        "rq_debug_apply_gi_asm": ([ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_char_p,
+                                   ctypes.c_size_t,
                                    ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
         "rq_decode_blocks_host": ([ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(BlockIO), ctypes.c_uint32,
                                    ctypes.c_uint32], ctypes.c_int),
@@ -386,13 +387,13 @@ def assemble(text):
     return n.value
 
 
-def apply_gi_asm(kc=16, g=6, pdg=2, assemble=True):
+def apply_gi_asm(kc=8, g=5, pdg=2, cpl=1, assemble=True):
     """rq_debug_apply_gi_asm: (assembly text, code object size or None) of the register-table apply kernel."""
     n = ctypes.c_size_t(0)
-    _check(lib().rq_debug_apply_gi_asm(kc, g, pdg, None, 0, ctypes.byref(n), None))
+    _check(lib().rq_debug_apply_gi_asm(kc, g, pdg, cpl, None, 0, ctypes.byref(n), None))
     buf = ctypes.create_string_buffer(n.value + 1)
     co = ctypes.c_size_t(0)
-    _check(lib().rq_debug_apply_gi_asm(kc, g, pdg, buf, n.value + 1, None, ctypes.byref(co) if assemble else None))
+    _check(lib().rq_debug_apply_gi_asm(kc, g, pdg, cpl, buf, n.value + 1, None, ctypes.byref(co) if assemble else None))
     return buf.value.decode(), (co.value if assemble else None)
 
 
