@@ -244,6 +244,10 @@ uint32_t rq_debug_decode_margin(uint32_t margin);
  * rq_apply_gi kernel, rq_applygi.cpp), 0 = k_apply's v_perm byte tables.  Sets the mode (values > 1
  * leave it) and returns the previous one; both give the same bytes. */
 uint32_t rq_debug_apply_mode(uint32_t mode);
+/* The decode's first solve pass (e <= 64): 1 = in place (k_solve_ip: rows of e bytes, the eliminated
+ * column holds the pivot row's identity column), 0 = Gauss-Jordan on [M | I] (k_solve_pq).  Sets the
+ * mode (values > 1 leave it) and returns the previous one; both give the same X. */
+uint32_t rq_debug_solve_mode(uint32_t mode);
 /* The register-table apply kernel's assembly for shape (KC outputs per wave, groups of G syndromes,
  * loads PDG groups ahead, CPL dword columns per lane): copied into text (cap bytes, NUL-terminated) when given, its length in
  * *text_len, and, when code_bytes is given, assembled in process (its code object size). */

@@ -43,57 +43,6 @@ struct PackArgs {
 // within the block) at xpiv + erased_off[b].
 __host__ __device__ inline uint32_t x_stride(uint32_t e) { return 64u * ((e + 63u) / 64u); }
 
-struct SolveArgs {
-    const uint32_t* blk_map;    // grid.x -> block index
-    const uint32_t* erased_off; // per block ranges into erased[]
-    const uint32_t* erased;
-    const uint32_t* rep_off;    // per block: first received repair row in rep_uidx[] / recv
-    const uint32_t* rep_cnt;    // per block: received repairs the solvers may use (the first rep_cnt[b])
-    const uint32_t* rep_uidx;
-    const uint8_t* mrep;
-    uint32_t mrep_stride;
-    uint8_t* xcoef;             // X of solved block bi at xcoef + 64 * xoff[bi]
-    const uint32_t* xoff;
-    uint16_t* xpiv;             // xpiv[erased_off[b] + m]: received repair (index within block b) of X row m
-    int32_t* status;            // per block: 1 ok, 0 rank-deficient, ST_FALLBACK (general solver)
-    uint8_t* gws;               // general solver: basis of block bi at gws + 64 * goff[bi] when e > lds_e
-    const uint32_t* goff;
-    uint32_t lds_e;             // largest e whose basis the general solver keeps in LDS
-    // host-decided statuses of all n_all blocks (ST_PENDING for the solver's blocks), read by the
-    // first solver launch in place of an upload (nullptr: status already holds them)
-    const int32_t* status_init;
-    uint32_t n_all;
-    // first pass (k_solve_pm<1, ...>): use at most e + row_margin received repairs (0 = up to 64); a
-    // block rank-deficient on them is deferred to the later passes like one beyond 64
-    uint32_t row_margin;
-    uint32_t n_map;             // entries of blk_map (the general solver's grid strides over them)
-    uint32_t diag_steps;        // experiments builds (RQHIP_SOLVE_STEPS): pivot steps of k_solve_pq (timing only)
-};
-constexpr int32_t ST_PENDING = -100;   // queued for the solver
-constexpr int32_t ST_FALLBACK = -101;  // beyond the fast solvers: the general solver decides
-// General-solver basis row width (coefficients then combination of selected rows), 16-byte aligned.
-__host__ __device__ inline uint32_t basis_width(uint32_t e) { return (2u * e + 15u) & ~15u; }
-
-struct ApplyArgs {
-    const uint32_t* blk_map;
-    const uint32_t* erased_off;
-    const uint32_t* erased;
-    const uint32_t* rep_off;
-    const uint32_t* rep_uidx;
-    const uint8_t* recv;        // received repair rows (T bytes each), rep_off order
-    const uint8_t* r0;          // n_union rows of T bytes per block
-    uint32_t n_union;
-    const uint8_t* xcoef;
-    const uint32_t* xoff;
-    const uint16_t* xpiv;
-    const int32_t* status;
-    uint8_t* data;
-    uint64_t data_stride;
-    uint32_t T;
-    uint32_t max_e;             // largest e of the batch (slice sizing)
-    uint32_t out_sc1 = 0;       // 1: recovered rows stored sc1 (written through, not left dirty in L2)
-};
-
 // The register-table apply (rq_applygi.cpp): x_E = g_E ^ X s as 8 GF(2) bit planes.  Shape: KC outputs
 // per wave (8 or 16), syndromes in groups of G (4..6) whose 2^G subset XORs form a table in VGPRs,
 // syndrome loads PDG groups ahead (1..2).
@@ -149,6 +98,60 @@ struct XbitsArgs {
     uint32_t T, n_union;
 };
 
+struct SolveArgs {
+    const uint32_t* blk_map;    // grid.x -> block index
+    const uint32_t* erased_off; // per block ranges into erased[]
+    const uint32_t* erased;
+    const uint32_t* rep_off;    // per block: first received repair row in rep_uidx[] / recv
+    const uint32_t* rep_cnt;    // per block: received repairs the solvers may use (the first rep_cnt[b])
+    const uint32_t* rep_uidx;
+    const uint8_t* mrep;
+    uint32_t mrep_stride;
+    uint8_t* xcoef;             // X of solved block bi at xcoef + 64 * xoff[bi]
+    const uint32_t* xoff;
+    uint16_t* xpiv;             // xpiv[erased_off[b] + m]: received repair (index within block b) of X row m
+    int32_t* status;            // per block: 1 ok, 0 rank-deficient, ST_FALLBACK (general solver)
+    uint8_t* gws;               // general solver: basis of block bi at gws + 64 * goff[bi] when e > lds_e
+    const uint32_t* goff;
+    uint32_t lds_e;             // largest e whose basis the general solver keeps in LDS
+    // host-decided statuses of all n_all blocks (ST_PENDING for the solver's blocks), read by the
+    // first solver launch in place of an upload (nullptr: status already holds them)
+    const int32_t* status_init;
+    uint32_t n_all;
+    // first pass (k_solve_pm<1, ...>): use at most e + row_margin received repairs (0 = up to 64); a
+    // block rank-deficient on them is deferred to the later passes like one beyond 64
+    uint32_t row_margin;
+    uint32_t n_map;             // entries of blk_map (the general solver's grid strides over them)
+    uint32_t diag_steps;        // experiments builds (RQHIP_SOLVE_STEPS): pivot steps of k_solve_pq (timing only)
+    // k_solve also writes the register-table apply's index stream (the shipped shape 8, 5, 2) when set
+    uint32_t xb_on;
+    XbitsArgs xb;
+};
+constexpr int32_t ST_PENDING = -100;   // queued for the solver
+constexpr int32_t ST_FALLBACK = -101;  // beyond the fast solvers: the general solver decides
+// General-solver basis row width (coefficients then combination of selected rows), 16-byte aligned.
+__host__ __device__ inline uint32_t basis_width(uint32_t e) { return (2u * e + 15u) & ~15u; }
+
+struct ApplyArgs {
+    const uint32_t* blk_map;
+    const uint32_t* erased_off;
+    const uint32_t* erased;
+    const uint32_t* rep_off;
+    const uint32_t* rep_uidx;
+    const uint8_t* recv;        // received repair rows (T bytes each), rep_off order
+    const uint8_t* r0;          // n_union rows of T bytes per block
+    uint32_t n_union;
+    const uint8_t* xcoef;
+    const uint32_t* xoff;
+    const uint16_t* xpiv;
+    const int32_t* status;
+    uint8_t* data;
+    uint64_t data_stride;
+    uint32_t T;
+    uint32_t max_e;             // largest e of the batch (slice sizing)
+    uint32_t out_sc1 = 0;       // 1: recovered rows stored sc1 (written through, not left dirty in L2)
+};
+
 // Kernel arguments of the generated apply kernel; its prologue loads them at these byte offsets.
 struct ApplyGiArgs {
     const uint32_t* gi;         // 0
@@ -174,8 +177,9 @@ int launch_pack_rows(const PackArgs& a, void* stream);
 // general solver (any e, every received repair) for the blocks they deferred.
 // need_general: some block may end in the general solver (e or candidate repairs > 64); wide: some
 // block has 64 < e <= 128 (the two-row-per-lane fast solver runs first).
+// xbits_done (optional): set when the launches also wrote the index stream of a.xb (a.xb_on and k_solve ran).
 int launch_solve(const SolveArgs& a, uint32_t n_blocks, bool need_general, bool wide, uint32_t max_lds_e,
-                 void* stream);
+                 void* stream, bool* xbits_done = nullptr);
 int launch_apply(const ApplyArgs& a, uint32_t n_strips, uint32_t n_blocks, void* stream);
 int launch_gather(const DevParams& p, const uint8_t* C, uint32_t T, const uint32_t* esi, uint32_t n, uint8_t* out,
                   void* stream);
@@ -183,5 +187,7 @@ int launch_gather(const DevParams& p, const uint8_t* C, uint32_t T, const uint32
 size_t solve_ws_bytes(uint32_t e);
 uint32_t solve_lds_e_max();
 int upload_tables();  // rand / degree tables to __constant__ memory (once per device)
+// the first solve pass: 1 = k_solve_ip (in place), 0 = k_solve_pq<1, 4> (rq_debug_solve_mode)
+extern uint32_t g_solve_ip;
 
 }  // namespace rq

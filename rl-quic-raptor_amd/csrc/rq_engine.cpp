@@ -1367,7 +1367,33 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     s.row_margin = solve_row_margin();
     s.n_map = nw;
     s.diag_steps = 0;
-    if (launch_solve(s, nw, need_general, wide, max_lds_e, beside ? (void*)w->cs : stream))
+    // the register-table apply's index stream: written by k_solve's grid when it runs (the shipped shape),
+    // else by k_xbits after the solvers
+    XbitsArgs xa{};
+    if (gi) {
+        xa.blk_map = s.blk_map;
+        xa.status = s.status;
+        xa.erased_off = s.erased_off;
+        xa.erased = s.erased;
+        xa.rep_off = s.rep_off;
+        xa.rep_uidx = s.rep_uidx;
+        xa.xcoef = s.xcoef;
+        xa.xoff = s.xoff;
+        xa.xpiv = s.xpiv;
+        xa.recv = static_cast<const uint8_t*>(repair);
+        xa.r0 = w->r0.as<uint8_t>();
+        xa.data = static_cast<uint8_t*>(data);
+        xa.data_stride = data_stride;
+        xa.gi = w->gi.as<uint32_t>();
+        xa.L = gl;
+        xa.T = T;
+        xa.n_union = (uint32_t)uni.size();
+    }
+    const GiShape shipped;
+    s.xb_on = gi && max_e && gsh.KC == shipped.KC && gsh.G == shipped.G && gsh.PDG == shipped.PDG ? 1u : 0u;
+    s.xb = xa;
+    bool xbits_done = false;
+    if (launch_solve(s, nw, need_general, wide, max_lds_e, beside ? (void*)w->cs : stream, &xbits_done))
         return fail(RQ_ERR_DEVICE, "k_solve launch failed");
     if (beside) {
         HIP_TRY(hipEventRecord(w->solved, w->cs));
@@ -1398,25 +1424,7 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     static const uint32_t apply_sc1 = [] { const char* e = knob("RQHIP_APPLY_SC1"); return e && e[0] == '1' ? 1u : 0u; }();
     ap.out_sc1 = apply_sc1;
     if (gi && nw && max_e) {
-        XbitsArgs xa;
-        xa.blk_map = ap.blk_map;
-        xa.status = ap.status;
-        xa.erased_off = ap.erased_off;
-        xa.erased = ap.erased;
-        xa.rep_off = ap.rep_off;
-        xa.rep_uidx = ap.rep_uidx;
-        xa.xcoef = ap.xcoef;
-        xa.xoff = ap.xoff;
-        xa.xpiv = ap.xpiv;
-        xa.recv = ap.recv;
-        xa.r0 = ap.r0;
-        xa.data = ap.data;
-        xa.data_stride = data_stride;
-        xa.gi = w->gi.as<uint32_t>();
-        xa.L = gl;
-        xa.T = T;
-        xa.n_union = ap.n_union;
-        if (launch_xbits(xa, nw, gsh, stream)) return fail(RQ_ERR_DEVICE, "k_xbits launch failed");
+        if (!xbits_done && launch_xbits(xa, nw, gsh, stream)) return fail(RQ_ERR_DEVICE, "k_xbits launch failed");
         ApplyGiArgs ga{};
         ga.gi = xa.gi;
         ga.block_bytes = gl.block * 4;
@@ -2338,6 +2346,12 @@ int rq_debug_apply_gi_asm(uint32_t kc, uint32_t g, uint32_t pdg, uint32_t cpl, c
         *code_bytes = co.size();
     }
     return RQ_OK;
+}
+
+uint32_t rq_debug_solve_mode(uint32_t mode) {
+    const uint32_t old = g_solve_ip;
+    if (mode <= 1) g_solve_ip = mode;
+    return old;
 }
 
 uint32_t rq_debug_apply_mode(uint32_t mode) {

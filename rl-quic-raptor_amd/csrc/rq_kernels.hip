@@ -96,8 +96,7 @@ int launch_pack_rows(const PackArgs& a, void* stream) {
 // sum_m X[k][m] s_m = sum_b alpha^b sum_g Tab_g[idx_b], where Tab_g holds the 2^G XORs of group g's
 // syndromes (the apply kernel, rq_applygi.cpp).  Unsolved blocks get a header with status 0 only.
 template <int KC, int G, int PDG>
-__global__ void __launch_bounds__(256) k_xbits(XbitsArgs a) {
-    const uint32_t bi = blockIdx.x, tid = threadIdx.x;
+__device__ void xbits_block(const XbitsArgs& a, uint32_t bi, uint32_t tid) {
     const uint32_t b = a.blk_map[bi];
     const GiLayout& L = a.L;
     uint32_t* base = a.gi + (size_t)bi * L.block;
@@ -154,6 +153,11 @@ __global__ void __launch_bounds__(256) k_xbits(XbitsArgs a) {
         d[0] = make_uint4(v[0], v[1], v[2], v[3]);
         d[1] = make_uint4(v[4], v[5], v[6], v[7]);
     }
+}
+
+template <int KC, int G, int PDG>
+__global__ void __launch_bounds__(256) k_xbits(XbitsArgs a) {
+    xbits_block<KC, G, PDG>(a, blockIdx.x, threadIdx.x);
 }
 
 int launch_xbits(const XbitsArgs& a, uint32_t n_blocks, const GiShape& s, void* stream) {
@@ -375,6 +379,117 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
 
 
 
+// The same solve in place (e <= 64 on the first e + margin received repairs): a row holds only its e
+// coefficient bytes, and the column eliminated at step k is reused for the identity column of that step's
+// pivot row (the classic in-place Gauss-Jordan inverse).  After step k, byte k of row j holds c_j =
+// f_j / f_p (the multiple of pivot row p it took) and byte k of the pivot row 1 / f_p, so at the end row
+// pivl[k] byte m = X[k][m].  Every step updates all of a row's live quads (the identity columns keep
+// changing), but rows are e bytes wide instead of e + e + margin: ceil(e / 16) quads, one per wave.
+template <int NW>
+__global__ void __launch_bounds__(64 * NW) k_solve_ip(SolveArgs a) {
+    constexpr uint32_t NT = 64 * NW, NROWS = 64, SW = 20;  // rows, row stride (dwords: 16 + 4 against bank conflicts)
+    static_assert(NW == 4, "one 16-byte quad of each row per wave");
+    __shared__ __attribute__((aligned(16))) uint32_t rows[NROWS * SW];
+    __shared__ __attribute__((aligned(4))) uint8_t ex[512], lg[256];
+    __shared__ uint8_t pivl[NROWS];
+    __shared__ uint32_t Es[NROWS];
+    __shared__ __attribute__((aligned(16))) uint4 tlA[510];
+    __shared__ uint32_t tlB[510];
+    __shared__ uint32_t pinfo[256];
+    __shared__ uint8_t fcol[2][NROWS];
+    const uint32_t b = a.blk_map[blockIdx.x];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
+    if (a.status_init)
+        for (uint32_t i = blockIdx.x * NT + tid; i < a.n_all; i += gridDim.x * NT)
+            if (a.status_init[i] != ST_PENDING) a.status[i] = a.status_init[i];
+    const uint32_t e = a.erased_off[b + 1] - a.erased_off[b];
+    const uint32_t nr = a.rep_cnt[b];
+    if (e > NROWS) {
+        if (tid == 0) a.status[b] = ST_FALLBACK;
+        return;
+    }
+    const uint32_t nrow = a.row_margin ? min(min(nr, NROWS), e + a.row_margin) : min(nr, NROWS);
+    const uint32_t* E = a.erased + a.erased_off[b];
+    const uint32_t* U = a.rep_uidx + a.rep_off[b];
+    for (uint32_t i = tid; i < e; i += NT) Es[i] = E[i];
+    gf_tables_copy(ex, lg);
+    for (uint32_t l = tid; l < 510; l += NT) {
+        const uint32_t lm = l < 255 ? l : l - 255;
+        tlA[l] = make_uint4(kPerm.A[lm][0], kPerm.A[lm][1], kPerm.A[lm][2], kPerm.A[lm][3]);
+        tlB[l] = kPerm.B[lm];
+    }
+    for (uint32_t i = tid; i < NROWS * SW; i += NT) rows[i] = 0;
+    __syncthreads();
+    if (lane < nrow) gather_row<NW>(reinterpret_cast<uint8_t*>(rows + lane * SW), a.mrep + (size_t)U[lane] * a.mrep_stride, Es, e, g);
+    for (uint32_t x = tid; x < 256; x += NT) {  // as k_solve_pq: log f | log(1 ^ 1/f) << 8 | (1 ^ 1/f != 0) << 16
+        uint32_t v = 0;
+        if (x) {
+            const uint32_t lx = lg[x], cp = 1u ^ ex[255u - lx];
+            v = lx | (cp ? (uint32_t)lg[cp] << 8 | 1u << 16 : 0u);
+        }
+        pinfo[x] = v;
+    }
+    __syncthreads();
+    for (uint32_t r = tid; r < NROWS; r += NT) fcol[0][r] = (uint8_t)(rows[r * SW] & 0xFFu);
+    __syncthreads();
+    const uint32_t q1 = (e + 15) >> 4;  // quads holding the e columns
+    bool used = lane >= nrow;
+    uint4* myq = reinterpret_cast<uint4*>(rows + lane * SW) + g;
+    const uint8_t* rb = reinterpret_cast<const uint8_t*>(rows);
+    for (uint32_t k = 0; k < e; ++k) {
+        const uint4 R = *myq;  // this wave's quad of the lane's row (quads past q1 stay zero)
+        const uint32_t f = fcol[k & 1][lane];
+        const uint32_t pif = pinfo[f];
+        const uint64_t bal = __ballot(f != 0 && !used);
+        if (!bal) {  // uniform over the block
+            if (tid == 0) a.status[b] = (nr > nrow) ? ST_FALLBACK : 0;
+            return;
+        }
+        const uint32_t p = (uint32_t)__ffsll((unsigned long long)bal) - 1;
+        const bool piv = lane == p;
+        used |= piv;
+        if (tid == 0) pivl[k] = (uint8_t)p;
+        const uint4 P = reinterpret_cast<const uint4*>(rows + p * SW)[g];
+        const uint32_t pip = __builtin_amdgcn_readlane(pif, p);
+        const uint32_t ilgp = 255u - (pip & 0xFFu);
+        // c_j = f_j / f_p; the pivot lane 1 ^ 1 / f_p, which leaves row_p / f_p
+        const bool act = piv ? ((pif >> 16) & 1u) != 0 : f != 0;
+        const uint32_t l = piv ? (pif >> 8) & 0xFFu : (pif & 0xFFu) + ilgp;
+        const uint4 A = tlA[l];
+        const uint32_t B = tlB[l];
+        const uint32_t kn = k + 1;
+        if (g < q1) {
+            const uint32_t px = __builtin_amdgcn_readfirstlane(P.x), py = __builtin_amdgcn_readfirstlane(P.y);
+            const uint32_t pz = __builtin_amdgcn_readfirstlane(P.z), pw = __builtin_amdgcn_readfirstlane(P.w);
+            uint4 r = R;
+            r.x ^= perm_mul(A, B, px);
+            r.y ^= perm_mul(A, B, py);
+            r.z ^= perm_mul(A, B, pz);
+            r.w ^= perm_mul(A, B, pw);
+            if (g == (k >> 4)) {  // byte k: c_j (its identity entry for pivot p), or 1 / f_p on the pivot row
+                const uint32_t cb = ((A.x >> 8) & 0xFFu) ^ (piv ? 1u : 0u), sh = (k & 3u) * 8, d = (k >> 2) & 3u;
+                uint32_t& dw = d == 0 ? r.x : d == 1 ? r.y : d == 2 ? r.z : r.w;
+                dw = (dw & ~(0xFFu << sh)) | (cb << sh);
+            }
+            if (act) *myq = r;
+            if (kn < e && g == (kn >> 4)) {  // the next step's column, from this wave's registers
+                const uint4 v = act ? r : R;
+                const uint32_t d = (kn >> 2) & 3u;
+                const uint32_t dw = d == 0 ? v.x : d == 1 ? v.y : d == 2 ? v.z : v.w;
+                fcol[kn & 1][lane] = (uint8_t)((dw >> ((kn & 3u) * 8)) & 0xFFu);
+            }
+        }
+        __syncthreads();
+    }
+    uint8_t* xc = a.xcoef + 64ull * a.xoff[blockIdx.x];
+    const uint32_t xs = x_stride(e);
+    uint16_t* XP = a.xpiv + a.erased_off[b];
+    for (uint32_t m = tid; m < e; m += NT) XP[m] = pivl[m];
+    for (uint32_t m = g; m < e; m += NW)
+        for (uint32_t k = lane; k < e; k += 64) xc[m * xs + k] = rb[pivl[k] * SW * 4 + m];
+    if (tid == 0) a.status[b] = 1;
+}
+
 // General solver for the blocks the fast solvers deferred: any e, every received repair.  The
 // received rows are taken in order and reduced against a Gauss-Jordan basis of the rows kept so far
 // (basis row i: pivot column pc[i], coefficients zero on every other pivot column, then the
@@ -483,6 +598,14 @@ __global__ void __launch_bounds__(256) k_solve(SolveArgs a) {
     }
     __syncthreads();  // todo / ntodo are rewritten by the next pass
     }
+    // The register-table apply's index stream (k_xbits' work, in this launch instead of one of its own):
+    // this workgroup's blocks are the ones it checked above, all solved by now (earlier launches, or
+    // this workgroup's own passes: their status and X were written before the barriers above).
+    if (a.xb_on)
+        for (uint32_t bi = blockIdx.x; bi < a.n_map; bi += gridDim.x) {
+            __syncthreads();
+            xbits_block<8, 5, 2>(a.xb, bi, tid);
+        }
 }
 
 // k_solve's working set for e erased rows (LDS when e <= lds_e, else global workspace).
@@ -506,8 +629,13 @@ static bool knob_on(const char* name, bool dflt) {
 }
 #endif
 
+// The first solve in place (k_solve_ip) or on [M | I] (k_solve_pq<1, 4>); rq_debug_solve_mode switches it.
+uint32_t g_solve_ip = 0;
+static bool solve_in_place() { return g_solve_ip != 0; }
+
 int launch_solve(const SolveArgs& a_in, uint32_t n_blocks, bool need_general, bool wide, uint32_t max_lds_e,
-                 void* stream) {
+                 void* stream, bool* xbits_done) {
+    if (xbits_done) *xbits_done = false;
     // the first solver launch copies the host-decided statuses (a_in.status_init); later launches never do
     SolveArgs first = a_in;
     first.diag_steps = 0;
@@ -534,6 +662,7 @@ int launch_solve(const SolveArgs& a_in, uint32_t n_blocks, bool need_general, bo
         else if (nw == 2) hipLaunchKernelGGL((k_solve_pq<1, 2>), dim3(n_blocks), dim3(128), 0, st, first);
         else if (nw == 8) hipLaunchKernelGGL((k_solve_pq<1, 8>), dim3(n_blocks), dim3(512), 0, st, first);
         else if (pf) hipLaunchKernelGGL((k_solve_pq<1, 4, true>), dim3(n_blocks), dim3(256), 0, st, first);
+        else if (solve_in_place()) hipLaunchKernelGGL((k_solve_ip<4>), dim3(n_blocks), dim3(256), 0, st, first);
         else hipLaunchKernelGGL((k_solve_pq<1, 4>), dim3(n_blocks), dim3(256), 0, st, first);
         rx = (int)hipGetLastError();
     }
@@ -548,7 +677,8 @@ int launch_solve(const SolveArgs& a_in, uint32_t n_blocks, bool need_general, bo
     }
 #else
     // e <= 64 on the first e + margin received repairs (statuses copied in by this launch)
-    hipLaunchKernelGGL((k_solve_pq<1, 4>), dim3(n_blocks), dim3(256), 0, st, first);
+    if (solve_in_place()) hipLaunchKernelGGL((k_solve_ip<4>), dim3(n_blocks), dim3(256), 0, st, first);
+    else hipLaunchKernelGGL((k_solve_pq<1, 4>), dim3(n_blocks), dim3(256), 0, st, first);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !need_general) return (int)e;
     if (wide) {  // blocks with 64 < e <= 128; the rare rank-deficient-on-64-rows block goes to k_solve
@@ -571,7 +701,9 @@ int launch_solve(const SolveArgs& a_in, uint32_t n_blocks, bool need_general, bo
     if (const char* g = std::getenv("RQHIP_GSOLVE_GRID")) grid = std::max(1, std::min(256, std::atoi(g)));
 #endif
     hipLaunchKernelGGL(k_solve, dim3(grid), dim3(256), lds, (hipStream_t)stream, a);
-    return (int)hipGetLastError();
+    const hipError_t err = hipGetLastError();
+    if (err == hipSuccess && xbits_done) *xbits_done = a.xb_on != 0;
+    return (int)err;
 }
 
 uint32_t solve_lds_e_max() {

@@ -44,7 +44,7 @@ EXPORTED = (
     "rq_decoder_create", "rq_decoder_k", "rq_decoder_add", "rq_decoder_decode", "rq_decoder_free",
     "rq_encode_batch", "rq_decode_batch", "rq_decode_batch_async", "rq_encode_batch_host", "rq_decode_batch_host", "rq_device_count", "rq_set_device",
     "rq_debug_colprog_eval", "rq_debug_colprog_emulate", "rq_debug_colprog_assemble", "rq_debug_decode_margin",
-    "rq_debug_apply_mode", "rq_debug_apply_gi_asm",
+    "rq_debug_apply_mode", "rq_debug_apply_gi_asm", "rq_debug_solve_mode",
     "rq_decode_blocks_host", "rq_host_alloc", "rq_host_free", "rq_debug_colprog_passes",
     "rq_debug_shard_plan", "rq_debug_virtual_shards", "rq_debug_tuple", "rq_stream_release", "rq_shutdown",
     "rq_launch_timing", "rq_launch_time", "rq_debug_pair_emulate", "rq_debug_dma4_emulate", "rq_debug_decode_plan",
@@ -190,6 +190,7 @@ def _load(path):
                                       ctypes.c_int),
         "rq_debug_decode_margin": ([ctypes.c_uint32], ctypes.c_uint32),
         "rq_debug_apply_mode": ([ctypes.c_uint32], ctypes.c_uint32),
+        "rq_debug_solve_mode": ([ctypes.c_uint32], ctypes.c_uint32),
         "rq_debug_apply_gi_asm": ([ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_char_p,
                                    ctypes.c_size_t,
                                    ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
@@ -395,6 +396,11 @@ def apply_gi_asm(kc=8, g=5, pdg=2, cpl=1, assemble=True):
     co = ctypes.c_size_t(0)
     _check(lib().rq_debug_apply_gi_asm(kc, g, pdg, cpl, buf, n.value + 1, None, ctypes.byref(co) if assemble else None))
     return buf.value.decode(), (co.value if assemble else None)
+
+
+def solve_mode(mode):
+    """rq_debug_solve_mode: 1 = in-place first solve (k_solve_ip), 0 = k_solve_pq; returns the previous mode."""
+    return lib().rq_debug_solve_mode(mode)
 
 
 def apply_mode(mode):

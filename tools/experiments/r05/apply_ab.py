@@ -1,6 +1,7 @@
 """A/B of the decode's apply kernels on config 3 (1 024 blocks K=1024 T=1200, 55 of 1 100 symbols erased):
 decode_ms of rq_decode_batch_async with rq_debug_apply_mode 0 (k_apply) and 1 (register-table apply),
-interleaved, and a bytes check of both against the source.  Usage: python apply_ab.py [reps]"""
+interleaved, and a bytes check of both against the source.  Usage: python apply_ab.py [reps] [apply|solve]
+("solve": rq_debug_solve_mode 0 = k_solve_pq, 1 = in-place k_solve_ip instead)."""
 import os
 import sys
 import time
@@ -15,6 +16,7 @@ import rqhip as rq  # noqa: E402
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    setm = rq.solve_mode if len(sys.argv) > 2 and sys.argv[2] == "solve" else rq.apply_mode
     K, T, N, B, ne = 1024, 1200, 1100, 1024, 55
     dev = torch.device("cuda:0")
     g = torch.Generator().manual_seed(3)
@@ -36,7 +38,7 @@ def main():
     data = src.clone()
     res = {0: [], 1: []}
     for mode in (0, 1):
-        rq.apply_mode(mode)
+        setm(mode)
         d = src.clone()
         st = db.run(d, rep)
         torch.cuda.synchronize()
@@ -46,7 +48,7 @@ def main():
     s = torch.cuda.current_stream()
     for it in range(reps):
         for mode in (0, 1):
-            rq.apply_mode(mode)
+            setm(mode)
             for _ in range(2):
                 db.run_async(data, rep, stream=s)
             torch.cuda.synchronize()
@@ -60,7 +62,6 @@ def main():
     for mode in (0, 1):
         a = np.array(res[mode])
         print(f"mode {mode}: decode_ms median {np.median(a):.4f} min {a.min():.4f} max {a.max():.4f}", flush=True)
-    rq.apply_mode(1)
 
 
 if __name__ == "__main__":
