@@ -95,13 +95,14 @@ int launch_pack_rows(const PackArgs& a, void* stream) {
 // slice, group and output the eight G-bit subsets idx_b = sum_t bit_b(X[k][G g + t]) << t, so that
 // sum_m X[k][m] s_m = sum_b alpha^b sum_g Tab_g[idx_b], where Tab_g holds the 2^G XORs of group g's
 // syndromes (the apply kernel, rq_applygi.cpp).  Unsolved blocks get a header with status 0 only.
-template <int KC, int G, int PDG>
-__device__ void xbits_block(const XbitsArgs& a, uint32_t bi, uint32_t tid) {
-    const uint32_t b = a.blk_map[bi];
+// Block bi's part of the stream from X given as X(k, m) (coefficient byte of syndrome m in output k) and
+// XP(m) (the received row, within the block, of syndrome m); nthr threads from tid.  An unsolved block
+// (solved = false) gets its header only.
+template <int KC, int G, int PDG, class XF, class PF>
+__device__ void gi_stream(const XbitsArgs& a, uint32_t bi, uint32_t b, uint32_t e, bool solved, uint32_t tid,
+                          uint32_t nthr, XF X, PF XP) {
     const GiLayout& L = a.L;
     uint32_t* base = a.gi + (size_t)bi * L.block;
-    const bool solved = a.status[b] == 1;
-    const uint32_t e = a.erased_off[b + 1] - a.erased_off[b];
     const uint32_t ngr = (e + G - 1) / G, nsl = (e + KC - 1) / KC;
     if (tid < 16) {
         uint64_t v = 0;
@@ -116,43 +117,52 @@ __device__ void xbits_block(const XbitsArgs& a, uint32_t bi, uint32_t tid) {
     }
     if (!solved) return;
     const uint32_t* E = a.erased + a.erased_off[b];
-    const uint16_t* XP = a.xpiv + a.erased_off[b];
     const uint32_t* RU = a.rep_uidx + a.rep_off[b];
-    const uint8_t* xc = a.xcoef + 64ull * a.xoff[bi];
-    const uint32_t xs = x_stride(e), T = a.T;
-    for (uint32_t i = tid; i < nsl * 16; i += 256) {
+    const uint32_t T = a.T;
+    for (uint32_t i = tid; i < nsl * 16; i += nthr) {
         const uint32_t sl = i >> 4, k = i & 15, ko = sl * KC + k;
         base[L.er + i] = (k < (uint32_t)KC && ko < e) ? E[ko] * T : 0u;
     }
-    for (uint32_t i = tid; i < (ngr + PDG + 1) * 16; i += 256) {
+    for (uint32_t i = tid; i < (ngr + PDG + 1) * 16; i += nthr) {
         const uint32_t q = i >> 4, w = i & 15, t = w >> 1, m = G * q + t;
         uint32_t v = 0;
         if (t < (uint32_t)G && m < e) {
-            const uint32_t j = XP[m];
+            const uint32_t j = XP(m);
             v = (w & 1) ? RU[j] * T : j * T;
         }
         base[L.of + i] = v;
     }
-    for (uint32_t i = tid; i < nsl * ngr * KC; i += 256) {
+    for (uint32_t i = tid; i < nsl * ngr * KC; i += nthr) {
         const uint32_t k = i % KC, r = i / KC, g = r % ngr, sl = r / ngr, ko = sl * KC + k;
         uint32_t x[G];
 #pragma unroll
         for (int t = 0; t < G; ++t) {
             const uint32_t m = G * g + t;
-            x[t] = (ko < e && m < e) ? xc[(size_t)m * xs + ko] : 0u;
+            x[t] = (ko < e && m < e) ? (uint32_t)X(ko, m) : 0u;
         }
         uint32_t v[8];
 #pragma unroll
         for (int bit = 0; bit < 8; ++bit) {
-            uint32_t s = 0;
+            uint32_t sb = 0;
 #pragma unroll
-            for (int t = 0; t < G; ++t) s |= ((x[t] >> bit) & 1u) << t;
-            v[bit] = s;
+            for (int t = 0; t < G; ++t) sb |= ((x[t] >> bit) & 1u) << t;
+            v[bit] = sb;
         }
         uint4* d = reinterpret_cast<uint4*>(base + L.ix + sl * L.ix_slice + g * 8 * KC + k * 8);
         d[0] = make_uint4(v[0], v[1], v[2], v[3]);
         d[1] = make_uint4(v[4], v[5], v[6], v[7]);
     }
+}
+
+template <int KC, int G, int PDG>
+__device__ void xbits_block(const XbitsArgs& a, uint32_t bi, uint32_t tid) {
+    const uint32_t b = a.blk_map[bi];
+    const uint32_t e = a.erased_off[b + 1] - a.erased_off[b];
+    const uint8_t* xc = a.xcoef + 64ull * a.xoff[bi];
+    const uint32_t xs = x_stride(e);
+    const uint16_t* xp = a.xpiv + a.erased_off[b];
+    gi_stream<KC, G, PDG>(a, bi, b, e, a.status[b] == 1, tid, 256, [&](uint32_t k, uint32_t m) { return xc[(size_t)m * xs + k]; },
+                          [&](uint32_t m) { return (uint32_t)xp[m]; });
 }
 
 template <int KC, int G, int PDG>
@@ -307,6 +317,9 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
         }
         if (p == 0xFFFFFFFFu) {  // uniform over the block: every wave saw the same rows
             if (tid == 0) a.status[b] = (nr > nrow) ? ST_FALLBACK : 0;
+            if (a.xb_on && nr <= nrow)  // final: the apply skips it (a deferred block's solver writes its part)
+                gi_stream<8, 5, 2>(a.xb, blockIdx.x, b, e, false, tid, NT, [](uint32_t, uint32_t) { return 0u; },
+                                   [](uint32_t) { return 0u; });
             return;
         }
 #pragma unroll
@@ -370,9 +383,15 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
     const uint32_t xs = x_stride(e);
     uint16_t* XP = a.xpiv + a.erased_off[b];
     for (uint32_t m = tid; m < e; m += NT) XP[m] = pivl[m];
-    for (uint32_t m = g; m < e; m += NW) {  // wave g writes rows m = g, g + NW, ... (no index division)
-        const uint32_t pm = pivl[m];
-        for (uint32_t k = lane; k < e; k += 64) xc[m * xs + k] = rb[pivl[k] * SW * 4 + e + pm];
+    if (a.xb_on) {  // the register-table apply's stream straight from the rows: X[k][m] = row pivl[k], column e + pivl[m]
+        gi_stream<8, 5, 2>(a.xb, blockIdx.x, b, e, true, tid, NT,
+                           [&](uint32_t k, uint32_t m) { return (uint32_t)rb[pivl[k] * SW * 4 + e + pivl[m]]; },
+                           [&](uint32_t m) { return (uint32_t)pivl[m]; });
+    } else {
+        for (uint32_t m = g; m < e; m += NW) {  // wave g writes rows m = g, g + NW, ... (no index division)
+            const uint32_t pm = pivl[m];
+            for (uint32_t k = lane; k < e; k += 64) xc[m * xs + k] = rb[pivl[k] * SW * 4 + e + pm];
+        }
     }
     if (tid == 0) a.status[b] = 1;
 }
@@ -581,6 +600,9 @@ __global__ void __launch_bounds__(256) k_solve(SolveArgs a) {
     }
     if (np < e) {
         if (tid == 0) a.status[b] = 0;
+        if (a.xb_on)
+            gi_stream<8, 5, 2>(a.xb, bi, b, e, false, tid, nthr, [](uint32_t, uint32_t) { return 0u; },
+                               [](uint32_t) { return 0u; });
         __syncthreads();
         continue;
     }
@@ -594,18 +616,15 @@ __global__ void __launch_bounds__(256) k_solve(SolveArgs a) {
         xc[(size_t)m * xs + pc[i]] = A[(size_t)i * W2 + e + m];
     }
     if (tid == 0) a.status[b] = 1;
+    if (a.xb_on) {  // the apply's stream from the X just written (visible to the workgroup after the barrier)
+        __syncthreads();
+        gi_stream<8, 5, 2>(a.xb, bi, b, e, true, tid, nthr, [&](uint32_t k, uint32_t m) { return (uint32_t)xc[(size_t)m * xs + k]; },
+                           [&](uint32_t m) { return (uint32_t)XP[m]; });
+    }
     __syncthreads();  // the next block reuses the LDS
     }
     __syncthreads();  // todo / ntodo are rewritten by the next pass
     }
-    // The register-table apply's index stream (k_xbits' work, in this launch instead of one of its own):
-    // this workgroup's blocks are the ones it checked above, all solved by now (earlier launches, or
-    // this workgroup's own passes: their status and X were written before the barriers above).
-    if (a.xb_on)
-        for (uint32_t bi = blockIdx.x; bi < a.n_map; bi += gridDim.x) {
-            __syncthreads();
-            xbits_block<8, 5, 2>(a.xb, bi, tid);
-        }
 }
 
 // k_solve's working set for e erased rows (LDS when e <= lds_e, else global workspace).
@@ -635,9 +654,18 @@ static bool solve_in_place() { return g_solve_ip != 0; }
 
 int launch_solve(const SolveArgs& a_in, uint32_t n_blocks, bool need_general, bool wide, uint32_t max_lds_e,
                  void* stream, bool* xbits_done) {
-    if (xbits_done) *xbits_done = false;
     // the first solver launch copies the host-decided statuses (a_in.status_init); later launches never do
     SolveArgs first = a_in;
+    // k_solve_pq and k_solve write the apply's stream themselves (xb_on); any other first solver writes X
+    // only, and the caller runs k_xbits
+    bool stream_ok = solve_in_place() == false;
+#ifdef RQHIP_EXPERIMENTS
+    stream_ok = stream_ok && !std::getenv("RQHIP_SOLVE_PM") && !std::getenv("RQHIP_SOLVE_LUT") &&
+                !std::getenv("RQHIP_SOLVE_PQ") && !std::getenv("RQHIP_SOLVE_PF") && !std::getenv("RQHIP_SOLVE_LEAN") &&
+                !std::getenv("RQHIP_SOLVE_NW");
+#endif
+    if (!stream_ok) first.xb_on = 0;
+    if (xbits_done) *xbits_done = first.xb_on != 0;
     first.diag_steps = 0;
     const hipStream_t st = (hipStream_t)stream;
 #ifdef RQHIP_EXPERIMENTS
@@ -701,9 +729,7 @@ int launch_solve(const SolveArgs& a_in, uint32_t n_blocks, bool need_general, bo
     if (const char* g = std::getenv("RQHIP_GSOLVE_GRID")) grid = std::max(1, std::min(256, std::atoi(g)));
 #endif
     hipLaunchKernelGGL(k_solve, dim3(grid), dim3(256), lds, (hipStream_t)stream, a);
-    const hipError_t err = hipGetLastError();
-    if (err == hipSuccess && xbits_done) *xbits_done = a.xb_on != 0;
-    return (int)err;
+    return (int)hipGetLastError();
 }
 
 uint32_t solve_lds_e_max() {
