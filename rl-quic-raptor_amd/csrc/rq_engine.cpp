@@ -161,6 +161,10 @@ struct Workspace {
     // never synchronises the device while the context lock is held
     hipEvent_t last = nullptr;
     int mark(void* stream) {
+#ifdef RQHIP_EXPERIMENTS
+        static const bool nomark = std::getenv("RQHIP_NOMARK") != nullptr;  // timing only: what the markers cost
+        if (nomark) return RQ_OK;
+#endif
         if (!last && hipEventCreateWithFlags(&last, internal_event_flags()) != hipSuccess) {
             last = nullptr;
             return fail(RQ_ERR_DEVICE, "hipEventCreate failed");
