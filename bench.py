@@ -117,6 +117,15 @@ def erasure_pattern(K, N, n_blocks, n_erase, seed):
     return er, rep
 
 
+def sample_steps(steps):
+    """The timed steps that carry timing events: every fourth from the second (at least two when there
+    are two steps or more), so that most steps run without the events' markers."""
+    s = [i for i in range(steps) if i % 4 == 1]
+    if len(s) < 2:
+        s = [i for i in range(steps) if i % 2 == 1][:2]
+    return s or [0]
+
+
 def pmc_traffic(kernel, K, T, N, B):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary of this exact
     workload (profiles/rNN_traffic.json, written by tools/gpu_profile.sh); (None, None) if absent."""
@@ -356,7 +365,7 @@ def run_config2(args):
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
-    sampled = [s for s in range(args.steps) if s % 2 == 1] or [0]  # timing events on a sample (config 3)
+    sampled = sample_steps(args.steps)  # timing events on a sample (as config 3)
     ev = {s: tuple(torch.cuda.Event(enable_timing=True) for _ in range(2)) for s in sampled}
     rqhip.launch_time(reset=True)
     t0 = time.perf_counter()
@@ -568,10 +577,10 @@ def main():
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
-    # Timing events on every other timed step (from the second): the stream markers and the
+    # Timing events on every fourth timed step (from the second): the stream markers and the
     # dispatch-recorded events of rq_launch_timing add ~1 % each to a step they bracket
-    # (profiles/r03_dense/r03tb, r03f), so the other half run as a caller would run them.
-    sampled = [s for s in range(args.steps) if s % 2 == 1] or [0]
+    # (profiles/r03_dense/r03tb, r03f), so the other steps run as a caller would run them.
+    sampled = sample_steps(args.steps)
     ev = {s: tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for s in sampled}
     rqhip.launch_time(reset=True)
     t0 = time.perf_counter()

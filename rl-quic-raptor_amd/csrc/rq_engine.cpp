@@ -160,6 +160,9 @@ struct Workspace {
     // an evicted or released workspace is freed once it has completed (DevCtx::reap), so eviction
     // never synchronises the device while the context lock is held
     hipEvent_t last = nullptr;
+    // the event that currently marks this workspace's last use: `last`, or a decode call's up[set]
+    // recorded after its downloads (one marker per call instead of two)
+    hipEvent_t done = nullptr;
     int mark(void* stream) {
 #ifdef RQHIP_EXPERIMENTS
         static const bool nomark = std::getenv("RQHIP_NOMARK") != nullptr;  // timing only: what the markers cost
@@ -170,9 +173,10 @@ struct Workspace {
             return fail(RQ_ERR_DEVICE, "hipEventCreate failed");
         }
         if (hipEventRecord(last, (hipStream_t)stream) != hipSuccess) return fail(RQ_ERR_DEVICE, "hipEventRecord failed");
+        done = last;
         return RQ_OK;
     }
-    bool idle() const { return !last || hipEventQuery(last) != hipErrorNotReady; }
+    bool idle() const { return !done || hipEventQuery(done) != hipErrorNotReady; }
     ~Workspace() {
         if (last) (void)hipEventDestroy(last);
         for (hipEvent_t& e : up)
@@ -1458,21 +1462,23 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
         z.pack = w->pk.as<uint8_t>();
         if (launch_pack_rows(z, stream)) return fail(RQ_ERR_DEVICE, "k_pack_rows launch failed");
     }
-    // the last kernel that reads the staging is queued: `up` (no fence) before the downloads, so the
-    // stream's last command stays a copy whose completion makes its bytes visible to the host
+    // The downloads, then one event: `up` (the staging's readers are done; recorded after the downloads,
+    // which is later than needed) doubles as the workspace's last-use marker (`done`).  Without zero
+    // copy `up` was recorded after the upload and the call marks `last` as before.  (Two markers per call
+    // measured ~2.5 us each between the kernels, profiles/r05_solve.)
+    if (po) HIP_TRY(hipMemcpyAsync(w->h_pack.p, w->pk.p, pack_bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
+    HIP_TRY(hipMemcpyAsync(async ? (void*)status : w->h_status.p, dst_status, n_blocks * 4, hipMemcpyDeviceToHost,
+                           (hipStream_t)stream));
     if (zero_copy) {
         HIP_TRY(hipEventRecord(w->up[set], (hipStream_t)stream));
         up_guard.armed = false;
-    }
-    if (po) HIP_TRY(hipMemcpyAsync(w->h_pack.p, w->pk.p, pack_bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
-    if (async) {  // statuses land in the caller's pinned array when the stream gets here
-        HIP_TRY(hipMemcpyAsync(status, dst_status, n_blocks * 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
         mark_guard.armed = false;
-        return w->mark(stream);
+        w->done = w->up[set];
+    } else {
+        mark_guard.armed = false;
+        if ((rc = w->mark(stream))) return rc;
     }
-    HIP_TRY(hipMemcpyAsync(w->h_status.p, dst_status, n_blocks * 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
-    mark_guard.armed = false;
-    if ((rc = w->mark(stream))) return rc;
+    if (async) return RQ_OK;  // statuses land in the caller's pinned array when the stream gets here
     if (fin == Fin::Deferred) return RQ_OK;  // decode_collect after the caller's stream sync
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
     decode_collect(w, blk_map, eoff, T, status, po);
