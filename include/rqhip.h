@@ -249,7 +249,8 @@ uint32_t rq_debug_apply_mode(uint32_t mode);
  * mode (values > 1 leave it) and returns the previous one; both give the same X. */
 uint32_t rq_debug_solve_mode(uint32_t mode);
 /* The register-table apply kernel's assembly for shape (KC outputs per wave, groups of G syndromes,
- * loads PDG groups ahead, CPL dword columns per lane): copied into text (cap bytes, NUL-terminated) when given, its length in
+ * loads PDG groups ahead, CPL dword columns per lane in bits 7:0 of cpl, two subset numbers per index
+ * dword when bit 8 is set): copied into text (cap bytes, NUL-terminated) when given, its length in
  * *text_len, and, when code_bytes is given, assembled in process (its code object size). */
 int rq_debug_apply_gi_asm(uint32_t kc, uint32_t g, uint32_t pdg, uint32_t cpl, char* text, size_t cap, size_t* text_len,
                           size_t* code_bytes);

@@ -43,8 +43,8 @@ struct Asm {
 }  // namespace
 
 bool gi_shape_ok(const GiShape& sh) {
-    return sh.KC >= 4 && sh.KC <= 16 && sh.KC % 4 == 0 && sh.G >= 4 && sh.G <= 6 && sh.PDG >= 1 && sh.PDG <= 2 &&
-           sh.CPL >= 1 && sh.CPL <= 2 && gi_vgprs(sh) <= 256;
+    return sh.KC >= 4 && sh.KC <= 16 && sh.KC % (sh.PACK ? 8 : 4) == 0 && sh.G >= 4 && sh.G <= 6 && sh.PDG >= 1 &&
+           sh.PDG <= 2 && sh.CPL >= 1 && sh.CPL <= 2 && sh.PACK <= 1 && gi_vgprs(sh) <= 256;
 }
 
 // VGPRs: v0 lane (prologue only), v1 the lane's byte offset in a row (column c at + 256 c), the syndrome
@@ -59,13 +59,13 @@ uint32_t gi_vgprs(const GiShape& sh) { return gi_tb(sh) + sh.CPL * ((1u << sh.G)
 
 std::string gi_kernel_name(const GiShape& sh) {
     return "rq_apply_gi_k" + std::to_string(sh.KC) + "_g" + std::to_string(sh.G) + "_p" + std::to_string(sh.PDG) +
-           "_c" + std::to_string(sh.CPL) + (sh.diag ? "_d" + std::to_string(sh.diag) : std::string());
+           "_c" + std::to_string(sh.CPL) + (sh.PACK ? "_x2" : "") + (sh.diag ? "_d" + std::to_string(sh.diag) : std::string());
 }
 
 std::string emit_apply_gi_asm(const GiShape& sh) {
     const uint32_t KC = sh.KC, G = sh.G, PDG = sh.PDG, CPL = sh.CPL, NT = 1u << G;
     const uint32_t RING = 2, TB = gi_tb(sh), AC = TB + CPL * NT, NV = gi_vgprs(sh);
-    const uint32_t PAIRS = KC / 4;                       // 32 index dwords per pair of 16-dword pieces
+    const uint32_t PK = sh.PACK, PAIRS = PK ? KC / 8 : KC / 4;  // 32 index dwords per pair of 16-dword pieces
     const uint32_t UNR = (PDG * PAIRS) % 2 ? 2 * PDG : PDG;  // groups per loop body: ring slots, and pieces A/B alternate
     const std::string kname = gi_kernel_name(sh);
     auto RA = [&](uint32_t c, uint32_t p, uint32_t t) { return RING + (c * PDG + p) * 2 * G + t; };
@@ -228,10 +228,17 @@ std::string emit_apply_gi_asm(const GiShape& sh) {
             }
             if (sh.diag & 4) continue;
             for (uint32_t q = 0; q < 32; ++q) {
-                const uint32_t k = 4 * j + q / 8, b = q % 8;
+                // unpacked: dword q = output 4j + q / 8, bit q % 8; packed: output 8j + q / 4, bits 2 (q % 4) + 0, 1
+                const uint32_t k = PK ? 8 * j + q / 4 : 4 * j + q / 8, b = PK ? 2 * (q % 4) : q % 8;
                 if (j == 0 && q == 0) a.f("s_set_gpr_idx_on s%u, gpr_idx(SRC0)", cur + q);
                 else a.f("s_set_gpr_idx_idx s%u", cur + q);
                 for (uint32_t c = 0; c < CPL; ++c) a.f("v_xor_b32_e32 v%u, v%u, v%u", ACC(c, k, b), TBC(c), ACC(c, k, b));
+                if (PK) {  // the high half: S0[7:0] after the shift (the idx instruction reads only bits 7:0)
+                    a.f("s_lshr_b32 s%u, s%u, 16", cur + q, cur + q);
+                    a.f("s_set_gpr_idx_idx s%u", cur + q);
+                    for (uint32_t c = 0; c < CPL; ++c)
+                        a.f("v_xor_b32_e32 v%u, v%u, v%u", ACC(c, k, b + 1), TBC(c), ACC(c, k, b + 1));
+                }
             }
         }
         if (!(sh.diag & 4)) a.line("s_set_gpr_idx_off");

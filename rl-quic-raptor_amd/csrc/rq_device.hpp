@@ -49,6 +49,7 @@ __host__ __device__ inline uint32_t x_stride(uint32_t e) { return 64u * ((e + 63
 struct GiShape {
     uint32_t KC = 8, G = 5, PDG = 2;
     uint32_t CPL = 1;   // dword columns per lane (64-column strips per wave), 1 or 2
+    uint32_t PACK = 0;  // 1: two subset numbers per index dword (the high one by s_lshr_b32)
     uint32_t diag = 0;  // experiments (timing only, wrong bytes): 1 no index loads, 2 no syndrome loads, 4 no lookups
 };
 
@@ -74,7 +75,7 @@ __host__ __device__ inline GiLayout gi_layout(uint32_t max_e, const GiShape& s) 
     L.er = 16;
     L.of = L.er + 16 * L.nslm;
     L.ix = L.of + 16 * (L.ngrm + s.PDG + 1);
-    L.ix_slice = 8 * s.KC * L.ngrm;
+    L.ix_slice = (s.PACK ? 4 : 8) * s.KC * L.ngrm;
     L.block = L.ix + L.nslm * L.ix_slice;
     return L;
 }

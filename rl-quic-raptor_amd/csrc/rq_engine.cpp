@@ -1162,10 +1162,10 @@ const GiShape& apply_gi_shape() {
     static const GiShape sh = [] {
         GiShape g;
         if (const char* e = knob("RQHIP_APPLY_GI")) {
-            unsigned kc = 0, gg = 0, pd = 0, cpl = 1;
-            if (std::sscanf(e, "%u,%u,%u,%u", &kc, &gg, &pd, &cpl) >= 3) {
+            unsigned kc = 0, gg = 0, pd = 0, cpl = 1, pk = 0;
+            if (std::sscanf(e, "%u,%u,%u,%u,%u", &kc, &gg, &pd, &cpl, &pk) >= 3) {
                 GiShape t;
-                t.KC = kc; t.G = gg; t.PDG = pd; t.CPL = cpl;
+                t.KC = kc; t.G = gg; t.PDG = pd; t.CPL = cpl; t.PACK = pk;
                 if (gi_shape_ok(t)) g = t;
             }
         }
@@ -1178,7 +1178,7 @@ const GiShape& apply_gi_shape() {
 // The apply kernel of this device, assembled (amd_comgr, in process) on first use.  Caller holds ctx->mu.
 int get_gi_kernel(DevCtx* ctx, const GiShape& sh, hipFunction_t* fn) {
     if (ctx->gi_fn && ctx->gi_shape.KC == sh.KC && ctx->gi_shape.G == sh.G && ctx->gi_shape.PDG == sh.PDG &&
-        ctx->gi_shape.CPL == sh.CPL && ctx->gi_shape.diag == sh.diag) {
+        ctx->gi_shape.CPL == sh.CPL && ctx->gi_shape.PACK == sh.PACK && ctx->gi_shape.diag == sh.diag) {
         *fn = ctx->gi_fn;
         return RQ_OK;
     }
@@ -1401,7 +1401,8 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     // 17.6 us against 4.7 + 8.5 us for k_solve and k_xbits apart (256 LDS-heavy workgroups, four blocks
     // each, one after another).
     const GiShape shipped;
-    s.xb_on = gi && max_e && gsh.KC == shipped.KC && gsh.G == shipped.G && gsh.PDG == shipped.PDG ? 1u : 0u;
+    s.xb_on = gi && max_e && gsh.KC == shipped.KC && gsh.G == shipped.G && gsh.PDG == shipped.PDG &&
+                      gsh.PACK == shipped.PACK ? 1u : 0u;
     s.xb = xa;
     bool xbits_done = false;
     if (launch_solve(s, nw, need_general, wide, max_lds_e, beside ? (void*)w->cs : stream, &xbits_done))
@@ -2343,8 +2344,9 @@ uint32_t rq_debug_virtual_shards(uint32_t n) {
 int rq_debug_apply_gi_asm(uint32_t kc, uint32_t g, uint32_t pdg, uint32_t cpl, char* text, size_t cap, size_t* text_len,
                           size_t* code_bytes) {
     GiShape sh;
-    sh.KC = kc; sh.G = g; sh.PDG = pdg; sh.CPL = cpl;
-    if (!gi_shape_ok(sh)) return fail(RQ_ERR_BAD_ARG, "apply shape: KC 4..16 (a multiple of 4), G 4..6, PDG 1..2, CPL 1..2, <= 256 VGPRs");
+    sh.KC = kc; sh.G = g; sh.PDG = pdg; sh.CPL = cpl & 0xff; sh.PACK = cpl >> 8;
+    if (!gi_shape_ok(sh))
+        return fail(RQ_ERR_BAD_ARG, "apply shape: KC 4..16 (a multiple of 4, of 8 packed), G 4..6, PDG 1..2, CPL 1..2, <= 256 VGPRs");
     const std::string src = emit_apply_gi_asm(sh);
     if (text_len) *text_len = src.size();
     if (text && cap) {

@@ -98,7 +98,7 @@ int launch_pack_rows(const PackArgs& a, void* stream) {
 // Block bi's part of the stream from X given as X(k, m) (coefficient byte of syndrome m in output k) and
 // XP(m) (the received row, within the block, of syndrome m); nthr threads from tid.  An unsolved block
 // (solved = false) gets its header only.
-template <int KC, int G, int PDG, class XF, class PF>
+template <int KC, int G, int PDG, class XF, class PF, int PK = 0>
 __device__ void gi_stream(const XbitsArgs& a, uint32_t bi, uint32_t b, uint32_t e, bool solved, uint32_t tid,
                           uint32_t nthr, XF X, PF XP) {
     const GiLayout& L = a.L;
@@ -148,43 +148,55 @@ __device__ void gi_stream(const XbitsArgs& a, uint32_t bi, uint32_t b, uint32_t 
             for (int t = 0; t < G; ++t) sb |= ((x[t] >> bit) & 1u) << t;
             v[bit] = sb;
         }
-        uint4* d = reinterpret_cast<uint4*>(base + L.ix + sl * L.ix_slice + g * 8 * KC + k * 8);
-        d[0] = make_uint4(v[0], v[1], v[2], v[3]);
-        d[1] = make_uint4(v[4], v[5], v[6], v[7]);
+        if (PK) {  // two per dword: bits b = 2i (low half) and 2i + 1 (high half)
+            uint4* d = reinterpret_cast<uint4*>(base + L.ix + sl * L.ix_slice + g * 4 * KC + k * 4);
+            d[0] = make_uint4(v[0] | v[1] << 16, v[2] | v[3] << 16, v[4] | v[5] << 16, v[6] | v[7] << 16);
+        } else {
+            uint4* d = reinterpret_cast<uint4*>(base + L.ix + sl * L.ix_slice + g * 8 * KC + k * 8);
+            d[0] = make_uint4(v[0], v[1], v[2], v[3]);
+            d[1] = make_uint4(v[4], v[5], v[6], v[7]);
+        }
     }
 }
 
-template <int KC, int G, int PDG>
+template <int KC, int G, int PDG, int PK = 0>
 __device__ void xbits_block(const XbitsArgs& a, uint32_t bi, uint32_t tid) {
     const uint32_t b = a.blk_map[bi];
     const uint32_t e = a.erased_off[b + 1] - a.erased_off[b];
     const uint8_t* xc = a.xcoef + 64ull * a.xoff[bi];
     const uint32_t xs = x_stride(e);
     const uint16_t* xp = a.xpiv + a.erased_off[b];
-    gi_stream<KC, G, PDG>(a, bi, b, e, a.status[b] == 1, tid, 256, [&](uint32_t k, uint32_t m) { return xc[(size_t)m * xs + k]; },
-                          [&](uint32_t m) { return (uint32_t)xp[m]; });
+    auto X = [&](uint32_t k, uint32_t m) { return xc[(size_t)m * xs + k]; };
+    auto P = [&](uint32_t m) { return (uint32_t)xp[m]; };
+    gi_stream<KC, G, PDG, decltype(X), decltype(P), PK>(a, bi, b, e, a.status[b] == 1, tid, 256, X, P);
 }
 
-template <int KC, int G, int PDG>
+template <int KC, int G, int PDG, int PK = 0>
 __global__ void __launch_bounds__(256) k_xbits(XbitsArgs a) {
-    xbits_block<KC, G, PDG>(a, blockIdx.x, threadIdx.x);
+    xbits_block<KC, G, PDG, PK>(a, blockIdx.x, threadIdx.x);
 }
 
 int launch_xbits(const XbitsArgs& a, uint32_t n_blocks, const GiShape& s, void* stream) {
     if (!n_blocks) return 0;
     const hipStream_t st = (hipStream_t)stream;
 #define RQ_XB(kc, g, p)                                                                                   \
-    if (s.KC == kc && s.G == g && s.PDG == p) {                                                           \
+    if (s.KC == kc && s.G == g && s.PDG == p && !s.PACK) {                                                \
         hipLaunchKernelGGL((k_xbits<kc, g, p>), dim3(n_blocks), dim3(256), 0, st, a);                     \
+        return (int)hipGetLastError();                                                                    \
+    }
+#define RQ_XBP(kc, g, p)                                                                                  \
+    if (s.KC == kc && s.G == g && s.PDG == p && s.PACK) {                                                 \
+        hipLaunchKernelGGL((k_xbits<kc, g, p, 1>), dim3(n_blocks), dim3(256), 0, st, a);                  \
         return (int)hipGetLastError();                                                                    \
     }
     RQ_XB(8, 5, 2)
 #ifdef RQHIP_EXPERIMENTS
     RQ_XB(16, 6, 1) RQ_XB(16, 6, 2) RQ_XB(16, 5, 2) RQ_XB(8, 6, 2) RQ_XB(8, 5, 1) RQ_XB(8, 4, 1) RQ_XB(16, 4, 2)
     RQ_XB(8, 4, 2) RQ_XB(8, 6, 1) RQ_XB(12, 5, 1) RQ_XB(12, 5, 2) RQ_XB(4, 5, 1) RQ_XB(4, 4, 1) RQ_XB(4, 5, 2)
-    RQ_XB(12, 4, 2) RQ_XB(16, 5, 1)
+    RQ_XB(12, 4, 2) RQ_XB(16, 5, 1) RQ_XBP(8, 5, 2) RQ_XBP(8, 5, 1) RQ_XBP(16, 5, 2) RQ_XBP(8, 6, 2)
 #endif
 #undef RQ_XB
+#undef RQ_XBP
     return (int)hipErrorInvalidValue;
 }
 

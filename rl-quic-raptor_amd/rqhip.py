@@ -388,9 +388,10 @@ def assemble(text):
     return n.value
 
 
-def apply_gi_asm(kc=8, g=5, pdg=2, cpl=1, assemble=True):
+def apply_gi_asm(kc=8, g=5, pdg=2, cpl=1, pack=0, assemble=True):
     """rq_debug_apply_gi_asm: (assembly text, code object size or None) of the register-table apply kernel."""
     n = ctypes.c_size_t(0)
+    cpl |= pack << 8
     _check(lib().rq_debug_apply_gi_asm(kc, g, pdg, cpl, None, 0, ctypes.byref(n), None))
     buf = ctypes.create_string_buffer(n.value + 1)
     co = ctypes.c_size_t(0)

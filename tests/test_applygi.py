@@ -10,7 +10,7 @@ import pytest
 import rqhip
 
 SHAPES = [(8, 5, 2, 1), (8, 5, 1, 1), (8, 4, 1, 1), (8, 6, 2, 1), (12, 5, 2, 1), (16, 6, 2, 1), (4, 4, 1, 2),
-          (8, 5, 1, 2)]
+          (8, 5, 1, 2), (8, 5, 2, 1, 1), (16, 5, 2, 1, 1), (8, 5, 1, 2, 1)]
 
 
 def _vgprs(text):
@@ -21,7 +21,7 @@ def _vgprs(text):
 def test_shapes_assemble(shape):
     text, code = rqhip.apply_gi_asm(*shape)
     assert code > 0
-    kc, g, pdg, cpl = shape
+    g = shape[1]
     nv = _vgprs(text)
     # the index mode reads v[table + idx] with idx < 2^G: every table register is allocated
     tables = [int(m) for m in re.findall(r"v_xor_b32_e32 v\d+, v(\d+), v\d+\n\ts_set_gpr_idx", text)]
@@ -48,7 +48,7 @@ def test_shipped_shape_occupancy():
 
 
 def test_bad_shapes_refused():
-    for shape in ((6, 5, 2, 1), (8, 7, 2, 1), (8, 5, 3, 1), (8, 5, 2, 3), (16, 6, 2, 2)):
+    for shape in ((6, 5, 2, 1), (8, 7, 2, 1), (8, 5, 3, 1), (8, 5, 2, 3), (16, 6, 2, 2), (4, 4, 1, 1, 1), (12, 5, 2, 1, 1)):
         with pytest.raises(rqhip.RaptorQError):
             rqhip.apply_gi_asm(*shape)
 
