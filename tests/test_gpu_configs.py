@@ -175,3 +175,49 @@ def test_k2048_t1200_matches_oracle(gpu, rq):
         jobs.append((K, T, recv))
     for b, (ok, payload) in zip((3, 30), _oracle_map("oracle_decode", jobs)):
         assert ok and payload == src_h[b].tobytes(), "block %d" % b
+
+
+def test_config3_zero_overhead_statuses_match_oracle(gpu, rq):
+    """Config 3's full batch received with no overhead (55 of 1 100 symbols lost, exactly K received:
+    the surviving sources and the first repairs that cover the erasures), so some blocks are
+    rank-deficient (~0.4 % at K=1024).  The GPU's status of every rank-deficient block and of 16
+    decodable ones against the oracle decoder on the same received symbols (ok flag; payload where
+    ok); every decodable block equals its source."""
+    K, T, N, nb = 1024, 1200, 1100, 1024
+    esis = list(range(K, N))
+    src = _src(gpu, nb, K, T, 6)
+    out = _encode(rq, gpu, src, K, T, esis)
+    rng = np.random.default_rng(61)
+    er, rl = [], []
+    for _ in range(nb):
+        lost = set(rng.choice(N, 55, replace=False).tolist())
+        er.append(sorted(i for i in lost if i < K))
+        rl.append([e for e in range(K, N) if e not in lost][:len(er[-1])])
+    assert all(len(r) == len(e) for e, r in zip(er, rl))
+    bi = torch.tensor([b for b in range(nb) for _ in rl[b]], device=gpu, dtype=torch.long)
+    ri = torch.tensor([e - K for b in range(nb) for e in rl[b]], device=gpu, dtype=torch.long)
+    rep = out.view(nb, N - K, T)[bi, ri].contiguous()
+    data = src.clone()
+    eb = torch.tensor([b for b in range(nb) for _ in er[b]], device=gpu, dtype=torch.long)
+    ei = torch.tensor([i for b in range(nb) for i in er[b]], device=gpu, dtype=torch.long)
+    data.view(nb, K, T)[eb, ei] = 0xA5
+    st = rq.DecodeBatch(K, T, er, rl).run(data, rep)
+    torch.cuda.synchronize()
+    assert set(np.unique(st).tolist()) <= {0, 1}
+    good = torch.tensor(st == 1, device=gpu)
+    assert torch.equal(data[good], src[good])
+    src_h = src.cpu().numpy()
+    out_h = out.view(nb, N - K, T).cpu().numpy()
+    failed = [b for b in range(nb) if st[b] == 0]
+    assert len(failed) < 40, len(failed)  # ~4 expected
+    ok_blocks = [b for b in range(nb) if st[b] == 1]
+    sample = failed + ok_blocks[:: max(1, len(ok_blocks) // 16)][:16]
+    jobs = []
+    for b in sample:
+        recv = {i: src_h[b, i * T:(i + 1) * T].tobytes() for i in range(K) if i not in set(er[b])}
+        recv.update({e: out_h[b, e - K].tobytes() for e in rl[b]})
+        jobs.append((K, T, recv))
+    for b, (ok, payload) in zip(sample, _oracle_map("oracle_decode", jobs)):
+        assert bool(ok) == (st[b] == 1), "block %d: GPU status %d, oracle ok %s" % (b, st[b], ok)
+        if ok:
+            assert payload == src_h[b].tobytes(), "block %d" % b
