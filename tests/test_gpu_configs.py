@@ -17,6 +17,7 @@ import rqcpu  # noqa: E402
 import rqshard  # noqa: E402
 
 THREADS = min(16, os.cpu_count() or 1)
+ZERO_OVERHEAD_DEFICIENT = [433, 567, 868]
 
 
 def _src(gpu, n_blocks, K, T, seed):
@@ -209,7 +210,10 @@ def test_config3_zero_overhead_statuses_match_oracle(gpu, rq):
     src_h = src.cpu().numpy()
     out_h = out.view(nb, N - K, T).cpu().numpy()
     failed = [b for b in range(nb) if st[b] == 0]
-    assert len(failed) < 40, len(failed)  # ~4 expected
+    print("zero-overhead config 3: %d rank-deficient blocks: %s" % (len(failed), failed))
+    # rank deficiency depends only on the received ESIs (seed 61's pattern), not on the data: the same
+    # three blocks as the oracle decoder finds on CPU (tests/test_zero_overhead_pattern.py)
+    assert failed == ZERO_OVERHEAD_DEFICIENT, failed
     ok_blocks = [b for b in range(nb) if st[b] == 1]
     sample = failed + ok_blocks[:: max(1, len(ok_blocks) // 16)][:16]
     jobs = []
