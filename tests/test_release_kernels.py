@@ -22,7 +22,7 @@ SHIPPED = {
     "rq::k_solve(rq::SolveArgs)",
     "rq::k_pack_rows(rq::PackArgs)",
     "rq::k_gather(rq::DevParams, unsigned char const*, unsigned int, unsigned int const*, unsigned int, unsigned char*)",
-    "void rq::k_xbits<8, 5, 2>(rq::XbitsArgs)",
+    "void rq::k_xbits<8, 5, 2, 0>(rq::XbitsArgs)",
     "void rq::k_solve_ip<4>(rq::SolveArgs)",
 } | {
     "void rq::k_apply<%d, %d, 2, %d, true>(rq::ApplyArgs, unsigned int, unsigned int, unsigned int)" % (kc, c, occ)
