@@ -202,11 +202,13 @@ def cpu_baseline(K, T, N, n_erase, n_blocks):
     engine's algorithm (the same column program evaluated in 64-byte strips; syndrome decode with
     AVX2 split-nibble GF(256) mul-adds, the reference's asmSSSE3MulAdd technique), on a bounded
     sample of the same workload: all cores of the process's share (host_cores, one block per thread at
-    a time) as the reported value, and 1 thread beside it.  The oracle is only the checker (tests)."""
+    a time) as the reported value, and 1 thread beside it; the oracle (the library's per-block algorithm
+    restated in C, oracle/) on one block beside both, as the reference's own CPU path."""
     threads, cores_src = host_cores()
     te1, td1 = cpu_run(K, T, N, n_erase, max(8, n_blocks // 8), 1, 4242)
     nb1 = max(8, n_blocks // 8)
     teN, tdN = cpu_run(K, T, N, n_erase, n_blocks, threads, 9000)
+    teO, tdO = oracle_run(K, T, N, n_erase, 4343)
     gb = lambda nb, t: round(nb * K * T / t / 1e9, 4)
     return {"value": gb(n_blocks, teN + tdN), "unit": "GB/s", "cores": threads, "cores_source": cores_src,
             "kind": "port",
@@ -217,7 +219,36 @@ def cpu_baseline(K, T, N, n_erase, n_blocks):
             "encode_gbs": gb(n_blocks, teN), "decode_gbs": gb(n_blocks, tdN),
             "one_thread": {"value": gb(nb1, te1 + td1), "cores": 1, "encode_gbs": gb(nb1, te1),
                            "decode_gbs": gb(nb1, td1), "sample": "%d blocks" % nb1},
+            "oracle_one_thread": {"value": gb(1, teO + tdO), "cores": 1, "encode_gbs": gb(1, teO),
+                                  "decode_gbs": gb(1, tdO),
+                                  "sample": "1 block: oracle/rq_oracle.c, the library's own algorithm restated (Solve "
+                                            "with inactivation and dense GF(256) elimination per block, RQ/solver.go)"},
             "reference_go_1core_gbs": 0.094}
+
+
+def oracle_run(K, T, N, n_erase, seed):
+    """One block through the oracle (the C restatement of the library's per-block algorithm, 1 thread):
+    encode of the N - K repairs, then a decode with n_erase of the N symbols lost; seconds each."""
+    from oracle import oracle as O
+    rng = np.random.default_rng(seed)
+    src = rng.integers(0, 256, K * T, dtype=np.uint8)
+    t0 = time.perf_counter()
+    enc = O.OracleEncoder(src.tobytes(), T)
+    rep = {e: enc.gen_symbol(e).tobytes() for e in range(K, N)}
+    te = time.perf_counter() - t0
+    lost = set(rng.choice(N, n_erase, replace=False).tolist())
+    t0 = time.perf_counter()
+    dec = O.OracleDecoder(K * T, T)
+    for i in range(K):
+        if i not in lost:
+            dec.add_symbol(i, src[i * T:(i + 1) * T].tobytes())
+    for e, row in rep.items():
+        if e not in lost:
+            dec.add_symbol(e, row)
+    ok, payload = dec.decode()
+    td = time.perf_counter() - t0
+    assert ok and payload == src.tobytes(), "oracle baseline decode mismatch"
+    return te, td
 
 
 def cpu_baseline_encode(K, T, esis, n_blocks):
