@@ -127,6 +127,9 @@ struct SolveArgs {
     // k_solve also writes the register-table apply's index stream (the shipped shape 8, 5, 2) when set
     uint32_t xb_on;
     XbitsArgs xb;
+    // k_solve (the last solver launch) also writes every block's final status here: the caller's pinned
+    // status array as the device sees it, so an async decode needs no status download (nullptr: none)
+    int32_t* host_status;
 };
 constexpr int32_t ST_PENDING = -100;   // queued for the solver
 constexpr int32_t ST_FALLBACK = -101;  // beyond the fast solvers: the general solver decides

@@ -1203,7 +1203,8 @@ int get_gi_kernel(DevCtx* ctx, const GiShape& sh, hipFunction_t* fn) {
 int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, void* data, uint64_t data_stride,
                 const std::vector<uint32_t>& eoff, const uint32_t* erased, const std::vector<uint32_t>& roff,
                 const uint32_t* repair_esi, const std::vector<uint32_t>& cnt, const std::vector<uint32_t>& blk_map,
-                const void* repair, int32_t* status, void* stream, PackOut* po, Fin fin, uint32_t mx_hint = 0) {
+                const void* repair, int32_t* status, void* stream, PackOut* po, Fin fin, uint32_t mx_hint = 0,
+                int32_t* status_dev = nullptr) {
     int rc;
     const bool async = fin == Fin::Async;
     DecodePlan& pl = decode_plan_scratch();
@@ -1404,6 +1405,11 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     s.xb_on = gi && max_e && gsh.KC == shipped.KC && gsh.G == shipped.G && gsh.PDG == shipped.PDG &&
                       gsh.PACK == shipped.PACK ? 1u : 0u;
     s.xb = xa;
+    // An async call whose status array the device can write (rq_decode_batch_async's pinned array) gets
+    // its statuses from k_solve, the last solver launch, instead of a download after the apply (a copy
+    // kernel and its gap, ~8 us per call).  Without the general solver the download stays.
+    const bool status_by_solver = async && status_dev && need_general && !po;
+    s.host_status = status_by_solver ? status_dev : nullptr;
     bool xbits_done = false;
     if (launch_solve(s, nw, need_general, wide, max_lds_e, beside ? (void*)w->cs : stream, &xbits_done))
         return fail(RQ_ERR_DEVICE, "k_solve launch failed");
@@ -1468,8 +1474,9 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     // copy `up` was recorded after the upload and the call marks `last` as before.  (Two markers per call
     // measured ~2.5 us each between the kernels, profiles/r05_solve.)
     if (po) HIP_TRY(hipMemcpyAsync(w->h_pack.p, w->pk.p, pack_bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
-    HIP_TRY(hipMemcpyAsync(async ? (void*)status : w->h_status.p, dst_status, n_blocks * 4, hipMemcpyDeviceToHost,
-                           (hipStream_t)stream));
+    if (!status_by_solver)
+        HIP_TRY(hipMemcpyAsync(async ? (void*)status : w->h_status.p, dst_status, n_blocks * 4, hipMemcpyDeviceToHost,
+                               (hipStream_t)stream));
     if (zero_copy) {
         HIP_TRY(hipEventRecord(w->up[set], (hipStream_t)stream));
         up_guard.armed = false;
@@ -1499,6 +1506,7 @@ struct DecodeJob {
     const uint32_t *erased = nullptr, *n_repair = nullptr, *repair_esi = nullptr;
     const void* repair = nullptr;
     int32_t* status = nullptr;
+    int32_t* status_dev = nullptr;  // async: the status array's device address (k_solve writes it)
     void* stream = nullptr;
     std::vector<uint32_t> eoff, roff, blk_map, cnt;
     uint32_t rmax = 0;        // the largest received repair ESI (decode_args)
@@ -1554,7 +1562,7 @@ int decode_begin(DevCtx* ctx, DecodeJob* j, const uint32_t* n_erased, PackOut* p
     if (rc || j->blk_map.empty()) return rc;
     const uint32_t n_blocks = j->n_blocks;
     return decode_pass(ctx, j->p, j->T, n_blocks, j->data, j->data_stride, j->eoff, j->erased, j->roff, j->repair_esi,
-                       j->cnt, j->blk_map, j->repair, j->status, j->stream, po, fin, decode_mx_hint(*j));
+                       j->cnt, j->blk_map, j->repair, j->status, j->stream, po, fin, decode_mx_hint(*j), j->status_dev);
 }
 
 // After a Sync pass (or a Deferred one and a sync of its stream): the all-repairs pass for the
@@ -1577,10 +1585,11 @@ int decode_finish(DevCtx* ctx, DecodeJob* j, PackOut* po, bool collect, const Ro
 int decode_locked(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, void* data, uint64_t data_stride,
                   const uint32_t* n_erased, const uint32_t* erased, const uint32_t* n_repair,
                   const uint32_t* repair_esi, const void* repair, int32_t* status, void* stream,
-                  PackOut* po = nullptr, Fin fin = Fin::Sync) {
+                  PackOut* po = nullptr, Fin fin = Fin::Sync, int32_t* status_dev = nullptr) {
     DecodeJob j;
     j.p = p; j.T = T; j.n_blocks = n_blocks; j.data = data; j.data_stride = data_stride; j.erased = erased;
     j.n_repair = n_repair; j.repair_esi = repair_esi; j.repair = repair; j.status = status; j.stream = stream;
+    j.status_dev = fin == Fin::Async ? status_dev : nullptr;
     int rc = decode_begin(ctx, &j, n_erased, po, fin);
     if (rc || fin == Fin::Async) return rc;
     return decode_finish(ctx, &j, po, false);
@@ -2428,8 +2437,10 @@ int rq_decode_batch_async(const rq_decode_desc* d) {
     CtxRef ctx;
     if ((rc = get_ctx(&ctx))) return rc;
     std::lock_guard<std::mutex> lk(ctx->mu);
+    // the device's view of the pinned status array (k_solve writes the final statuses straight into it)
+    int32_t* status_dev = static_cast<int32_t*>(pa.devicePointer);
     return decode_locked(ctx, p, d->T, d->n_blocks, d->data, d->data_stride, d->n_erased, d->erased, d->n_repair,
-                         d->repair_esi, d->repair, d->status, d->stream, nullptr, Fin::Async);
+                         d->repair_esi, d->repair, d->status, d->stream, nullptr, Fin::Async, status_dev);
 }
 
 int rq_encode_batch_host(const rq_encode_desc* d, uint32_t device_mask) {

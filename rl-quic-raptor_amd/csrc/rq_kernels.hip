@@ -635,6 +635,13 @@ __global__ void __launch_bounds__(256) k_solve(SolveArgs a) {
     }
     __syncthreads();  // the next block reuses the LDS
     }
+    if (a.host_status) {  // this pass's blocks are final now (solved above, or by an earlier solver)
+        const uint32_t bi = base + tid * gridDim.x;
+        if (tid < 256 && bi < a.n_map) {
+            const uint32_t b = a.blk_map[bi];
+            a.host_status[b] = a.status[b];
+        }
+    }
     __syncthreads();  // todo / ntodo are rewritten by the next pass
     }
 }
