@@ -984,6 +984,7 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
         "s_load_dwordx8 s[12:19], s[0:1], 0x20",
         "s_load_dwordx4 s[48:51], s[0:1], 0x40",
         "s_waitcnt lgkmcnt(0)",
+        "CPFETCH",
         "v_lshlrev_b32_e32 V_SCROFF, 2, v0",
         "v_add_u32_e32 V_LDS2, 0x10000, V_SCROFF",
         "s_mov_b32 s24, s4",
@@ -1038,8 +1039,41 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
         "v_mul_lo_u32 v4, v2, s11",
         "v_add_u32_e32 V_OUTOFF, v4, v3",
     };
+    const uint32_t W = std::max<uint32_t>(1, mp.wg_waves);
     auto put = [&](const char* p) {
         std::string l(p);
+        if (l == "CPFETCH") {
+            // Descriptor fetch (ColKernArgs::cp_*, a decode's syndrome launch): workgroups past the
+            // persistent grid (s2 >= n_wg = s49) copy their cp_chunk-byte piece of the descriptors from
+            // pinned host memory to the device, 16 bytes per lane per round trip, and exit.  They run on
+            // the SIMDs the grid leaves free, beside the program; the solve that reads the copy is the
+            // next kernel in the stream.  Vector loads and stores only.
+            line("s_cmp_lt_u32 s2, s49");
+            line("s_cbranch_scc1 .Ldmain");
+            line("s_load_dwordx4 s[56:59], s[0:1], 0x50");  // cp_src, cp_dst
+            line("s_load_dwordx2 s[60:61], s[0:1], 0x60");  // cp_bytes, cp_chunk
+            line("s_waitcnt lgkmcnt(0)");
+            line("s_sub_u32 s62, s2, s49");
+            line("s_mul_i32 s62, s62, s61");   // the piece's first byte
+            line("s_add_u32 s63, s62, s61");
+            line("s_min_u32 s63, s63, s60");   // its end
+            line("v_lshlrev_b32_e32 v1, 4, v0");
+            line("v_add_u32_e32 v1, s62, v1");
+            s += ".Ldcp:\n";
+            line("v_cmp_gt_u32_e32 vcc, s63, v1");
+            line("s_and_b64 exec, exec, vcc");
+            line("s_cbranch_execz .Ldcpend");
+            line("global_load_dwordx4 v[4:7], v1, s[56:57]");
+            line("s_waitcnt vmcnt(0)");
+            line("global_store_dwordx4 v1, v[4:7], s[58:59]");
+            std::snprintf(buf, sizeof buf, "v_add_u32_e32 v1, 0x%x, v1", 1024u * W);
+            line(buf);
+            line("s_branch .Ldcp");
+            s += ".Ldcpend:\n";
+            line("s_endpgm");
+            s += ".Ldmain:\n";
+            return;
+        }
         const std::pair<const char*, int> names[] = {
             {"V_SRCOFF", V_SRCOFF}, {"V_OUTOFF", V_OUTOFF}, {"V_SCROFF", V_SCROFF}, {"V_LDS2", rv.lds2}};
         for (const auto& nm : names)
@@ -1047,7 +1081,6 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
                 l.replace(at, std::strlen(nm.first), "v" + std::to_string(nm.second));
         line(l.c_str());
     };
-    const uint32_t W = std::max<uint32_t>(1, mp.wg_waves);
     const uint32_t LB = mp.n_lds_slots * 256u;  // LDS bytes per wave
     if (W == 1) {
         for (const char* p : pro_once) put(p);
@@ -1166,15 +1199,15 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
     s += "\t.section .rodata,\"a\",@progbits\n\t.p2align 6, 0x0\n\t.amdhsa_kernel " + kname + "\n";
     const std::string lds = std::to_string((mp.lds_base + mp.n_lds_slots) * 256u * W);
     s += "\t\t.amdhsa_group_segment_fixed_size " + lds + "\n\t\t.amdhsa_private_segment_fixed_size 0\n";
-    s += "\t\t.amdhsa_kernarg_size 80\n\t\t.amdhsa_user_sgpr_count 2\n";
+    s += "\t\t.amdhsa_kernarg_size 104\n\t\t.amdhsa_user_sgpr_count 2\n";
     s += "\t\t.amdhsa_user_sgpr_kernarg_segment_ptr 1\n\t\t.amdhsa_system_sgpr_workgroup_id_x 1\n";
     s += "\t\t.amdhsa_system_vgpr_workitem_id 0\n\t\t.amdhsa_next_free_vgpr " + std::to_string(n_regs) + "\n";
     s += "\t\t.amdhsa_next_free_sgpr " + std::to_string(ROW_WIN + 32) + "\n\t\t.amdhsa_accum_offset " + std::to_string(acc_off) +
          "\n\t\t.amdhsa_reserve_vcc 0\n";
     s += "\t\t.amdhsa_ieee_mode 0\n\t\t.amdhsa_dx10_clamp 0\n\t.end_amdhsa_kernel\n\t.text\n";
     s += "\t.amdgpu_metadata\n---\namdhsa.kernels:\n  - .agpr_count: " + std::to_string(n_regs - acc_off) + "\n    .args:\n";
-    s += "      - .offset: 0\n        .size: 80\n        .value_kind: by_value\n";
-    s += "    .group_segment_fixed_size: " + lds + "\n    .kernarg_segment_align: 8\n    .kernarg_segment_size: 80\n";
+    s += "      - .offset: 0\n        .size: 104\n        .value_kind: by_value\n";
+    s += "    .group_segment_fixed_size: " + lds + "\n    .kernarg_segment_align: 8\n    .kernarg_segment_size: 104\n";
     s += "    .max_flat_workgroup_size: " + std::to_string(64 * W) + "\n    .name: " + kname + "\n    .private_segment_fixed_size: 0\n";
     s += "    .sgpr_count: " + std::to_string(ROW_WIN + 32) + "\n    .symbol: " + kname + ".kd\n    .vgpr_count: " + std::to_string(n_regs) +
          "\n    .wavefront_size: 64\n";

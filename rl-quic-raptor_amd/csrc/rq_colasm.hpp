@@ -139,8 +139,13 @@ struct ColKernArgs {
     uint32_t n_wg;        // persistent grid size (workgroups): workgroup g takes iterations g, g + n_wg, ...
                           // and its wave w the item iteration * W + w
     uint64_t row_off;     // uint32 table: soffset of the program's j-th source load (colprog_src_rows[j] * T)
+    // descriptor fetch (a decode's syndrome launch): workgroups n_wg, n_wg + 1, ... copy cp_bytes (a
+    // multiple of 16) from cp_src (pinned host memory) to cp_dst, cp_chunk bytes each, and exit
+    uint64_t cp_src;
+    uint64_t cp_dst;
+    uint32_t cp_bytes, cp_chunk;
 };
-static_assert(sizeof(ColKernArgs) == 80, "kernarg layout");
+static_assert(sizeof(ColKernArgs) == 104, "kernarg layout");
 
 std::string emit_colprog_asm(const MProg& mp, const std::string& kname);
 // Source rows of the program's buffer loads in issue order (the kernel's row_off table is these

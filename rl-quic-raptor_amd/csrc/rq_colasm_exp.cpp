@@ -327,15 +327,15 @@ std::string emit_pair_asm(const PairProg& pp, const std::string& kname) {
     s += "\t.section .rodata,\"a\",@progbits\n\t.p2align 6, 0x0\n\t.amdhsa_kernel " + kname + "\n";
     const std::string lds = std::to_string(pair_lds_bytes(pp));
     s += "\t\t.amdhsa_group_segment_fixed_size " + lds + "\n\t\t.amdhsa_private_segment_fixed_size 0\n";
-    s += "\t\t.amdhsa_kernarg_size 80\n\t\t.amdhsa_user_sgpr_count 2\n";
+    s += "\t\t.amdhsa_kernarg_size 104\n\t\t.amdhsa_user_sgpr_count 2\n";
     s += "\t\t.amdhsa_user_sgpr_kernarg_segment_ptr 1\n\t\t.amdhsa_system_sgpr_workgroup_id_x 1\n";
     s += "\t\t.amdhsa_system_vgpr_workitem_id 0\n\t\t.amdhsa_next_free_vgpr " + std::to_string(n_regs) + "\n";
     s += "\t\t.amdhsa_next_free_sgpr " + std::to_string(ROW_WIN + 32) + "\n\t\t.amdhsa_accum_offset " + std::to_string(acc_off) +
          "\n\t\t.amdhsa_reserve_vcc 0\n";
     s += "\t\t.amdhsa_ieee_mode 0\n\t\t.amdhsa_dx10_clamp 0\n\t.end_amdhsa_kernel\n\t.text\n";
     s += "\t.amdgpu_metadata\n---\namdhsa.kernels:\n  - .agpr_count: " + std::to_string(n_regs - acc_off) + "\n    .args:\n";
-    s += "      - .offset: 0\n        .size: 80\n        .value_kind: by_value\n";
-    s += "    .group_segment_fixed_size: " + lds + "\n    .kernarg_segment_align: 8\n    .kernarg_segment_size: 80\n";
+    s += "      - .offset: 0\n        .size: 104\n        .value_kind: by_value\n";
+    s += "    .group_segment_fixed_size: " + lds + "\n    .kernarg_segment_align: 8\n    .kernarg_segment_size: 104\n";
     s += "    .max_flat_workgroup_size: 128\n    .name: " + kname + "\n    .private_segment_fixed_size: 0\n";
     s += "    .sgpr_count: " + std::to_string(ROW_WIN + 32) + "\n    .symbol: " + kname + ".kd\n    .vgpr_count: " + std::to_string(n_regs) +
          "\n    .wavefront_size: 64\n";

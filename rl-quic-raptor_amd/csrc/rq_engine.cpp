@@ -764,8 +764,16 @@ bool xcd_order() {
 }
 
 // Run a column program over n_blocks device-resident blocks.  Caller holds ctx->mu.
+// A decode's descriptor fetch riding on its syndrome launch (ColKernArgs::cp_*): bytes (a multiple of 16)
+// from pinned host memory to the device.
+struct DescFetch {
+    const void* src = nullptr;  // the device's address of the pinned staging
+    void* dst = nullptr;
+    uint32_t bytes = 0;
+};
+
 int launch_col(DevCtx* ctx, ColKernel* k, uint32_t T, uint32_t n_blocks, const void* src, uint64_t src_stride,
-               void* out, uint64_t out_stride, void* stream) {
+               void* out, uint64_t out_stride, void* stream, const DescFetch* df = nullptr) {
     if (T < 8 || T % 4) return fail(RQ_ERR_BAD_ARG, "device-resident symbols: T must be a multiple of 4, at least 8");
     if (n_blocks == 0) return RQ_OK;
     if (!k->dma4_rows.empty() && (T % 16 || src_stride % 16 || (uintptr_t)src % 16))
@@ -839,6 +847,18 @@ int launch_col(DevCtx* ctx, ColKernel* k, uint32_t T, uint32_t n_blocks, const v
         const uint32_t wgs = std::min(resident, ((iters + rounds - 1) / rounds + 7) / 8 * 8);
         a.n_items = iters;
         a.n_wg = wgs;
+        // the descriptor fetch rides on the first launch: up to the SIMDs the grid leaves free (64 at
+        // K=1024 x 1 024 blocks), at least one workgroup, 1 KiB per wave per round trip
+        uint32_t n_cp = 0;
+        if (df && df->bytes && b0 == 0) {
+            const uint32_t free_wg = resident > wgs ? resident - wgs : 0u;
+            const uint32_t per_wg = 1024u * Wg;
+            n_cp = std::max<uint32_t>(1, std::min<uint32_t>(std::max<uint32_t>(free_wg, 1), (df->bytes + per_wg - 1) / per_wg));
+            a.cp_src = (uint64_t)(uintptr_t)df->src;
+            a.cp_dst = (uint64_t)(uintptr_t)df->dst;
+            a.cp_bytes = df->bytes;
+            a.cp_chunk = ((df->bytes + n_cp - 1) / n_cp + 15) & ~15u;
+        }
         if (xcd_order() && wgs % 8 == 0) {  // the remap needs the stride to keep g % 8 fixed
             a.xcd_q = iters / 8;
             a.xcd_n = a.xcd_q * 8;
@@ -855,12 +875,12 @@ int launch_col(DevCtx* ctx, ColKernel* k, uint32_t T, uint32_t n_blocks, const v
             }
             const auto& pr = ctx->tev[ctx->tev_used++];
             mg.armed = w != nullptr;
-            HIP_TRY(hipExtModuleLaunchKernel(k->fn, wgs * 64 * Wg, 1, 1, 64 * Wg, 1, 1, 0, (hipStream_t)stream, nullptr,
-                                             cfg, pr.first, pr.second, 0));
+            HIP_TRY(hipExtModuleLaunchKernel(k->fn, (wgs + n_cp) * 64 * Wg, 1, 1, 64 * Wg, 1, 1, 0, (hipStream_t)stream,
+                                             nullptr, cfg, pr.first, pr.second, 0));
             continue;
         }
         mg.armed = w != nullptr;
-        HIP_TRY(hipModuleLaunchKernel(k->fn, wgs, 1, 1, 64 * Wg, 1, 1, 0, (hipStream_t)stream, nullptr, cfg));
+        HIP_TRY(hipModuleLaunchKernel(k->fn, wgs + n_cp, 1, 1, 64 * Wg, 1, 1, 0, (hipStream_t)stream, nullptr, cfg));
     }
     mg.armed = false;
     return w ? w->mark(stream) : RQ_OK;
@@ -1242,14 +1262,19 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     // statuses alone go to the device); `up` then marks the end of the call's kernels.  Measured
     // 1-2 % faster per step than the in-stream copy (profiles/r02aa; RQHIP_DEC_ZC=0 restores it in
     // experiments builds).
-    // Descriptor mode (RQHIP_DEC_ZC in experiments builds): 2 = side-stream upload (the default), 1 =
-    // zero copy, 0 = in-stream upload.  Measured at 1 024 blocks K=1024 (profiles/r03_solve2): zero
-    // copy leaves the solve and the apply reading every descriptor over PCIe (solve 77 us, apply 188)
-    // against 58 / 176 us from device memory, but an in-stream upload costs more than that before the
-    // solve (decode 0.663 against 0.647 ms); the side stream's copy runs beside the syndrome program.
-    static const int desc_mode = [] { const char* e = knob("RQHIP_DEC_ZC"); return e ? std::atoi(e) : 2; }();
+    // Descriptor mode (RQHIP_DEC_ZC in experiments builds): 3 = fetched from the pinned staging by spare
+    // workgroups of the syndrome launch (the default), 2 = side-stream upload, 1 = zero copy, 0 =
+    // in-stream upload.  Measured at 1 024 blocks K=1024 (profiles/r03_solve2): zero copy leaves the
+    // solve and the apply reading every descriptor over PCIe (solve 77 us, apply 188) against 58 / 176
+    // us from device memory, but an in-stream upload costs more than that before the solve (decode
+    // 0.663 against 0.647 ms); the side stream's copy runs beside the syndrome program but the caller's
+    // stream then waits for it across queues (~6 us before the solve, profiles/r05n).  The fetch runs
+    // beside the program as well, on the SIMDs its persistent grid leaves free, and needs no wait.
+    static const int desc_mode = [] { const char* e = knob("RQHIP_DEC_ZC"); return e ? std::atoi(e) : 3; }();
     const bool zero_copy = desc_mode != 0;  // statuses in dstatus, `up` after the last kernel
-    const bool side = desc_mode == 2;
+    const bool fetch = desc_mode == 3 && !k->pair;  // (the two-wave programs carry no fetch)
+    const bool side = desc_mode == 2 || (desc_mode == 3 && !fetch);
+    const size_t idx_bytes = (n_idx * 4 + 15) & ~(size_t)15;  // the fetch moves 16-byte pieces
     if (side && !w->cs) {  // events first: a half-built pair is destroyed, never published
         hipEvent_t ev[2] = {nullptr, nullptr};
         hipStream_t cs = nullptr;
@@ -1268,10 +1293,10 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     // the set's staging and (zero copy / side upload) its device copy were last read by call n - 2's
     // kernels, which precede `up[set]`
     HIP_TRY(hipEventSynchronize(w->up[set]));
-    if ((rc = w->h_idx[set].ensure(n_idx * 4)) || (rc = w->h_status.ensure((size_t)n_blocks * 4))) return rc;
-    if (w->idx[set].cap < n_idx * 4 || w->dstatus.cap < (size_t)n_blocks * 4)
+    if ((rc = w->h_idx[set].ensure(idx_bytes)) || (rc = w->h_status.ensure((size_t)n_blocks * 4))) return rc;
+    if (w->idx[set].cap < idx_bytes || w->dstatus.cap < (size_t)n_blocks * 4)
         HIP_TRY(hipStreamSynchronize((hipStream_t)stream));  // realloc: idle
-    if ((rc = w->idx[set].ensure(n_idx * 4))) return rc;
+    if ((rc = w->idx[set].ensure(idx_bytes))) return rc;
     fill_idx(w->h_idx[set].as<uint32_t>());
     const uint32_t* di;
     int32_t* dst_status;
@@ -1282,13 +1307,15 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
         Workspace* w = nullptr;
         hipStream_t s = nullptr;
         uint32_t set = 0;
+        bool side = false;
         bool armed = false;
         ~UpGuard() {
             if (!armed) return;
-            (void)hipStreamWaitEvent(s, w->cpy[set], 0);
+            if (side) (void)hipStreamWaitEvent(s, w->cpy[set], 0);
             (void)hipEventRecord(w->up[set], s);
         }
-    } up_guard{w, (hipStream_t)stream, set, false};
+    } up_guard{w, (hipStream_t)stream, set, side, false};
+    DescFetch df;
     MarkGuard mark_guard{w, stream};
     if (side) {
         if ((rc = w->dstatus.ensure((size_t)n_blocks * 4))) return rc;
@@ -1296,6 +1323,17 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
         HIP_TRY(hipMemcpyAsync(w->idx[set].p, w->h_idx[set].p, n_idx * 4, hipMemcpyHostToDevice, w->cs));
         up_guard.armed = true;
         HIP_TRY(hipEventRecord(w->cpy[set], w->cs));
+        di = w->idx[set].as<uint32_t>();
+        dst_status = w->dstatus.as<int32_t>();  // the host-decided statuses: copied by the first solver
+    } else if (fetch) {
+        if ((rc = w->dstatus.ensure((size_t)n_blocks * 4))) return rc;
+        void* hdev = nullptr;
+        HIP_TRY(hipHostGetDevicePointer(&hdev, w->h_idx[set].p, 0));
+        df.src = hdev;
+        df.dst = w->idx[set].p;
+        df.bytes = (uint32_t)idx_bytes;
+        mark_guard.armed = true;
+        up_guard.armed = true;  // the syndrome launch reads the staging: `up[set]` after it on any return
         di = w->idx[set].as<uint32_t>();
         dst_status = w->dstatus.as<int32_t>();  // the host-decided statuses: copied by the first solver
     } else if (zero_copy) {
@@ -1352,7 +1390,8 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     // or between it and the solve (the default).
     static const bool wait_early = [] { const char* e = knob("RQHIP_DESC_WAIT"); return e && e[0] == '1'; }();
     if (side && !beside && wait_early) HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, w->cpy[set], 0));
-    if (!beside && (rc = launch_col(ctx, k, T, n_blocks, data, data_stride, w->r0.p, (uint64_t)uni.size() * T, stream)))
+    if (!beside && (rc = launch_col(ctx, k, T, n_blocks, data, data_stride, w->r0.p, (uint64_t)uni.size() * T, stream,
+                                    fetch ? &df : nullptr)))
         return rc;
     if (side && !beside && !wait_early) HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, w->cpy[set], 0));
     SolveArgs s;

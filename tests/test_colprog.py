@@ -99,7 +99,8 @@ SCALAR_ALLOWED = {"s_add_u32", "s_addc_u32", "s_and_b32", "s_and_b64", "s_endpgm
                   "s_lshl_b32", "s_lshr_b32", "s_mov_b32", "s_mul_hi_u32", "s_mul_i32", "s_nop",
                   "s_waitcnt", "s_cmp_ge_u32", "s_cbranch_scc1", "s_mov_b64", "s_cmp_lt_u32",
                   "s_cselect_b32", "s_load_dwordx2", "s_load_dwordx4", "s_load_dwordx16",
-                  "s_getpc_b64", "s_sub_u32", "s_subb_u32", "s_setpc_b64"}
+                  "s_getpc_b64", "s_sub_u32", "s_subb_u32", "s_setpc_b64",
+                  "s_min_u32", "s_cbranch_execz", "s_branch"}  # (the decode's descriptor-fetch loop)
 
 
 def test_program_size_and_assembly(rq):
