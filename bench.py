@@ -118,9 +118,10 @@ def erasure_pattern(K, N, n_blocks, n_erase, seed):
 
 
 def sample_steps(steps):
-    """The timed steps that carry timing events: every fourth from the second (at least two when there
-    are two steps or more), so that most steps run without the events' markers."""
-    s = [i for i in range(steps) if i % 4 == 1]
+    """The timed steps that carry timing events: every eighth from the second (at least two when there
+    are two steps or more), so that most steps run without the events' markers (a sampled step and the
+    one after it wait ~10 + ~5 us more between the decode's apply and the next encode, profiles/r05t)."""
+    s = [i for i in range(steps) if i % 8 == 1]
     if len(s) < 2:
         s = [i for i in range(steps) if i % 2 == 1][:2]
     return s or [0]
@@ -608,7 +609,7 @@ def main():
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
-    # Timing events on every fourth timed step (from the second): the stream markers and the
+    # Timing events on every eighth timed step (from the second): the stream markers and the
     # dispatch-recorded events of rq_launch_timing add ~1 % each to a step they bracket
     # (profiles/r03_dense/r03tb, r03f), so the other steps run as a caller would run them.
     sampled = sample_steps(args.steps)

@@ -59,7 +59,7 @@ uint32_t gi_vgprs(const GiShape& sh) { return gi_tb(sh) + sh.CPL * ((1u << sh.G)
 
 std::string gi_kernel_name(const GiShape& sh) {
     return "rq_apply_gi_k" + std::to_string(sh.KC) + "_g" + std::to_string(sh.G) + "_p" + std::to_string(sh.PDG) +
-           "_c" + std::to_string(sh.CPL) + (sh.PACK ? "_x2" : "") + (sh.diag ? "_d" + std::to_string(sh.diag) : std::string());
+           "_c" + std::to_string(sh.CPL) + (sh.PACK ? "_x2" : "") + (sh.stpol ? "_st" + std::to_string(sh.stpol) : std::string()) + (sh.diag ? "_d" + std::to_string(sh.diag) : std::string());
 }
 
 std::string emit_apply_gi_asm(const GiShape& sh) {
@@ -277,7 +277,9 @@ std::string emit_apply_gi_asm(const GiShape& sh) {
         a.line("s_cbranch_scc1 .Lend");
         for (uint32_t c = 0; c < CPL; ++c) {
             col_exec(a, c, true);
-            a.f("buffer_store_dword v%u, v1, s[56:59], s%u offen offset:%u", ACC(c, k, 0), 64 + k, 256 * c);
+            static const char* const pol[] = {"", " nt", " sc1", " sc0 sc1"};
+            a.f("buffer_store_dword v%u, v1, s[56:59], s%u offen offset:%u%s", ACC(c, k, 0), 64 + k, 256 * c,
+                pol[sh.stpol & 3]);
             col_exec(a, c, false);
         }
     }

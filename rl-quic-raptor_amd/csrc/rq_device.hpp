@@ -51,6 +51,7 @@ struct GiShape {
     uint32_t CPL = 1;   // dword columns per lane (64-column strips per wave), 1 or 2
     uint32_t PACK = 0;  // 1: two subset numbers per index dword (the high one by s_lshr_b32)
     uint32_t diag = 0;  // experiments (timing only, wrong bytes): 1 no index loads, 2 no syndrome loads, 4 no lookups
+    uint32_t stpol = 0; // experiments: recovered-row store policy, 0 plain, 1 nt, 2 sc1, 3 sc0 sc1
 };
 
 // Per block bi of the solve list, the dword stream k_xbits writes at gi + bi * block and the apply kernel

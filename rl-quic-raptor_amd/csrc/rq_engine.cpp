@@ -1190,6 +1190,7 @@ const GiShape& apply_gi_shape() {
             }
         }
         if (const char* d = knob("RQHIP_APPLY_DIAG")) g.diag = (uint32_t)std::atoi(d);
+        if (const char* d = knob("RQHIP_APPLY_STPOL")) g.stpol = (uint32_t)std::atoi(d) & 3u;
         return g;
     }();
     return sh;
@@ -1198,7 +1199,8 @@ const GiShape& apply_gi_shape() {
 // The apply kernel of this device, assembled (amd_comgr, in process) on first use.  Caller holds ctx->mu.
 int get_gi_kernel(DevCtx* ctx, const GiShape& sh, hipFunction_t* fn) {
     if (ctx->gi_fn && ctx->gi_shape.KC == sh.KC && ctx->gi_shape.G == sh.G && ctx->gi_shape.PDG == sh.PDG &&
-        ctx->gi_shape.CPL == sh.CPL && ctx->gi_shape.PACK == sh.PACK && ctx->gi_shape.diag == sh.diag) {
+        ctx->gi_shape.CPL == sh.CPL && ctx->gi_shape.PACK == sh.PACK && ctx->gi_shape.diag == sh.diag &&
+        ctx->gi_shape.stpol == sh.stpol) {
         *fn = ctx->gi_fn;
         return RQ_OK;
     }
