@@ -225,3 +225,23 @@ def test_config3_zero_overhead_statuses_match_oracle(gpu, rq):
         assert bool(ok) == (st[b] == 1), "block %d: GPU status %d, oracle ok %s" % (b, st[b], ok)
         if ok:
             assert payload == src_h[b].tobytes(), "block %d" % b
+
+
+def test_decode_descriptor_fetch_with_a_full_grid(gpu, rq):
+    """218 blocks at K=1024 T=1200 are 1 022 64-column items: the syndrome launch's persistent grid takes
+    every resident slot (1 024 one-wave workgroups), so the workgroup that fetches the decode's
+    descriptors from the pinned staging runs only once a program workgroup has finished.  Every block
+    decodes back to its source, sync and async."""
+    K, T, N, nb, n_erase = 1024, 1200, 1100, 218, 55
+    esis = list(range(K, N))
+    src = _src(gpu, nb, K, T, 218)
+    out = _encode(rq, gpu, src, K, T, esis)
+    data, st, er, rl, rep = _erase_decode(rq, gpu, src, out, K, T, N, n_erase, 218)
+    assert (st == 1).all() and torch.equal(data, src)
+    data2 = src.clone()
+    eb = torch.tensor([b for b in range(nb) for _ in er[b]], device=gpu, dtype=torch.long)
+    ei = torch.tensor([i for b in range(nb) for i in er[b]], device=gpu, dtype=torch.long)
+    data2.view(nb, K, T)[eb, ei] = 0x3C
+    st2 = rq.DecodeBatch(K, T, er, rl).run_async(data2, rep)
+    torch.cuda.synchronize()
+    assert (st2 == 1).all() and torch.equal(data2, src)
