@@ -9,10 +9,11 @@ value = source bytes (n_blocks * K * T, all ranks) / (encode + decode wall time,
 Inputs are resident in HBM when the timed region starts; the erasure pattern's descriptor arrays
 are host arrays prepared once and uploaded by every decode call (part of the timed work).
 
-roofline: the dominant kernel is the encode column program (rq_colprog_K1024_n76).  achieved =
+roofline: the dominant kernel is the column program (rq_colprog_K1024_n76), launched twice per step:
+the encode and the decode's syndrome pass, the same kernel over the same bytes.  achieved =
 algorithmic bytes per launch (K*T source bytes per block x blocks, SURVEY.md sec. 8d: the HBM-read
-roofline) / its mean launch time, measured with HIP events recorded on the launch stream inside the
-timed region; traffic = FETCH_SIZE + WRITE_SIZE of one launch from the committed rocprofv3 PMC
+roofline) / its mean launch time over both launches (as rocprofv3's per-kernel average), measured with
+HIP events recorded by the launches' own dispatches on the launch stream inside the timed region; traffic = FETCH_SIZE + WRITE_SIZE of one launch from the committed rocprofv3 PMC
 passes of this exact workload (profiles/rNN_traffic.json, tools/gpu_profile.sh), else null.
 
 Multi-GPU: one process per GPU (torch.distributed); each rank owns `--blocks` independent blocks
@@ -620,14 +621,15 @@ def main():
         samp = s in ev
         if samp:
             ev[s][0].record(stream)
-            # the encode's column-program launches record their own kernel start / stop (rq_launch_timing)
+            # the column program's launches (the encode's and the decode's syndrome pass) record their
+            # own kernel start / stop (rq_launch_timing)
             rqhip.launch_timing(True)
         rqhip.encode_batch(src, K, T, esis, rep, stream=stream)
         if samp:
-            rqhip.launch_timing(False)
             ev[s][1].record(stream)
         st_async = (db.run if args.sync_decode else db.run_async)(data, recv, stream=stream)
         if samp:
+            rqhip.launch_timing(False)
             ev[s][2].record(stream)
     torch.cuda.synchronize()
     t_rank = time.perf_counter() - t0  # this rank's own time, before the closing barrier
@@ -650,12 +652,14 @@ def main():
     enc_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1, _ in ev.values()]))
     dec_ms = float(np.mean([e1.elapsed_time(e2) for _, e1, e2 in ev.values()]))
     kern_ms, n_launch = rqhip.launch_time(reset=True)
-    enc_kernel_ms = kern_ms / len(ev)  # the encode's kernel time per sampled step (one launch unless split)
+    # the column program's time per pass over the B blocks, the mean of the sampled steps' encode and
+    # syndrome passes (one launch each, unless a 4 GiB buffer span splits one)
+    col_kernel_ms = kern_ms / (2 * len(ev))
     total_blocks = rqshard.sum_over_ranks(B, dist, coll_dev)
     value = total_blocks * K * T * args.steps / dt / 1e9
     if rank == 0:
         kname = "rq_colprog_K%d_n%d" % (K, R)
-        achieved = B * K * T / (enc_kernel_ms * 1e-3) / 1e9
+        achieved = B * K * T / (col_kernel_ms * 1e-3) / 1e9
         traffic, traffic_src = pmc_traffic(kname, K, T, N, B)
         line = {
             "metric": METRIC, "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
@@ -674,11 +678,11 @@ def main():
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "traffic_source": traffic_src, "algorithmic_bytes_per_launch": B * K * T,
                          "launch_ms": round(kern_ms / max(n_launch, 1), 4), "launches_per_step": n_launch // len(ev),
-                         "launch_timing": "HIP events recorded by the encode launches' own dispatches "
-                                          "(hipExtModuleLaunchKernel, rq_launch_timing) on the bench stream, "
-                                          "on timed steps %s" % sorted(ev),
+                         "launch_timing": "HIP events recorded by the column program's own dispatches "
+                                          "(hipExtModuleLaunchKernel, rq_launch_timing) on the bench stream: "
+                                          "the encode and the decode's syndrome launch of timed steps %s" % sorted(ev),
                          # total read + write rate of the launch, (K + R) * T per block
-                         "achieved_read_write": round(B * (K + R) * T / (enc_kernel_ms * 1e-3) / 1e9, 2)},
+                         "achieved_read_write": round(B * (K + R) * T / (col_kernel_ms * 1e-3) / 1e9, 2)},
         }
         if args.cpu_sample > 0 and world == 1:
             line["cpu_baseline"] = cpu_baseline(K, T, N, n_erase, args.cpu_sample)
