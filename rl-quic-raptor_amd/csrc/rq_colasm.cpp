@@ -1133,7 +1133,10 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
     // reads four 8 KiB strides of its own code (one dword per 128-B line; slice (wg / 8) % 32 within
     // its XCD), so the XCD's waves pull the whole program into their L2 in parallel, then wait once.
     // Bounds-checked buffer loads (num_records = code length): nothing beyond the code is read.
-    static const bool code_pf = [] { const char* e = knob("RQHIP_CODEPF"); return !e || e[0] != '0'; }();
+    // RQHIP_CODEPF=2 (experiments): the four loads land in a 256-byte LDS sink (buffer_load ... lds, no
+    // VGPR written) and the wave starts its item without waiting for them.
+    static const int code_pf = [] { const char* e = knob("RQHIP_CODEPF"); return e ? std::atoi(e) : 1; }();
+    const bool pf_sink = code_pf == 2 && W == 1 && mp.lds_base + mp.n_lds_slots < 160;
     if (W == 1 && code_pf && !(diag & 4) && mp.n_vgpr >= 12) {  // v5, v6, v8..v11 are program registers
         line("s_getpc_b64 s[44:45]");
         s += ".Lcpf:\n";
@@ -1147,11 +1150,16 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
         line("s_lshl_b32 s43, s43, 13");
         line("v_lshlrev_b32_e32 v5, 7, v0");
         line("v_add_u32_e32 v5, s43, v5");
+        if (pf_sink) {
+            std::snprintf(buf, sizeof buf, "s_mov_b32 m0, %u", (mp.lds_base + mp.n_lds_slots) * 256u);
+            line(buf);
+        }
         for (uint32_t k = 0; k < 4; ++k) {
             std::snprintf(buf, sizeof buf, "v_add_u32_e32 v6, 0x%x, v5", k * 32u * 8192u); line(buf);
-            std::snprintf(buf, sizeof buf, "buffer_load_dword v%u, v6, s[44:47], 0 offen", 8 + k); line(buf);
+            if (pf_sink) line("buffer_load_dword v6, s[44:47], 0 offen lds");
+            else { std::snprintf(buf, sizeof buf, "buffer_load_dword v%u, v6, s[44:47], 0 offen", 8 + k); line(buf); }
         }
-        line("s_waitcnt vmcnt(0)");
+        if (!pf_sink) line("s_waitcnt vmcnt(0)");
     }
     // experiments: RQHIP_STAGGER=n delays the odd workgroups' start by n x 127 x 64 cycles (do the
     // first rounds' coinciding load bursts cost time?)
@@ -1197,7 +1205,7 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
     s += ".Lfunc_end:\n\t.size " + kname + ", .Lfunc_end-" + kname + "\n";
     s += "\t.p2alignl 6, 3212836864\n\t.fill 256, 4, 3212836864\n";
     s += "\t.section .rodata,\"a\",@progbits\n\t.p2align 6, 0x0\n\t.amdhsa_kernel " + kname + "\n";
-    const std::string lds = std::to_string((mp.lds_base + mp.n_lds_slots) * 256u * W);
+    const std::string lds = std::to_string((mp.lds_base + mp.n_lds_slots) * 256u * W + (pf_sink ? 256u : 0u));
     s += "\t\t.amdhsa_group_segment_fixed_size " + lds + "\n\t\t.amdhsa_private_segment_fixed_size 0\n";
     s += "\t\t.amdhsa_kernarg_size 104\n\t\t.amdhsa_user_sgpr_count 2\n";
     s += "\t\t.amdhsa_user_sgpr_kernarg_segment_ptr 1\n\t\t.amdhsa_system_sgpr_workgroup_id_x 1\n";
