@@ -1043,11 +1043,14 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
     auto put = [&](const char* p) {
         std::string l(p);
         if (l == "CPFETCH") {
+            if (mp.n_vgpr < 24) return;  // (v1..v23 below; the host launches no fetch workgroups then)
             // Descriptor fetch (ColKernArgs::cp_*, a decode's syndrome launch): workgroups past the
             // persistent grid (s2 >= n_wg = s49) copy their cp_chunk-byte piece of the descriptors from
-            // pinned host memory to the device, 16 bytes per lane per round trip, and exit.  They run on
+            // pinned host memory to the device, four 16-byte loads per lane in flight (4 KiB per wave
+            // per round trip; cp_bytes and cp_chunk are multiples of 4 KiB x W), and exit.  They run on
             // the SIMDs the grid leaves free, beside the program; the solve that reads the copy is the
             // next kernel in the stream.  Vector loads and stores only.
+            const uint32_t WB = 1024u * W;  // bytes per workgroup per load
             line("s_cmp_lt_u32 s2, s49");
             line("s_cbranch_scc1 .Ldmain");
             line("s_load_dwordx4 s[56:59], s[0:1], 0x50");  // cp_src, cp_dst
@@ -1063,10 +1066,21 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
             line("v_cmp_gt_u32_e32 vcc, s63, v1");
             line("s_and_b64 exec, exec, vcc");
             line("s_cbranch_execz .Ldcpend");
-            line("global_load_dwordx4 v[4:7], v1, s[56:57]");
+            for (uint32_t u = 1; u < 4; ++u) {
+                std::snprintf(buf, sizeof buf, "v_add_u32_e32 v%u, 0x%x, v1", 1 + u, u * WB);
+                line(buf);
+            }
+            // addresses in v1..v4, data in v[8:23] (disjoint: a store's address must survive the loads)
+            for (uint32_t u = 0; u < 4; ++u) {
+                std::snprintf(buf, sizeof buf, "global_load_dwordx4 v[%u:%u], v%u, s[56:57]", 8 + 4 * u, 11 + 4 * u, 1 + u);
+                line(buf);
+            }
             line("s_waitcnt vmcnt(0)");
-            line("global_store_dwordx4 v1, v[4:7], s[58:59]");
-            std::snprintf(buf, sizeof buf, "v_add_u32_e32 v1, 0x%x, v1", 1024u * W);
+            for (uint32_t u = 0; u < 4; ++u) {
+                std::snprintf(buf, sizeof buf, "global_store_dwordx4 v%u, v[%u:%u], s[58:59]", 1 + u, 8 + 4 * u, 11 + 4 * u);
+                line(buf);
+            }
+            std::snprintf(buf, sizeof buf, "v_add_u32_e32 v1, 0x%x, v1", 4u * WB);
             line(buf);
             line("s_branch .Ldcp");
             s += ".Ldcpend:\n";

@@ -91,6 +91,7 @@ struct ColKernel {
     uint32_t waves_per_cu = 4;     // residency of the code object (registers, LDS)
     uint32_t wg_waves = 1;         // waves per workgroup (MProg::wg_waves)
     bool pair = false;             // two-wave program (emit_pair_asm): one item per workgroup iteration
+    bool fetch_ok = false;         // its workgroups past the grid can carry a decode's descriptor fetch
     std::vector<uint32_t> dma4_rows;  // four-row staging: every group's rows (needs 16-B aligned rows)
     MProg::Stats st{};
     uint64_t last_use = 0;         // LRU clock of the per-device cache
@@ -727,7 +728,7 @@ int get_col_kernel(DevCtx* ctx, const Params& p, const uint32_t* esi, uint32_t n
             ch.n_slots = lead.n_slots;
             ch.n_ins = (uint32_t)(pair ? pp.A.ins.size() + pp.B.ins.size() : mp.ins.size());
             ch.wg_waves = pair ? 2 : mp.wg_waves;
-            ch.flags = pair ? 1u : 0u;
+            ch.flags = pair ? 1u : (mp.n_vgpr >= 24 ? 2u : 0u);  // 2: carries the descriptor fetch (rq_colasm.cpp)
             ch.name_len = (uint32_t)kname.size();
             ch.co_len = co.size();
             ch.st = lead.st;
@@ -745,6 +746,7 @@ int get_col_kernel(DevCtx* ctx, const Params& p, const uint32_t* esi, uint32_t n
         k->waves_per_cu = ch.waves_per_cu;
         k->wg_waves = std::max<uint32_t>(1, ch.wg_waves);
         k->pair = (ch.flags & 1u) != 0;
+        k->fetch_ok = (ch.flags & 2u) != 0;
         k->st = ch.st;
         k->n_ins = ch.n_ins;
         slot = std::move(k);
@@ -764,16 +766,20 @@ bool xcd_order() {
 }
 
 // Run a column program over n_blocks device-resident blocks.  Caller holds ctx->mu.
-// A decode's descriptor fetch riding on its syndrome launch (ColKernArgs::cp_*): bytes (a multiple of 16)
-// from pinned host memory to the device.
+// A decode's descriptor fetch riding on its syndrome launch (ColKernArgs::cp_*): bytes (a multiple of
+// kFetchQuantum, both buffers that large) from pinned host memory to the device.  `carried` reports
+// whether the launch took it: only when its persistent grid leaves SIMDs free, so that the fetch runs
+// beside the program instead of after it.
+constexpr uint32_t kFetchQuantum = 16384;  // 4 KiB per wave and round trip, up to four waves per workgroup
 struct DescFetch {
     const void* src = nullptr;  // the device's address of the pinned staging
     void* dst = nullptr;
     uint32_t bytes = 0;
+    bool carried = false;
 };
 
 int launch_col(DevCtx* ctx, ColKernel* k, uint32_t T, uint32_t n_blocks, const void* src, uint64_t src_stride,
-               void* out, uint64_t out_stride, void* stream, const DescFetch* df = nullptr) {
+               void* out, uint64_t out_stride, void* stream, DescFetch* df = nullptr) {
     if (T < 8 || T % 4) return fail(RQ_ERR_BAD_ARG, "device-resident symbols: T must be a multiple of 4, at least 8");
     if (n_blocks == 0) return RQ_OK;
     if (!k->dma4_rows.empty() && (T % 16 || src_stride % 16 || (uintptr_t)src % 16))
@@ -847,17 +853,19 @@ int launch_col(DevCtx* ctx, ColKernel* k, uint32_t T, uint32_t n_blocks, const v
         const uint32_t wgs = std::min(resident, ((iters + rounds - 1) / rounds + 7) / 8 * 8);
         a.n_items = iters;
         a.n_wg = wgs;
-        // the descriptor fetch rides on the first launch: up to the SIMDs the grid leaves free (64 at
-        // K=1024 x 1 024 blocks), at least one workgroup, 1 KiB per wave per round trip
+        // the descriptor fetch rides on the first launch when its grid leaves SIMDs free (64 at K=1024 x
+        // 1 024 blocks): as many workgroups as free slots, up to one per 4 KiB x W round trip
         uint32_t n_cp = 0;
-        if (df && df->bytes && b0 == 0) {
-            const uint32_t free_wg = resident > wgs ? resident - wgs : 0u;
-            const uint32_t per_wg = 1024u * Wg;
-            n_cp = std::max<uint32_t>(1, std::min<uint32_t>(std::max<uint32_t>(free_wg, 1), (df->bytes + per_wg - 1) / per_wg));
+        const uint32_t free_wg = resident > wgs ? resident - wgs : 0u;
+        const uint32_t per_trip = 4096u * Wg;
+        if (df && df->bytes && b0 == 0 && free_wg && k->fetch_ok && df->bytes % per_trip == 0) {
+            n_cp = std::min<uint32_t>(free_wg, (df->bytes + per_trip - 1) / per_trip);
             a.cp_src = (uint64_t)(uintptr_t)df->src;
             a.cp_dst = (uint64_t)(uintptr_t)df->dst;
             a.cp_bytes = df->bytes;
-            a.cp_chunk = ((df->bytes + n_cp - 1) / n_cp + 15) & ~15u;
+            const uint32_t trips = (df->bytes / per_trip + n_cp - 1) / n_cp;  // per workgroup
+            a.cp_chunk = trips * per_trip;
+            df->carried = true;
         }
         if (xcd_order() && wgs % 8 == 0) {  // the remap needs the stride to keep g % 8 fixed
             a.xcd_q = iters / 8;
@@ -1276,8 +1284,9 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     const bool zero_copy = desc_mode != 0;  // statuses in dstatus, `up` after the last kernel
     const bool fetch = desc_mode == 3 && !k->pair;  // (the two-wave programs carry no fetch)
     const bool side = desc_mode == 2 || (desc_mode == 3 && !fetch);
-    const size_t idx_bytes = (n_idx * 4 + 15) & ~(size_t)15;  // the fetch moves 16-byte pieces
-    if (side && !w->cs) {  // events first: a half-built pair is destroyed, never published
+    const size_t idx_bytes = (n_idx * 4 + kFetchQuantum - 1) / kFetchQuantum * kFetchQuantum;  // fetch granularity
+    if ((side || fetch) && !w->cs) {  // events first: a half-built pair is destroyed, never published
+        // (the fetch falls back to the side-stream upload when the syndrome launch's grid is full)
         hipEvent_t ev[2] = {nullptr, nullptr};
         hipStream_t cs = nullptr;
         bool ok = hipEventCreateWithFlags(&ev[0], internal_event_flags()) == hipSuccess &&
@@ -1396,6 +1405,12 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
                                     fetch ? &df : nullptr)))
         return rc;
     if (side && !beside && !wait_early) HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, w->cpy[set], 0));
+    if (fetch && !df.carried) {  // no SIMD free beside the program: the upload on the side stream instead
+        HIP_TRY(hipMemcpyAsync(w->idx[set].p, w->h_idx[set].p, n_idx * 4, hipMemcpyHostToDevice, w->cs));
+        up_guard.side = true;
+        HIP_TRY(hipEventRecord(w->cpy[set], w->cs));
+        HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, w->cpy[set], 0));
+    }
     SolveArgs s;
     s.blk_map = di + o_map;
     s.erased_off = di + o_eoff;
