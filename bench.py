@@ -511,6 +511,7 @@ def run_config5(args):
             t2 = time.perf_counter()
             sh["t_enc"] += t1 - t0
             sh["t_dec"] += t2 - t1
+    settle_steps = settle(step, args.settle_ms)
     for _ in range(args.warmup):
         step()
     for sh in shapes:
@@ -547,6 +548,7 @@ def run_config5(args):
             "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (seeded numpy payload, seeded exact-count erasures), pinned host buffers",
             "config": {"workload": "mixed stream, %d MiB of source per shape per step, host-memory batch API" % mb,
+                       "settle": {"ms": args.settle_ms, "steps": settle_steps},
                        "shapes": per},
             # the path is bound by the PCIe link (pinned copies measured on this box), not HBM: achieved =
             # H2D bytes per second of the whole stream (the busier direction) against the box's pinned
