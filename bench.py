@@ -240,8 +240,11 @@ def cpu_baseline(K, T, N, n_erase, n_blocks):
                            "decode_gbs": gb(nb1, td1), "sample": "%d blocks" % nb1},
             "oracle_one_thread": {"value": gb(1, teO + tdO), "cores": 1, "encode_gbs": gb(1, teO),
                                   "decode_gbs": gb(1, tdO),
-                                  "sample": "1 block: oracle/rq_oracle.c, the library's own algorithm restated (Solve "
-                                            "with inactivation and dense GF(256) elimination per block, RQ/solver.go)"},
+                                  "sample": "1 block: oracle/rq_oracle.c, a naive dense GF(256) elimination of the "
+                                            "full constraint system per block (oracle/rq_oracle.c:199; no inactivation): "
+                                            "the parity checker, slower than the reference's own Solve"},
+            # the reference Go path (xssnick Solve with inactivation) on one core, measured in the survey
+            # container: the stated reference figure
             "reference_go_1core_gbs": 0.094}
 
 

@@ -9,8 +9,9 @@
 // go/cmd/raptorq_eval/main.go:85-103,199-222 compile unchanged.  Library errors carry the library's
 // own message (rq_last_error: "symbol size cannot be zero", "not enough symbols to decode", ...).
 //
-// Ownership: every returned slice is Go memory (copied out of C); C keeps no Go pointer
-// (rq_encoder_create and rq_decoder_add copy their inputs).  Handles are freed by finalizers.
+// Ownership: every returned slice is Go memory (copied out of C), except HostAlloc's pinned C memory;
+// C keeps no Go pointer (rq_encoder_create and rq_decoder_add copy their inputs; rq_tracker_add reads
+// none).  Handles are freed by finalizers.
 // tests/test_go_shim.py checks every C.rq_* call here against the prototypes of include/rqhip.h.
 package fec
 
@@ -142,6 +143,42 @@ func (d *RaptorQDecoder) Decode() (bool, []byte, error) {
 	return true, payload, nil
 }
 
+// RaptorQTracker is RaptorQDecoder's AddSymbol bookkeeping without the symbol bytes (rq_tracker_*): a
+// receiver that stages each symbol once in its own pinned buffer (go/fecquic/rq_stage.go) keeps the
+// decoder's readiness rule -- AddSymbol's bool, K <= unique symbols held (RQ/decoder.go:47,57; the
+// receiver counts the true returns, rxbuf.go:472) -- and decodes the staged blocks with DecodeBlocks.
+// No reference counterpart: the library's decoder always copies (RQ/decoder.go:39-57).
+type RaptorQTracker struct {
+	K int
+	L int
+	h *C.rq_tracker
+}
+
+func NewRaptorQTracker(dataSize int, L int) (*RaptorQTracker, error) {
+	if dataSize < 0 || L <= 0 {
+		return nil, errBadSizeL
+	}
+	var code C.int
+	h := C.rq_tracker_create(C.uint64_t(dataSize), C.uint32_t(L), &code)
+	if h == nil {
+		return nil, libErr(code)
+	}
+	t := &RaptorQTracker{K: int(C.rq_tracker_k(h)), L: L, h: h}
+	runtime.SetFinalizer(t, func(x *RaptorQTracker) { C.rq_tracker_free(x.h) })
+	return t, nil
+}
+
+// AddSymbol has RaptorQDecoder.AddSymbol's signature, checks and bool; only len(data) is read.
+func (t *RaptorQTracker) AddSymbol(id uint32, data []byte) (bool, error) {
+	var canTry C.int
+	code := C.rq_tracker_add(t.h, C.uint32_t(id), C.size_t(len(data)), &canTry)
+	runtime.KeepAlive(t)
+	if code != 0 {
+		return canTry != 0, libErr(code)
+	}
+	return canTry != 0, nil
+}
+
 // RaptorQEncodeBlock returns symbols 0..N-1 of one block of at most K*L bytes (longer data is cut
 // to K*L).  The repairs come from one batched call instead of N-K GenSymbol calls.
 func RaptorQEncodeBlock(data []byte, N, K, L int) ([]Packet, error) {
@@ -260,7 +297,9 @@ func DecodeBlocks(K, L int, data [][]byte, repair [][]byte, erased, repairESI []
 	ioMem := C.malloc(ioBytes)
 	defer C.free(ioMem)
 	io := unsafe.Slice((*C.rq_block_io)(ioMem), n)
-	var pin runtime.Pinner // the library reads these Go slices during the call only
+	// the library reads these slices during the call only; Pin keeps Go memory in place and is a no-op
+	// on memory that is not Go's (HostAlloc's pinned C memory: runtime.Pinner ignores non-heap pointers)
+	var pin runtime.Pinner
 	defer pin.Unpin()
 	for b := 0; b < n; b++ {
 		io[b] = C.rq_block_io{n_erased: C.uint32_t(len(erased[b])), n_repair: C.uint32_t(len(repairESI[b]))}

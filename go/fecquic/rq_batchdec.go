@@ -3,11 +3,12 @@
 //
 // The reference worker takes one ready block from decodeQ and calls its per-object decoder's Decode
 // (go/fecquic/rxbuf.go:336-377).  batchDecodeWorker keeps everything around that call -- the classifier
-// and its AddSymbol bookkeeping (haveU counts the true returns; a block is ready at haveU >= K), the
-// 50 ms DDL scheduler, the receive budget, the single writer -- and replaces the call: it drains up to
-// decodeBatchMax queued blocks, stages each block's received symbols in pinned memory (fec.HostAlloc:
-// source rows in place, repairs in ESI order) and decodes them with one fec.DecodeBlocks call per
-// library K.  rxbuf.go.patch points the workers here.  A status other than 1 is the reference's failed
+// and its AddSymbol bookkeeping (haveU counts the true returns of the fec.RaptorQTracker; a block is
+// ready at haveU >= K), the 50 ms DDL scheduler, the receive budget -- and replaces the call: it drains
+// up to decodeBatchMax queued blocks and decodes them with one fec.DecodeBlocks call per (library K, L),
+// on the rows ingest already staged in each block's pinned buffer (rq_stage.go): no host copy of a
+// received symbol between the datagram and the GPU.  The recovered block is written to the file from the
+// same buffer.  rxbuf.go.patch points the workers here.  A status other than 1 is the reference's failed
 // Decode: the block waits for more symbols (queued = false).
 package fecquic
 
@@ -20,14 +21,6 @@ import (
 
 // ready blocks per DecodeBlocks call (one worker drains the queue without waiting for more)
 const decodeBatchMax = 256
-
-type stagedBlock struct {
-	b         *rxBlock
-	data      []byte   // library K x L bytes of the pinned staging
-	repair    []byte   // the received repair rows, repairESI order
-	erased    []uint32 // source ESIs < library K not received
-	repairESI []uint32
-}
 
 // batchDecodeWorker runs in place of the reference worker loop until decodeQ closes.
 func (m *rxManager) batchDecodeWorker() {
@@ -52,8 +45,10 @@ func (m *rxManager) batchDecodeWorker() {
 // libraryK is the decoder's K for a block of dataSize bytes (NewRaptorQDecoder(dataSize, L)).
 func libraryK(dataSize, L int) int { return (dataSize + L - 1) / L }
 
+type groupKey struct{ kl, L int }
+
 func (m *rxManager) decodeBatch(batch []*rxBlock) {
-	groups := map[int][]*rxBlock{} // by library K: one DecodeBlocks call shares K
+	groups := map[groupKey][]*rxBlock{} // one DecodeBlocks call shares K and L
 	for _, b := range batch {
 		if b.done {
 			continue
@@ -62,46 +57,69 @@ func (m *rxManager) decodeBatch(batch []*rxBlock) {
 			b.queued = false // not ready yet (the reference worker's first check)
 			continue
 		}
-		kl := libraryK(b.dataSize, b.L)
-		groups[kl] = append(groups[kl], b)
+		k := groupKey{libraryK(b.dataSize, b.L), b.L}
+		groups[k] = append(groups[k], b)
 	}
-	for kl, blocks := range groups {
-		m.decodeGroup(kl, blocks)
+	for k, blocks := range groups {
+		m.decodeGroup(k.kl, k.L, blocks)
 	}
 }
 
-func (m *rxManager) decodeGroup(kl int, blocks []*rxBlock) {
-	L := blocks[0].L
-	stage := fec.HostAlloc(len(blocks) * kl * L)
-	if stage == nil {
-		stage = make([]byte, len(blocks)*kl*L) // pageable still works, at a lower PCIe rate
-	} else {
-		defer fec.HostFree(stage)
-	}
-	st := make([]stagedBlock, len(blocks))
-	m.mu.Lock() // a queued block's symbols no longer change (the classifier drops new ones), but
-	// the slabs are shared with the pool: copy under the lock
+type stagedBlock struct {
+	b         *rxBlock
+	st        *blockStage
+	data      []byte   // library K x L bytes: the staging's first rows
+	repair    []byte   // the received library repairs' rows, consecutive
+	erased    []uint32 // source ESIs < library K not received
+	repairESI []uint32
+}
+
+func (m *rxManager) decodeGroup(kl, L int, blocks []*rxBlock) {
+	// the ESIs the classifier accepted (a queued block's set no longer changes: the classifier drops its
+	// new symbols, rxbuf.go:446-458)
+	accepted := make([][]int, len(blocks))
+	m.mu.Lock()
 	for i, b := range blocks {
-		sb := &st[i]
-		sb.b = b
-		sb.data = stage[i*kl*L : (i+1)*kl*L]
-		esis := make([]int, 0, len(b.syms))
 		for esi := range b.syms {
-			esis = append(esis, esi)
+			accepted[i] = append(accepted[i], esi)
 		}
-		sort.Ints(esis)
+	}
+	m.mu.Unlock()
+	st := make([]stagedBlock, 0, len(blocks))
+	for i, b := range blocks {
+		bs := m.stage.lookup(b.id)
+		if bs == nil {
+			b.queued = false
+			continue
+		}
+		bs.mu.Lock()
+		bs.frozen = true // from here no ingest writes into bs.buf
+		bs.mu.Unlock()
+		sb := stagedBlock{b: b, st: bs, data: bs.buf[:kl*L]}
 		have := make([]bool, kl)
-		for _, esi := range esis {
-			s := b.syms[esi]
+		var reps []int // library repairs: ESI >= kl (rows esi below the wrapper K, K + i above it)
+		for _, esi := range accepted[i] {
 			if esi < kl {
-				n := copy(sb.data[esi*L:(esi+1)*L], s.b[:s.n])
-				clear(sb.data[esi*L+n : (esi+1)*L])
 				have[esi] = true
 			} else {
-				sb.repairESI = append(sb.repairESI, uint32(esi))
-				row := make([]byte, L)
-				copy(row, s.b[:s.n])
-				sb.repair = append(sb.repair, row...)
+				reps = append(reps, esi)
+			}
+		}
+		sort.Slice(reps, func(x, y int) bool { return bs.rowOf[reps[x]] < bs.rowOf[reps[y]] })
+		contiguous := true
+		for j, esi := range reps {
+			sb.repairESI = append(sb.repairESI, uint32(esi))
+			contiguous = contiguous && int(bs.rowOf[esi]) == kl+j
+		}
+		if contiguous {
+			sb.repair = bs.buf[kl*L : (kl+len(reps))*L] // the common case: the rows as ingest staged them
+		} else {
+			// a hole among the rows (a symbol the ring or the budget dropped, a short last block with a
+			// missing symbol below the wrapper K): these rows alone are gathered
+			sb.repair = make([]byte, len(reps)*L)
+			for j, esi := range reps {
+				r := int(bs.rowOf[esi])
+				copy(sb.repair[j*L:(j+1)*L], bs.buf[r*L:(r+1)*L])
 			}
 		}
 		for esi := 0; esi < kl; esi++ {
@@ -109,9 +127,11 @@ func (m *rxManager) decodeGroup(kl int, blocks []*rxBlock) {
 				sb.erased = append(sb.erased, uint32(esi))
 			}
 		}
+		st = append(st, sb)
 	}
-	m.mu.Unlock()
-
+	if len(st) == 0 {
+		return
+	}
 	data := make([][]byte, len(st))
 	repair := make([][]byte, len(st))
 	erased := make([][]uint32, len(st))
@@ -124,27 +144,41 @@ func (m *rxManager) decodeGroup(kl int, blocks []*rxBlock) {
 	status, err := fec.DecodeBlocks(kl, L, data, repair, erased, repairESI, 0)
 	m.decTimeTotal.Add(time.Since(t0).Milliseconds())
 	for i := range st {
-		b := st[i].b
+		b, bs := st[i].b, st[i].st
 		if err != nil || status[i] != 1 {
 			// the reference's failed Decode: likely needs more symbols
 			m.decodeFailures.Add(1)
+			bs.mu.Lock()
+			bs.frozen = false
+			bs.mu.Unlock()
 			b.queued = false
 			continue
 		}
-		// one contiguous write per block, out of the pinned staging (freed when this call returns)
-		out := make([]byte, b.dataSize)
-		copy(out, st[i].data)
-		m.writeQ <- writeTask{off: int64(int(b.id) * b.K * b.L), data: out}
+		// the block is whole in its staging: one write from there (the writer goroutine's bounds and
+		// counters, rxbuf.go:320-334), then the staging goes back to the free list
+		off := int64(int(b.id) * b.K * b.L)
+		out := bs.buf[:b.dataSize]
+		if rem := int64(m.fileSize) - off; rem < int64(len(out)) {
+			if rem < 0 {
+				rem = 0
+			}
+			out = out[:rem]
+		}
+		tw := time.Now()
+		_, _ = m.out.WriteAt(out, off)
+		dw := time.Since(tw)
+		m.writeTimeMs.Add(dw.Milliseconds())
+		m.writeTimeUs.Add(dw.Microseconds())
+		m.written.Add(uint64(len(out)))
 		m.decBlocks.Add(1)
 		m.mu.Lock()
 		for _, s := range b.syms {
 			m.inUse.Add(int64(-s.n))
-			s.n = 0
-			m.slabs.Put(s)
 		}
 		b.syms = nil
 		b.done = true
 		delete(m.blocks, b.id)
 		m.mu.Unlock()
+		m.stage.release(b.id)
 	}
 }

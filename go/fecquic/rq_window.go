@@ -9,6 +9,13 @@
 // A short last block keeps the per-object path: its library K is ceil(n/L) (the receiver builds its
 // decoder from the block's data size, rxbuf.go:437), and a padded block would be encoded under the
 // window's K instead.
+//
+// Latency: the reference emits a block's packets as soon as that block is encoded.  A window delays the
+// first packet by one window's read + encode, and holds the window's source and repairs in memory, so
+// the windows grow: firstWindowBlocks (4 blocks, ~5 MB at K=1024 L=1200) first, then doubling up to
+// windowBlocks (256 blocks, ~315 MB, enough for the library's H2D / kernel / D2H pipeline to run at the
+// PCIe rate, DESIGN.md sec. 5.6).  A file of a few blocks is sent after a few blocks' encode, not the
+// whole file's; encTime in transfer.go then measures each window's encode on the block that triggered it.
 package fecquic
 
 import (
@@ -17,9 +24,13 @@ import (
 	"github.com/quic-go/quic-go/fec"
 )
 
-// blocks per EncodeWindow call: 256 blocks of K=1024, L=1200 are 315 MB of source, enough for the
-// library's H2D / kernel / D2H pipeline to reach the PCIe rate (DESIGN.md sec. 5.6)
-const windowBlocks = 256
+// blocks per EncodeWindow call: the first window is small (time to first packet), later ones double
+// up to windowBlocks (256 blocks of K=1024, L=1200 are 315 MB of source, enough for the library's H2D /
+// kernel / D2H pipeline to reach the PCIe rate, DESIGN.md sec. 5.6)
+const (
+	firstWindowBlocks = 4
+	windowBlocks      = 256
+)
 
 type windowBlock struct {
 	pkts []fec.Packet
@@ -32,10 +43,11 @@ type windowReader struct {
 	deviceMask uint32
 	queue      []windowBlock
 	done       bool
+	window     int // blocks the next fill reads (firstWindowBlocks, doubling up to windowBlocks)
 }
 
 func newWindowReader(r io.Reader, N, K, L int, deviceMask uint32) *windowReader {
-	return &windowReader{r: r, N: N, K: K, L: L, deviceMask: deviceMask}
+	return &windowReader{r: r, N: N, K: K, L: L, deviceMask: deviceMask, window: firstWindowBlocks}
 }
 
 // next returns the next block's N packets in ESI order (the K source symbols, the last zero padded as
@@ -58,12 +70,20 @@ func (w *windowReader) next() ([]fec.Packet, int, error) {
 	return b.pkts, b.n, nil
 }
 
-// fill reads up to windowBlocks blocks and encodes the full ones in one call.
+// fill reads up to w.window blocks and encodes the full ones in one call; the next window is twice as
+// large, up to windowBlocks.
 func (w *windowReader) fill() error {
 	blockBytes := w.K * w.L
-	full := make([][]byte, 0, windowBlocks)
+	want := w.window
+	if w.window < windowBlocks {
+		w.window *= 2
+		if w.window > windowBlocks {
+			w.window = windowBlocks
+		}
+	}
+	full := make([][]byte, 0, want)
 	var tail []byte
-	for len(full) < windowBlocks {
+	for len(full) < want {
 		buf := make([]byte, blockBytes)
 		n, err := io.ReadFull(w.r, buf)
 		if err == io.EOF || err == io.ErrUnexpectedEOF {

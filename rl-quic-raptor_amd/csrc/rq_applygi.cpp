@@ -20,7 +20,10 @@
 // offsets arrive through scalar loads, two 16-dword pieces per wait (SMEM returns out of order, so each
 // wait is lgkmcnt(0) and a load issued right after one has a whole pair of pieces to land).
 #include <algorithm>
+#include <cctype>
 #include <cstdio>
+#include <cstring>
+#include <sstream>
 #include <string>
 #include <utility>
 #include <vector>
@@ -301,6 +304,81 @@ std::string emit_apply_gi_asm(const GiShape& sh) {
            "\n    .wavefront_size: 64\n";
     a.s += "amdhsa.target: amdgcn-amd-amdhsa--gfx950\namdhsa.version:\n  - 1\n  - 2\n...\n\t.end_amdgpu_metadata\n";
     return a.s;
+}
+
+// The index-mode guard.  In the VGPR index mode (s_set_gpr_idx_on) every VALU
+// instruction's enabled operand is offset by M0[7:0], and M0[15:12] holds the enable bits (SRC0, SRC1,
+// SRC2, DST).  So (1) a VALU instruction other than a lookup inside a region reads a shifted register;
+// (2) a whole-dword write of M0 replaces the index AND the enable bits -- a packed pair of subset numbers
+// written that way puts the second number's bits into the enables or into bits 7:5 of the index, and an
+// enabled DST or an index past the table reaches VGPRs beyond the allocation (the round-5 variant "M0
+// written by SALU moves to carry two indices per dword" faulted; its code was never committed, and this
+// generator has no such path); (3) the index itself is bits 7:0 of an SGPR the kernel loaded from the
+// stream, which k_xbits / the solvers (gi_stream) build from G bits, so it is < 2^G
+// (tests/test_applygi.py emulates that stream on the host).
+bool check_apply_gi_asm(const std::string& text, const GiShape& sh, std::string* err) {
+    const uint32_t NT = 1u << sh.G, NV = gi_vgprs(sh), TB = gi_tb(sh);
+    auto bad = [&](const std::string& why, const std::string& l) {
+        if (err) *err = "apply kernel index-mode check: " + why + ": `" + l + "`";
+        return false;
+    };
+    std::istringstream in(text);
+    std::string l;
+    bool on = false, body = false;
+    while (std::getline(in, l)) {
+        if (l.rfind(".amdhsa_kernel", 1) != std::string::npos || l.find(".section") != std::string::npos) break;
+        size_t a = l.find_first_not_of(" \t");
+        if (a == std::string::npos) continue;
+        const std::string t = l.substr(a);
+        if (t[0] == '.' && t.find(':') == std::string::npos) continue;  // directives
+        if (t.find(':') != std::string::npos && t.find(' ') == std::string::npos) {  // a label
+            if (on) return bad("label inside an index-mode region", t);
+            body = true;
+            continue;
+        }
+        if (!body && t.find(':') != std::string::npos) { body = true; continue; }  // the kernel symbol
+        std::string op = t.substr(0, t.find_first_of(" \t"));
+        // M0: never written or read by name (the index mode keeps its state there)
+        for (size_t at = t.find("m0"); at != std::string::npos; at = t.find("m0", at + 1)) {
+            const bool lft = at == 0 || !std::isalnum((unsigned char)t[at - 1]);
+            const bool rgt = at + 2 >= t.size() || !std::isalnum((unsigned char)t[at + 2]);
+            if (lft && rgt) return bad("M0 named while the kernel uses the VGPR index mode", t);
+        }
+        if (op == "s_set_gpr_idx_on") {
+            if (on) return bad("nested s_set_gpr_idx_on", t);
+            if (t.find("gpr_idx(SRC0)") == std::string::npos || t.find("DST") != std::string::npos ||
+                t.find("SRC1") != std::string::npos || t.find("SRC2") != std::string::npos)
+                return bad("index mode other than SRC0", t);
+            on = true;
+            continue;
+        }
+        if (op == "s_set_gpr_idx_off") {
+            if (!on) return bad("s_set_gpr_idx_off outside a region", t);
+            on = false;
+            continue;
+        }
+        if (op == "s_set_gpr_idx_idx") {
+            if (!on) return bad("s_set_gpr_idx_idx outside a region", t);
+            continue;
+        }
+        if (!on) continue;
+        if (op == "s_endpgm" || op.rfind("s_branch", 0) == 0 || op.rfind("s_cbranch", 0) == 0 || op == "s_setpc_b64")
+            return bad("control flow inside an index-mode region", t);
+        if (op.rfind("buffer_", 0) == 0 || op.rfind("global_", 0) == 0 || op.rfind("ds_", 0) == 0 ||
+            op.rfind("flat_", 0) == 0 || op.rfind("scratch_", 0) == 0)
+            return bad("memory instruction inside an index-mode region", t);
+        if (op[0] != 'v') continue;  // SALU (the index loads' bookkeeping)
+        unsigned d = 0, s0 = 0, s1 = 0;
+        if (op != "v_xor_b32_e32" || std::sscanf(t.c_str(), "v_xor_b32_e32 v%u, v%u, v%u", &d, &s0, &s1) != 3)
+            return bad("vector instruction other than a table lookup inside an index-mode region", t);
+        bool table = false;
+        for (uint32_t c = 0; c < sh.CPL; ++c) table |= s0 == TB + c * NT;
+        if (!table) return bad("indexed source is not a table base", t);
+        if (s0 + NT > NV) return bad("table end past the VGPR allocation", t);
+        if (d != s1 || (d >= s0 && d < s0 + NT)) return bad("lookup destination is not an accumulator outside the table", t);
+    }
+    if (on) return bad("index-mode region not closed", "end of kernel");
+    return true;
 }
 
 }  // namespace rq

@@ -22,6 +22,7 @@
 #include <cstring>
 #include <functional>
 #include <map>
+#include <unordered_set>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -29,7 +30,9 @@
 #include <vector>
 
 #include "../../include/rqhip.h"
+#include "../../include/rqhip_debug.h"
 #include "rq_applygi.hpp"
+#include "rq_gistream.hpp"
 #include "rq_colasm.hpp"
 #include "rq_colprog.hpp"
 #include "rq_device.hpp"
@@ -867,6 +870,14 @@ int launch_col(DevCtx* ctx, ColKernel* k, uint32_t T, uint32_t n_blocks, const v
             a.cp_chunk = trips * per_trip;
             df->carried = true;
         }
+#ifdef RQHIP_EXPERIMENTS
+        // RQHIP_FETCH_LOG=1: the launch shape of a decode's syndrome launch (tests/test_gpu_experimental_programs.py
+        // checks the fetch at W > 1 waves per workgroup, whose per-trip / chunk arithmetic W = 1 never exercises)
+        static const bool fetch_log = knob("RQHIP_FETCH_LOG") != nullptr;
+        if (fetch_log && df)
+            std::fprintf(stderr, "[fetch] carried=%d W=%u wgs=%u resident=%u n_cp=%u bytes=%u chunk=%u\n", df->carried ? 1 : 0,
+                         Wg, wgs, resident, n_cp, df->bytes, a.cp_chunk);
+#endif
         if (xcd_order() && wgs % 8 == 0) {  // the remap needs the stride to keep g % 8 fixed
             a.xcd_q = iters / 8;
             a.xcd_n = a.xcd_q * 8;
@@ -1182,6 +1193,16 @@ bool solve_beside() {
 // The decode's apply: 1 = the register-table kernel (rq_applygi.cpp, k_xbits + the generated kernel),
 // 0 = k_apply's v_perm byte tables.  rq_debug_apply_mode switches it (tests compare the two).
 uint32_t g_apply_mode = 1;
+// Stream bound of the register-table apply: e <= kGiMaxE and the whole stream of the solve
+// list <= kGiMaxBytes.  Within it every byte offset the kernel forms (block base, slice records, their
+// one-pair prefetch) stays far below 2^32 and the allocation stays small; config 3 (e ~ 60) needs 27 MB.
+constexpr uint32_t kGiMaxE = 512;
+constexpr uint64_t kGiMaxBytes = 512ull << 20;
+bool gi_stream_fits(uint32_t max_e, uint32_t n_solve, const GiShape& sh) {
+    if (max_e > kGiMaxE) return false;
+    const GiLayout gl = gi_layout(max_e, sh);
+    return (uint64_t)n_solve * gl.block * 4 + 4096 <= kGiMaxBytes;
+}
 
 // The register-table apply's shape: KC = 8 outputs per wave, groups of G = 5 syndromes, loads two groups
 // ahead, one dword column per lane (120 VGPRs: four waves per SIMD); RQHIP_APPLY_GI="KC,G,PDG[,CPL]" in
@@ -1214,7 +1235,8 @@ int get_gi_kernel(DevCtx* ctx, const GiShape& sh, hipFunction_t* fn) {
     }
     std::vector<char> co;
     std::string err;
-    if (!comgr_assemble(emit_apply_gi_asm(sh), &co, &err)) return fail(RQ_ERR_PLAN, err);
+    const std::string src = emit_apply_gi_asm(sh);
+    if (!check_apply_gi_asm(src, sh, &err) || !comgr_assemble(src, &co, &err)) return fail(RQ_ERR_PLAN, err);
     hipModule_t mod = nullptr;
     hipFunction_t f = nullptr;
     if (hipModuleLoadData(&mod, co.data()) != hipSuccess ||
@@ -1238,12 +1260,16 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     int rc;
     const bool async = fin == Fin::Async;
     DecodePlan& pl = decode_plan_scratch();
-    const bool gi = g_apply_mode == 1;
     const GiShape& gsh = apply_gi_shape();
     if ((rc = plan_decode(p, n_blocks, eoff, roff, repair_esi, cnt, blk_map, po != nullptr, &pl, mx_hint))) return rc;
+    const uint32_t nw = pl.nw, max_e = pl.max_e, max_lds_e = pl.max_lds_e;
+    // The register-table apply's stream is laid out for the batch's largest e (~1.6 e^2 dwords per block
+    // and the kernel's slice offsets in 32 bits): it runs only while the whole stream stays within
+    // gi_stream_fits' bound; a batch beyond it (one block with e in the thousands) takes k_apply, whose
+    // working set is e x 64 bytes of X per block.
+    const bool gi = g_apply_mode == 1 && gi_stream_fits(max_e, nw, gsh);
     hipFunction_t gi_fn = nullptr;
     if (gi && (rc = get_gi_kernel(ctx, gsh, &gi_fn))) return rc;
-    const uint32_t nw = pl.nw, max_e = pl.max_e, max_lds_e = pl.max_lds_e;
     const bool need_general = pl.need_general, wide = pl.wide;
     const uint64_t xo = pl.xo, go = pl.go;
     const size_t nz = pl.nz;
@@ -2007,6 +2033,15 @@ struct rq_enc {
     DevBuf d_src, d_C, d_esi, d_out;
 };
 
+// AddSymbol's bookkeeping alone (rq_tracker_*): which ESIs are held, no symbol bytes.
+struct rq_tracker {
+    Params p{};
+    uint32_t T = 0;
+    std::vector<uint8_t> have;       // K flags (the decoder's fast bitmap)
+    uint32_t nfast = 0;
+    std::unordered_set<uint32_t> slow;  // repair ESIs held (the decoder's slow map keys)
+};
+
 struct rq_dec {
     Params p{};
     uint64_t size = 0;
@@ -2413,6 +2448,8 @@ int rq_debug_apply_gi_asm(uint32_t kc, uint32_t g, uint32_t pdg, uint32_t cpl, c
     if (!gi_shape_ok(sh))
         return fail(RQ_ERR_BAD_ARG, "apply shape: KC 4..16 (a multiple of 4, of 8 packed), G 4..6, PDG 1..2, CPL 1..2, <= 256 VGPRs");
     const std::string src = emit_apply_gi_asm(sh);
+    std::string cerr;
+    if (!check_apply_gi_asm(src, sh, &cerr)) return fail(RQ_ERR_PLAN, cerr);
     if (text_len) *text_len = src.size();
     if (text && cap) {
         const size_t n = std::min(cap - 1, src.size());
@@ -2428,9 +2465,54 @@ int rq_debug_apply_gi_asm(uint32_t kc, uint32_t g, uint32_t pdg, uint32_t cpl, c
     return RQ_OK;
 }
 
+int rq_debug_gi_stream(uint32_t e, uint32_t max_e, uint32_t solved, const uint8_t* X, const uint16_t* piv,
+                       const uint32_t* erased, const uint32_t* rep_uidx, uint32_t nr, uint32_t n_union, uint32_t T,
+                       uint32_t bi, uint32_t* out, size_t out_words, uint32_t layout[7]) {
+    const GiShape sh;  // the shipped shape, which the solvers write (xb_on)
+    if (e == 0 || e > max_e || (solved && (!X || !piv || !erased || !rep_uidx)) || !out || !layout)
+        return fail(RQ_ERR_BAD_ARG, "gi stream emulation arguments");
+    const GiLayout L = gi_layout(max_e, sh);
+    layout[0] = L.nslm; layout[1] = L.ngrm; layout[2] = L.er; layout[3] = L.of; layout[4] = L.ix;
+    layout[5] = L.ix_slice; layout[6] = L.block;
+    if ((uint64_t)(bi + 1) * L.block > out_words) return fail(RQ_ERR_BAD_ARG, "gi stream buffer too small");
+    for (uint32_t m = 0; solved && m < e; ++m)
+        if (piv[m] >= nr || rep_uidx[piv[m]] >= n_union) return fail(RQ_ERR_BAD_ARG, "pivot row out of range");
+    const uint32_t eoff[2] = {0, e}, roff[2] = {0, nr};
+    XbitsArgs a{};
+    a.erased_off = eoff;
+    a.erased = erased;
+    a.rep_off = roff;
+    a.rep_uidx = rep_uidx;
+    a.recv = reinterpret_cast<const uint8_t*>(uintptr_t(0x100000000ull));  // addresses only (header words)
+    a.r0 = reinterpret_cast<const uint8_t*>(uintptr_t(0x200000000ull));
+    a.data = reinterpret_cast<uint8_t*>(uintptr_t(0x300000000ull));
+    a.data_stride = (uint64_t)T * 65536;
+    a.gi = out;
+    a.L = L;
+    a.T = T;
+    a.n_union = n_union;
+    auto XF = [&](uint32_t k, uint32_t m) { return (uint32_t)X[(size_t)k * e + m]; };
+    auto PF = [&](uint32_t m) { return (uint32_t)piv[m]; };
+    for (uint32_t tid = 0; tid < 256; ++tid)  // the solvers' 256 threads, one after another
+        gi_stream<8, 5, 2>(a, bi, 0, e, solved != 0, tid, 256, XF, PF);
+    return RQ_OK;
+}
+
+int rq_debug_apply_gi_check(uint32_t kc, uint32_t g, uint32_t pdg, uint32_t cpl, const char* text) {
+    GiShape sh;
+    sh.KC = kc; sh.G = g; sh.PDG = pdg; sh.CPL = cpl & 0xff; sh.PACK = cpl >> 8;
+    if (!text || !gi_shape_ok(sh)) return fail(RQ_ERR_BAD_ARG, "apply shape or text");
+    std::string err;
+    return check_apply_gi_asm(text, sh, &err) ? RQ_OK : fail(RQ_ERR_PLAN, err);
+}
+
 uint32_t rq_debug_solve_mode(uint32_t mode) {
     const uint32_t old = g_solve_ip;
+#ifdef RQHIP_EXPERIMENTS
     if (mode <= 1) g_solve_ip = mode;
+#else
+    (void)mode;  // the release library has k_solve_pq only (k_solve_ip: experiments library)
+#endif
     return old;
 }
 
@@ -2439,6 +2521,8 @@ uint32_t rq_debug_apply_mode(uint32_t mode) {
     if (mode <= 1) g_apply_mode = mode;
     return old;
 }
+
+int rq_debug_gi_fits(uint32_t max_e, uint32_t n_solve) { return gi_stream_fits(max_e, n_solve, apply_gi_shape()) ? 1 : 0; }
 
 uint32_t rq_debug_decode_margin(uint32_t margin) {
     const uint32_t old = g_subset_margin;
@@ -2742,6 +2826,46 @@ int rq_decoder_add(rq_dec* d, uint32_t esi, const uint8_t* sym, size_t len, int*
     if (can_try) *can_try = d->p.K <= d->nfast + (uint32_t)d->slow.size();
     return RQ_OK;
 }
+
+rq_tracker* rq_tracker_create(uint64_t data_size, uint32_t T, int* err) {
+    int dummy;
+    if (!err) err = &dummy;
+    Params p;
+    const int rc = calc_params(data_size, T, &p);
+    if (rc) { *err = fail(rc, rc == RQ_ERR_SYMBOL_SIZE_ZERO ? "failed to calc params: symbol size cannot be zero"
+                                                           : "failed to calc params: k is too big"); return nullptr; }
+    rq_tracker* t = new rq_tracker();
+    t->p = p;
+    t->T = T;
+    t->have.assign(p.K, 0);
+    *err = RQ_OK;
+    return t;
+}
+
+uint32_t rq_tracker_k(const rq_tracker* t) { return t ? t->p.K : 0; }
+
+int rq_tracker_add(rq_tracker* t, uint32_t esi, size_t len, int* can_try) {
+    if (!t) return fail(RQ_ERR_BAD_ARG, "null tracker");
+    if (len != t->T) {  // the decoder's check and message (RQ/decoder.go:39-57)
+        char buf[96];
+        std::snprintf(buf, sizeof buf, "incorrect symbol size %zu, should be %u", len, t->T);
+        return fail(RQ_ERR_SYMBOL_SIZE, buf);
+    }
+    if (esi < t->p.K) {
+        if (!t->have[esi]) {
+            t->have[esi] = 1;
+            t->nfast++;
+        }
+    } else {
+        t->slow.insert(esi);
+    }
+    if (can_try) *can_try = t->p.K <= t->nfast + (uint32_t)t->slow.size();
+    return RQ_OK;
+}
+
+uint32_t rq_tracker_held(const rq_tracker* t) { return t ? t->nfast + (uint32_t)t->slow.size() : 0; }
+
+void rq_tracker_free(rq_tracker* t) { delete t; }
 
 // Decode: the library's fast path when every source symbol is held; otherwise the batched syndrome
 // decode on one block (subset of e + 8 received repairs first, all of them if that is

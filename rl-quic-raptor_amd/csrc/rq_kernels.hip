@@ -23,6 +23,7 @@
 #include "rfc6330_tables.h"
 #include "rq_device.hpp"
 #include "rq_kernels_common.hpp"
+#include "rq_gistream.hpp"
 
 namespace rq {
 
@@ -89,76 +90,8 @@ int launch_pack_rows(const PackArgs& a, void* stream) {
 }
 
 // ------------------------------ decode: X -> the register-table apply's stream ---------------
-// One workgroup per block of the solve list: X (bytes, row m = syndrome in pivot order, byte k =
-// output) becomes the dword stream of rq_device.hpp GiLayout: a header (status, e, the block's row
-// bases), per slice of KC outputs their row offsets, per group of G syndromes their row offsets, and per
-// slice, group and output the eight G-bit subsets idx_b = sum_t bit_b(X[k][G g + t]) << t, so that
-// sum_m X[k][m] s_m = sum_b alpha^b sum_g Tab_g[idx_b], where Tab_g holds the 2^G XORs of group g's
-// syndromes (the apply kernel, rq_applygi.cpp).  Unsolved blocks get a header with status 0 only.
-// Block bi's part of the stream from X given as X(k, m) (coefficient byte of syndrome m in output k) and
-// XP(m) (the received row, within the block, of syndrome m); nthr threads from tid.  An unsolved block
-// (solved = false) gets its header only.
-template <int KC, int G, int PDG, class XF, class PF, int PK = 0>
-__device__ void gi_stream(const XbitsArgs& a, uint32_t bi, uint32_t b, uint32_t e, bool solved, uint32_t tid,
-                          uint32_t nthr, XF X, PF XP) {
-    const GiLayout& L = a.L;
-    uint32_t* base = a.gi + (size_t)bi * L.block;
-    const uint32_t ngr = (e + G - 1) / G, nsl = (e + KC - 1) / KC;
-    if (tid < 16) {
-        uint64_t v = 0;
-        if (tid >= 4 && tid < 10) {
-            const uint32_t w = (tid - 4) >> 1;
-            const uint64_t addr = w == 0 ? (uint64_t)(a.recv + (size_t)a.rep_off[b] * a.T)
-                                : w == 1 ? (uint64_t)(a.r0 + (size_t)b * a.n_union * a.T)
-                                         : (uint64_t)(a.data + (size_t)b * a.data_stride);
-            v = (tid & 1) ? addr >> 32 : addr & 0xFFFFFFFFu;
-        }
-        base[tid] = tid == 0 ? (uint32_t)solved : tid == 1 ? e : tid == 2 ? ngr : (uint32_t)v;
-    }
-    if (!solved) return;
-    const uint32_t* E = a.erased + a.erased_off[b];
-    const uint32_t* RU = a.rep_uidx + a.rep_off[b];
-    const uint32_t T = a.T;
-    for (uint32_t i = tid; i < nsl * 16; i += nthr) {
-        const uint32_t sl = i >> 4, k = i & 15, ko = sl * KC + k;
-        base[L.er + i] = (k < (uint32_t)KC && ko < e) ? E[ko] * T : 0u;
-    }
-    for (uint32_t i = tid; i < (ngr + PDG + 1) * 16; i += nthr) {
-        const uint32_t q = i >> 4, w = i & 15, t = w >> 1, m = G * q + t;
-        uint32_t v = 0;
-        if (t < (uint32_t)G && m < e) {
-            const uint32_t j = XP(m);
-            v = (w & 1) ? RU[j] * T : j * T;
-        }
-        base[L.of + i] = v;
-    }
-    for (uint32_t i = tid; i < nsl * ngr * KC; i += nthr) {
-        const uint32_t k = i % KC, r = i / KC, g = r % ngr, sl = r / ngr, ko = sl * KC + k;
-        uint32_t x[G];
-#pragma unroll
-        for (int t = 0; t < G; ++t) {
-            const uint32_t m = G * g + t;
-            x[t] = (ko < e && m < e) ? (uint32_t)X(ko, m) : 0u;
-        }
-        uint32_t v[8];
-#pragma unroll
-        for (int bit = 0; bit < 8; ++bit) {
-            uint32_t sb = 0;
-#pragma unroll
-            for (int t = 0; t < G; ++t) sb |= ((x[t] >> bit) & 1u) << t;
-            v[bit] = sb;
-        }
-        if (PK) {  // two per dword: bits b = 2i (low half) and 2i + 1 (high half)
-            uint4* d = reinterpret_cast<uint4*>(base + L.ix + sl * L.ix_slice + g * 4 * KC + k * 4);
-            d[0] = make_uint4(v[0] | v[1] << 16, v[2] | v[3] << 16, v[4] | v[5] << 16, v[6] | v[7] << 16);
-        } else {
-            uint4* d = reinterpret_cast<uint4*>(base + L.ix + sl * L.ix_slice + g * 8 * KC + k * 8);
-            d[0] = make_uint4(v[0], v[1], v[2], v[3]);
-            d[1] = make_uint4(v[4], v[5], v[6], v[7]);
-        }
-    }
-}
-
+// gi_stream (rq_gistream.hpp) writes one block's part; k_xbits runs it for every block of the solve
+// list, and the solvers run it for the blocks they finish (xb_on).
 template <int KC, int G, int PDG, int PK = 0>
 __device__ void xbits_block(const XbitsArgs& a, uint32_t bi, uint32_t tid) {
     const uint32_t b = a.blk_map[bi];
@@ -410,6 +343,8 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
 
 
 
+#ifdef RQHIP_EXPERIMENTS
+// Experiments library only (rq_debug_solve_mode(1)): measured no faster than k_solve_pq<1, 4>.
 // The same solve in place (e <= 64 on the first e + margin received repairs): a row holds only its e
 // coefficient bytes, and the column eliminated at step k is reused for the identity column of that step's
 // pivot row (the classic in-place Gauss-Jordan inverse).  After step k, byte k of row j holds c_j =
@@ -520,6 +455,7 @@ __global__ void __launch_bounds__(64 * NW) k_solve_ip(SolveArgs a) {
         for (uint32_t k = lane; k < e; k += 64) xc[m * xs + k] = rb[pivl[k] * SW * 4 + m];
     if (tid == 0) a.status[b] = 1;
 }
+#endif
 
 // General solver for the blocks the fast solvers deferred: any e, every received repair.  The
 // received rows are taken in order and reduced against a Gauss-Jordan basis of the rows kept so far
@@ -667,9 +603,14 @@ static bool knob_on(const char* name, bool dflt) {
 }
 #endif
 
-// The first solve in place (k_solve_ip) or on [M | I] (k_solve_pq<1, 4>); rq_debug_solve_mode switches it.
+// The first solve in place (k_solve_ip, experiments library) or on [M | I] (k_solve_pq<1, 4>);
+// rq_debug_solve_mode switches it in experiments builds.
 uint32_t g_solve_ip = 0;
+#ifdef RQHIP_EXPERIMENTS
 static bool solve_in_place() { return g_solve_ip != 0; }
+#else
+static bool solve_in_place() { return false; }
+#endif
 
 int launch_solve(const SolveArgs& a_in, uint32_t n_blocks, bool need_general, bool wide, uint32_t max_lds_e,
                  void* stream, bool* xbits_done) {
@@ -724,8 +665,7 @@ int launch_solve(const SolveArgs& a_in, uint32_t n_blocks, bool need_general, bo
     }
 #else
     // e <= 64 on the first e + margin received repairs (statuses copied in by this launch)
-    if (solve_in_place()) hipLaunchKernelGGL((k_solve_ip<4>), dim3(n_blocks), dim3(256), 0, st, first);
-    else hipLaunchKernelGGL((k_solve_pq<1, 4>), dim3(n_blocks), dim3(256), 0, st, first);
+    hipLaunchKernelGGL((k_solve_pq<1, 4>), dim3(n_blocks), dim3(256), 0, st, first);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !need_general) return (int)e;
     if (wide) {  // blocks with 64 < e <= 128; the rare rank-deficient-on-64-rows block goes to k_solve
@@ -1083,11 +1023,18 @@ static void launch_apply_pd(const ApplyArgs& a, uint32_t kc, dim3 g, uint32_t ec
 int launch_apply(const ApplyArgs& a, uint32_t /*n_strips*/, uint32_t n_blocks, void* stream) {
     const hipStream_t st = (hipStream_t)stream;
     const uint32_t Td = a.T / 4;
-    uint32_t cpl = 1, best = 0xFFFFFFFFu;  // fewest padded columns, then the widest lanes
+    uint32_t cpl = 1;
+#ifdef RQHIP_EXPERIMENTS
+    // fewest padded columns, then the widest lanes (1, 2, 4 or 5 dword columns per lane)
+    uint32_t best = 0xFFFFFFFFu;
     for (uint32_t c : {1u, 2u, 4u, 5u}) {
         const uint32_t w = 64 * c, pad = (Td + w - 1) / w * w - Td;
         if (pad <= best) { best = pad; cpl = c; }
     }
+#endif
+    // The release library runs k_apply only for the batches beyond the register-table apply's stream
+    // bound (rq_engine.cpp gi_stream_fits: some block with e > 512) and rq_debug_apply_mode(0): one dword
+    // column per lane.
     // balanced slices of KC <= 8 outputs (measured at e ~ 58, K=1024 T=1200: KC 4/8/12/16/20/28 ->
     // 244/210/238/254/282/324 us; small slices keep the accumulators few, so more waves fit per SIMD),
     // the slice's tables (20 B per coefficient) for MC syndromes within ~20 KB of LDS
@@ -1104,12 +1051,16 @@ int launch_apply(const ApplyArgs& a, uint32_t /*n_strips*/, uint32_t n_blocks, v
 #endif
     const uint32_t nu = (Td + 64 * cpl - 1) / (64 * cpl) * n_blocks;
     const dim3 g((nu + 7) / 8 * 8 * np);
+#ifdef RQHIP_EXPERIMENTS
     switch (cpl) {
         case 1: launch_apply_pd<1>(a, kc, g, ec, lds, st, nu, np, MC); break;
         case 2: launch_apply_pd<2>(a, kc, g, ec, lds, st, nu, np, MC); break;
         case 4: launch_apply_pd<4>(a, kc, g, ec, lds, st, nu, np, MC); break;
         default: launch_apply_pd<5>(a, kc, g, ec, lds, st, nu, np, MC); break;
     }
+#else
+    launch_apply_pd<1>(a, kc, g, ec, lds, st, nu, np, MC);
+#endif
     return (int)hipGetLastError();
 }
 

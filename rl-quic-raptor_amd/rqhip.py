@@ -48,7 +48,9 @@ EXPORTED = (
     "rq_decode_blocks_host", "rq_host_alloc", "rq_host_free", "rq_debug_colprog_passes",
     "rq_debug_shard_plan", "rq_debug_virtual_shards", "rq_debug_tuple", "rq_stream_release", "rq_shutdown",
     "rq_launch_timing", "rq_launch_time", "rq_debug_pair_emulate", "rq_debug_dma4_emulate", "rq_debug_decode_plan",
-    "rq_debug_assemble", "rq_debug_colprog_bound", "rq_debug_cache_roundtrip",
+    "rq_debug_assemble", "rq_debug_colprog_bound", "rq_debug_cache_roundtrip", "rq_debug_gi_fits",
+    "rq_debug_apply_gi_check", "rq_debug_gi_stream",
+    "rq_tracker_create", "rq_tracker_k", "rq_tracker_add", "rq_tracker_held", "rq_tracker_free",
 )
 
 
@@ -174,6 +176,11 @@ def _load(path):
         "rq_decoder_add": ([vp, ctypes.c_uint32, u8p, ctypes.c_size_t, ip], ctypes.c_int),
         "rq_decoder_decode": ([vp, u8p, ip], ctypes.c_int),
         "rq_decoder_free": ([vp], None),
+        "rq_tracker_create": ([ctypes.c_uint64, ctypes.c_uint32, ip], vp),
+        "rq_tracker_k": ([vp], ctypes.c_uint32),
+        "rq_tracker_add": ([vp, ctypes.c_uint32, ctypes.c_size_t, ip], ctypes.c_int),
+        "rq_tracker_held": ([vp], ctypes.c_uint32),
+        "rq_tracker_free": ([vp], None),
         "rq_encode_batch": ([ctypes.POINTER(EncodeDesc)], ctypes.c_int),
         "rq_decode_batch": ([ctypes.POINTER(DecodeDesc)], ctypes.c_int),
         "rq_decode_batch_async": ([ctypes.POINTER(DecodeDesc)], ctypes.c_int),
@@ -191,6 +198,11 @@ def _load(path):
         "rq_debug_decode_margin": ([ctypes.c_uint32], ctypes.c_uint32),
         "rq_debug_apply_mode": ([ctypes.c_uint32], ctypes.c_uint32),
         "rq_debug_solve_mode": ([ctypes.c_uint32], ctypes.c_uint32),
+        "rq_debug_gi_fits": ([ctypes.c_uint32, ctypes.c_uint32], ctypes.c_int),
+        "rq_debug_gi_stream": ([ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp, vp, ctypes.c_uint32,
+                                ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, vp, ctypes.c_size_t, u32p], ctypes.c_int),
+        "rq_debug_apply_gi_check": ([ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_char_p],
+                                    ctypes.c_int),
         "rq_debug_apply_gi_asm": ([ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_char_p,
                                    ctypes.c_size_t,
                                    ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
@@ -526,6 +538,39 @@ def NewRaptorQDecoder(dataSize, L):
     if not h:
         _check(err.value)
     return RaptorQDecoder(h, lib().rq_decoder_k(h), L, dataSize)
+
+
+class RaptorQTracker:
+    """The shim's RaptorQTracker (go/fec/raptorq_rqhip.go): RaptorQDecoder.AddSymbol's bookkeeping and
+    bool without the symbol bytes (rq_tracker_*), for a receiver that stages symbols itself."""
+
+    def __init__(self, handle, K, L):
+        self._h = handle
+        self.K = K
+        self.L = L
+
+    def AddSymbol(self, id, data):
+        can = ctypes.c_int(0)
+        _check(lib().rq_tracker_add(self._h, id, len(data), ctypes.byref(can)))
+        return bool(can.value)
+
+    def Held(self):
+        return lib().rq_tracker_held(self._h)
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.rq_tracker_free(self._h)
+            self._h = None
+
+
+def NewRaptorQTracker(dataSize, L):
+    if dataSize < 0 or L <= 0:
+        raise RaptorQError(RQ_ERR_BAD_ARG, "bad dataSize or L")
+    err = ctypes.c_int(0)
+    h = lib().rq_tracker_create(dataSize, L, ctypes.byref(err))
+    if not h:
+        _check(err.value)
+    return RaptorQTracker(h, lib().rq_tracker_k(h), L)
 
 
 def RaptorQEncodeBlock(data, N, K, L):

@@ -18,13 +18,15 @@ def test_clean_build_links(tmp_path):
     shutil.copytree(PKG / "fecquic", dst / "fecquic")
     shutil.copy(PKG / "Makefile", dst / "Makefile")
     (tmp_path / "include").mkdir()
-    shutil.copy(ROOT / "include" / "rqhip.h", tmp_path / "include" / "rqhip.h")
+    for h in ("rqhip.h", "rqhip_debug.h"):
+        shutil.copy(ROOT / "include" / h, tmp_path / "include" / h)
     r = subprocess.run(["make", "-s", "-C", str(dst), "-j8", "all"], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-4000:]
     so = dst / "build" / "librqhip.so"
     for f in ("librqhip.so", "librqcpu.so", "libfecquic.so", "fecquic", "raptorq_eval"):
         assert (dst / "build" / f).exists(), f
     L = ctypes.CDLL(str(so))
-    txt = re.sub(r"/\*.*?\*/", "", (ROOT / "include/rqhip.h").read_text(), flags=re.S)
+    txt = re.sub(r"/\*.*?\*/", "", (ROOT / "include/rqhip.h").read_text() + (ROOT / "include/rqhip_debug.h").read_text(),
+                 flags=re.S)
     for name in sorted(set(re.findall(r"\b(rq_[a-z_]+)\s*\(", txt))):
         assert hasattr(L, name), name

@@ -1,6 +1,6 @@
 """C-ABI boundary checks that need no GPU: the library loads, exports every symbol declared in
-include/rqhip.h, reports parameters and the reference's error strings, and fails loudly (no
-CPU fallback) when no device is present."""
+include/rqhip.h (the product ABI) and include/rqhip_debug.h (test-only diagnostics), reports parameters
+and the reference's error strings, and fails loudly (no CPU fallback) when no device is present."""
 import ctypes
 import re
 from pathlib import Path
@@ -11,19 +11,28 @@ import pytest
 ROOT = Path(__file__).resolve().parent.parent
 
 
-def header_functions():
-    txt = (ROOT / "include/rqhip.h").read_text()
+def header_functions(name="rqhip.h"):
+    txt = (ROOT / "include" / name).read_text()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
     return sorted(set(re.findall(r"\b(rq_\w+)\s*\(", txt)))
 
 
 def test_header_symbols_exported(rq):
-    names = header_functions()
+    names = sorted(set(header_functions()) | set(header_functions("rqhip_debug.h")))
     assert len(names) >= 20
     L = rq.lib()
     for n in names:
         assert hasattr(L, n), n
     assert sorted(rq.EXPORTED) == names
+
+
+def test_product_header_has_only_product_entries():
+    """include/rqhip.h is what the cgo shim binds: the reference's replacements, the batch paths, device
+    control and the bench's launch timing.  The diagnostics live in the test-only rqhip_debug.h."""
+    prod, dbg = header_functions(), header_functions("rqhip_debug.h")
+    assert not [n for n in prod if n.startswith("rq_debug_")], prod
+    assert dbg and all(n.startswith("rq_debug_") for n in dbg), dbg
+    assert not set(prod) & set(dbg)
 
 
 def test_params_and_errors(rq):
@@ -124,3 +133,30 @@ def test_decode_host_plan_argument_errors(rq):
     db.erased[0] = 1024  # an erased ESI at K
     with pytest.raises(rq.RaptorQError):
         db.host_plan_us(1)
+
+
+def test_tracker_bookkeeping_matches_the_decoder(rq, oracle):
+    """rq_tracker_* (the receiver's AddSymbol bookkeeping without the bytes) returns the
+    bool the oracle decoder's add_symbol returns (RQ/decoder.go:47,57: K <= unique symbols held) on the same
+    ESI sequence -- sources and repairs in random order with duplicates -- and refuses a wrong size with
+    the decoder's message."""
+    rng = np.random.default_rng(5)
+    for K, T, N, loss in ((26, 16, 32, 0.15), (64, 40, 80, 0.10), (256, 8, 282, 0.05), (5, 12, 8, 0.3)):
+        size = K * T - int(rng.integers(0, T))
+        data = bytes(rng.integers(0, 256, size, dtype=np.uint8))
+        enc = oracle.OracleEncoder(data, T)
+        keep = [i for i in range(N) if rng.random() >= loss]
+        seq = list(rng.permutation(keep)) + [int(x) for x in rng.choice(keep, 5)]  # + duplicates
+        tr = rq.NewRaptorQTracker(size, T)
+        dec = oracle.OracleDecoder(size, T)
+        assert tr.K == (size + T - 1) // T
+        got = [tr.AddSymbol(int(e), bytes(T)) for e in seq]
+        want = [dec.add_symbol(int(e), enc.gen_symbol(int(e)).tobytes()) for e in seq]
+        assert got == want, (K, seq)
+        assert tr.Held() == len(set(int(e) for e in seq))
+        with pytest.raises(rq.RaptorQError, match="incorrect symbol size %d, should be %d" % (T - 1, T)):
+            tr.AddSymbol(0, bytes(T - 1))
+    import ctypes
+    err = ctypes.c_int(0)
+    assert not rq.lib().rq_tracker_create(100, 0, ctypes.byref(err)) and err.value == rq.RQ_ERR_SYMBOL_SIZE_ZERO
+    assert "symbol size cannot be zero" in rq.lib().rq_last_error().decode()

@@ -1,11 +1,12 @@
-"""GPU: the decode's alternative kernels give the same bytes (apply and first solve).
+"""GPU: the decode's two apply kernels give the same bytes.
 
 The register-table apply (k_xbits + the generated rq_apply_gi kernel, rq_applygi.cpp; the default) and
 k_apply's v_perm byte tables (rq_debug_apply_mode(0)) compute x_E = g_E ^ X s from the same X.  Each case
 decodes one batch with both and compares every block's bytes and status; solved blocks must equal their
 source, unsolved ones keep their bytes.  Cases cover e from 1 to past 128 in one batch (a slice of 16
 outputs partly used, a last group of 1..5 syndromes), T not a multiple of 256 (a strip with lanes off)
-and T = 8 (two dwords), and a block left unsolved beside solved ones."""
+and T = 8 (two dwords), and a block left unsolved beside solved ones.  (The in-place first solver lives in
+the experiments library: tests/test_gpu_experimental_programs.py.)"""
 import numpy as np
 import pytest
 import torch
@@ -90,49 +91,16 @@ def test_apply_unsolved_block_keeps_bytes(gpu, rq):
     assert torch.equal(d1[0], src[0]) and torch.equal(d1[2], src[2])
 
 
-def _decode_solve_modes(rq, K, T, data, erased, reps, rep):
-    res = []
-    for mode in (0, 1):
-        d = data.clone()
-        old = rq.solve_mode(mode)
-        try:
-            st = rq.DecodeBatch(K, T, erased, reps).run(d, rep)
-            torch.cuda.synchronize()
-        finally:
-            rq.solve_mode(old)
-        res.append((d, np.array(st)))
-    return res
-
-
-@pytest.mark.parametrize("K,T,R,erase_counts", [
-    (1024, 1200, 76, [55, 1, 16, 17, 33, 48, 49, 64, 2, 3, 0, 63]),
-    (256, 256, 80, [64, 70, 5, 1, 32]),
-    (64, 8, 20, [20, 19, 1, 6]),
-])
-def test_in_place_solve_agrees(gpu, rq, K, T, R, erase_counts):
-    """k_solve_ip (rows of e bytes, in-place Gauss-Jordan) and k_solve_pq<1, 4> give the same statuses
-    and bytes; e > 64 takes the wide / general solvers either way."""
-    src, data, erased, reps, rep = _case(rq, gpu, K, T, R, erase_counts, 3 * K + T)
-    (d0, st0), (d1, st1) = _decode_solve_modes(rq, K, T, data, erased, reps, rep)
-    assert np.array_equal(st0, st1)
-    for b, ne in enumerate(erase_counts):
-        assert torch.equal(d0[b], d1[b]), (b, ne)
-        if st1[b] == 1:
-            assert torch.equal(d1[b], src[b]), (b, ne)
-
-
-def test_in_place_solve_margin_fallback(gpu, rq):
-    """With no row margin the first pass sees exactly e rows: blocks rank-deficient on them go to the
-    general solver under either first solver, with the same results."""
-    K, T, R = 128, 256, 40
-    src, data, erased, reps, rep = _case(rq, gpu, K, T, R, [40, 30, 20, 39, 8, 16], 11)
-    old = rq.lib().rq_debug_decode_margin(0)
-    try:
-        (d0, st0), (d1, st1) = _decode_solve_modes(rq, K, T, data, erased, reps, rep)
-    finally:
-        rq.lib().rq_debug_decode_margin(old)
-    assert np.array_equal(st0, st1)
-    assert torch.equal(d0, d1)
-    for b in range(len(st1)):
-        if st1[b] == 1:
-            assert torch.equal(d1[b], src[b]), b
+def test_apply_stream_bound_falls_back(gpu, rq):
+    """the register-table stream is laid out for the batch's largest e (~1.6 e^2 dwords per
+    block).  A batch holding one block with e = 560 beside low-e blocks is past the bound and takes
+    k_apply (every block recovered, the same bytes as rq_debug_apply_mode(0)); a single block at the
+    bound (e = 512) takes the register-table apply with its largest stream, bit-identical to k_apply."""
+    K, T = 1024, 64
+    assert rq.lib().rq_debug_gi_fits(560, 5) == 0 and rq.lib().rq_debug_gi_fits(512, 1) == 1
+    for ec, R in (([560, 3, 1, 7, 12], 600), ([512], 552)):
+        src, data, erased, reps, rep = _case(rq, gpu, K, T, R, ec, 5 + ec[0])
+        (d0, st0), (d1, st1) = _decode_both(rq, K, T, data, erased, reps, rep)
+        assert list(st1) == [1] * len(ec) and list(st0) == list(st1), (ec, st0, st1)
+        assert torch.equal(d0, d1), ec
+        assert torch.equal(d1, src), ec

@@ -229,9 +229,11 @@ def test_config3_zero_overhead_statuses_match_oracle(gpu, rq):
 
 def test_decode_descriptor_fetch_with_a_full_grid(gpu, rq):
     """218 blocks at K=1024 T=1200 are 1 022 64-column items: the syndrome launch's persistent grid takes
-    every resident slot (1 024 one-wave workgroups), so the workgroup that fetches the decode's
-    descriptors from the pinned staging runs only once a program workgroup has finished.  Every block
-    decodes back to its source, sync and async."""
+    every resident slot (its 1 022 items round up to 1 024 one-wave workgroups), so the descriptors travel
+    by the fallback (launch_col carries the fetch only when the grid leaves a slot free; here the
+    side-stream upload runs and the caller's stream waits for it).  Every block decodes back to its
+    source, sync and async.  The fetch itself is exercised by every config-3 decode (one-wave workgroups)
+    and, at four-wave workgroups, by tests/test_gpu_experimental_programs.py."""
     K, T, N, nb, n_erase = 1024, 1200, 1100, 218, 55
     esis = list(range(K, N))
     src = _src(gpu, nb, K, T, 218)

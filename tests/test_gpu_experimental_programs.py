@@ -28,11 +28,11 @@ VARIANTS = {
 }
 
 
-def _run(args, knobs, timeout=150):
+def _run(args, knobs, timeout=150, stderr=False):
     env = dict(os.environ, RQHIP_LIB=str(EXP), **knobs)
     r = subprocess.run([sys.executable] + args, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
-    return r.stdout
+    return (r.stdout, r.stderr) if stderr else r.stdout
 
 
 @pytest.mark.parametrize("name", sorted(VARIANTS))
@@ -50,3 +50,21 @@ def test_variant_encode_decode_step(name):
     post-timing bytes + statuses."""
     out = _run(["tools/experiments/bench_exp.py", "--steps", "1", "--warmup", "0", "--cpu-sample", "0"], VARIANTS[name])
     assert '"decode_ok_fraction": 1.0' in out and '"post_timing_check": "bytes+statuses"' in out, out
+
+
+def test_in_place_solve_agrees():
+    """k_solve_ip (experiments library, rq_debug_solve_mode(1)) and the shipped k_solve_pq<1, 4> give the
+    same statuses and bytes, with and without the first pass's row margin
+    (tools/experiments/solve_ip_check.py)."""
+    out = _run(["tools/experiments/solve_ip_check.py"], {})
+    assert out.count("ok ") == 4, out
+
+
+def test_descriptor_fetch_with_four_wave_workgroups():
+    """the decode's descriptor fetch rides on the syndrome launch's spare workgroups in 4 KiB x W
+    round trips; the release library runs W = 1, so the per-trip / chunk arithmetic at W = 4 is exercised
+    here (RQHIP_WG=4): the launch must carry the fetch at W = 4 (its logged shape) and every block of a
+    config-3 decode must come back bit-exact, sync and async (tools/experiments/fetch_wg_check.py)."""
+    out, err = _run(["tools/experiments/fetch_wg_check.py"], {"RQHIP_WG": "4", "RQHIP_FETCH_LOG": "1"}, stderr=True)
+    assert out.strip().endswith("ok"), out
+    assert re.search(r"\[fetch\] carried=1 W=4 ", err), err[-2000:]

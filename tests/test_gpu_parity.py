@@ -258,3 +258,107 @@ def test_decode_async_back_to_back(gpu, rq):
     # the async call refuses pageable status memory
     d = db._desc(data, rep, np.zeros(nb, np.int32), None)
     assert rq.lib().rq_decode_batch_async(d) == rq.RQ_ERR_BAD_ARG
+
+
+class _StagedBlock:
+    """Python mirror of go/fecquic/rq_stage.go + rq_batchdec.go for one block: ingest copies each symbol
+    once into the block's pinned staging (source ESI e at row e, repairs appended from row K), the
+    bookkeeping is the rq_tracker (AddSymbol's bool without the bytes), and the decode hands the staged
+    rows to rq_decode_blocks_host where they lie (a gather only when a row is missing below the repairs)."""
+
+    def __init__(self, rq, size, N, K, T):
+        import ctypes
+        self.rq, self.N, self.K, self.T, self.size = rq, N, K, T, size
+        self.ptr = rq.lib().rq_host_alloc(N * T)
+        assert self.ptr
+        self.buf = np.ctypeslib.as_array((ctypes.c_uint8 * (N * T)).from_address(self.ptr))
+        self.buf[:] = 0xA5  # stale bytes of a reused buffer
+        self.row_of = {}
+        self.n_rep = 0
+        self.tracker = rq.NewRaptorQTracker(size, T)
+        self.haveU = 0
+
+    def ingest(self, esi, sym):
+        if esi in self.row_of:
+            return None  # a duplicate: dropped at ingest
+        row = esi if esi < self.K else self.K + self.n_rep
+        self.n_rep += esi >= self.K
+        self.buf[row * self.T:(row + 1) * self.T] = np.frombuffer(sym, np.uint8)
+        self.row_of[esi] = row
+        inc = self.tracker.AddSymbol(esi, sym)
+        self.haveU += inc
+        return inc
+
+    def decode_args(self):
+        kl = self.tracker.K
+        reps = sorted((e for e in self.row_of if e >= kl), key=lambda e: self.row_of[e])
+        data = self.buf[:kl * self.T]
+        if all(self.row_of[e] == kl + j for j, e in enumerate(reps)):
+            rows = self.buf[kl * self.T:(kl + len(reps)) * self.T].reshape(-1, self.T)
+            gathered = False
+        else:
+            rows = np.stack([self.buf[self.row_of[e] * self.T:(self.row_of[e] + 1) * self.T] for e in reps]) \
+                if reps else np.zeros((0, self.T), np.uint8)
+            gathered = True
+        erased = [e for e in range(kl) if e not in self.row_of]
+        return data, erased, reps, rows, gathered
+
+    def free(self):
+        self.rq.lib().rq_host_free(self.ptr)
+
+
+@pytest.mark.parametrize("K,T,N,loss,seed,short", [(64, 1200, 80, 0.10, 1, False), (26, 1500, 32, 0.15, 2, False),
+                                                   (256, 64, 282, 0.05, 3, False), (5, 1100, 8, 0.3, 4, False),
+                                                   (64, 1200, 80, 0.10, 6, True)])
+def test_staged_receiver_matches_oracle(gpu, rq, oracle, K, T, N, loss, seed, short):
+    """The Go receiver's staged path on the shapes of test_decoder_matches_oracle: the
+    tracker's bools equal the oracle decoder's, symbol by symbol, in arrival order with duplicates; the
+    staged rows decode through rq_decode_blocks_host (all ready blocks of a trial in one call) to the
+    oracle's (ok, bytes).  short: last blocks of a file (library K < the wrapper K, so ESIs between them
+    are repairs staged at source rows)."""
+    rng = np.random.default_rng(seed)
+    ready, gathered = [], 0
+    for trial in range(6):
+        size = (K * T - int(rng.integers(0, T))) if not short else (int(rng.integers(K // 3, K - 3)) * T - 11)
+        data = rand_bytes(rng, size)
+        ref_enc = oracle.OracleEncoder(data, T)
+        syms = [ref_enc.gen_symbol(i).tobytes() for i in range(N)]
+        keep = [i for i in range(N) if rng.random() >= loss]
+        arrival = list(rng.permutation(keep)) + [int(x) for x in rng.choice(keep, 3)]
+        sb = _StagedBlock(rq, size, N, K, T)
+        rdec = oracle.OracleDecoder(size, T)
+        for e in arrival:
+            e = int(e)
+            want = rdec.add_symbol(e, syms[e])
+            got = sb.ingest(e, syms[e])
+            assert got is None or got == want, (trial, e)
+        try:
+            ref = rdec.decode()
+        except RuntimeError:
+            assert sb.haveU == 0 or sb.tracker.Held() < sb.tracker.K
+            sb.free()
+            continue
+        ready.append((sb, ref, data))
+    try:
+        assert ready
+        args = [sb.decode_args() for sb, _, _ in ready]
+        gathered = sum(a[4] for a in args)
+        kl = ready[0][0].tracker.K
+        same_k = [i for i, (sb, _, _) in enumerate(ready) if sb.tracker.K == kl]
+        st = rq.decode_blocks_host(kl, T, [args[i][:4] for i in same_k])
+        for j, i in enumerate(same_k):
+            sb, ref, data = ready[i]
+            assert (st[j] == 1) == ref[0], (i, st[j])
+            if ref[0]:
+                assert bytes(sb.buf[:sb.size]) == ref[1] == data
+        for i in set(range(len(ready))) - set(same_k):  # other library K (short blocks): one call each
+            sb, ref, data = ready[i]
+            st = rq.decode_blocks_host(sb.tracker.K, T, [args[i][:4]])
+            assert (st[0] == 1) == ref[0]
+            if ref[0]:
+                assert bytes(sb.buf[:sb.size]) == ref[1] == data
+        if not short:
+            assert gathered == 0  # full blocks: every decode used the staged rows as they lie
+    finally:
+        for sb, _, _ in ready:
+            sb.free()

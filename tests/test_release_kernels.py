@@ -1,9 +1,11 @@
 """The release library carries only what ships.
 
-The decode solvers measured and not shipped (k_solve_fast / pm / reg / lean, the pinfo-column PF
-variant, other wave counts), the unshipped k_apply shapes, and the pair / four-row-staging column
-programs live in experiments-only translation units (rq_kernels_exp.hip, rq_colasm_exp.cpp,
-rq_colprog_exp.cpp) linked into build_exp/librqhip.so alone.  This test reads the code objects embedded
+The decode solvers measured and not shipped (k_solve_fast / pm / reg / lean, the in-place k_solve_ip,
+the pinfo-column PF variant, other wave counts), the unshipped k_apply shapes (wider lanes, other
+slices), and the pair / four-row-staging column programs are built into build_exp/librqhip.so alone
+(experiments-only translation units rq_kernels_exp.hip, rq_colasm_exp.cpp, rq_colprog_exp.cpp, and
+RQHIP_EXPERIMENTS sections).  k_apply<4|8, 1, ...> ships: it is the decode's apply for a batch beyond
+the register-table stream's bound (rq_engine.cpp gi_stream_fits, some block with e > 512).  This test reads the code objects embedded
 in build/librqhip.so (the kernel descriptors' `.kd` symbols) and requires exactly the kernels the engine
 dispatches; the generated column programs are assembled at run time and are not in the file.  CPU only."""
 import re
@@ -15,7 +17,6 @@ import pytest
 import rqhip
 
 ROOT = Path(__file__).resolve().parent.parent
-CPLS = (1, 2, 4, 5)  # launch_apply's lane widths (fewest padded columns for T)
 SHIPPED = {
     "void rq::k_solve_pq<1, 4, false>(rq::SolveArgs)",
     "void rq::k_solve_pq<2, 4, false>(rq::SolveArgs)",
@@ -23,10 +24,8 @@ SHIPPED = {
     "rq::k_pack_rows(rq::PackArgs)",
     "rq::k_gather(rq::DevParams, unsigned char const*, unsigned int, unsigned int const*, unsigned int, unsigned char*)",
     "void rq::k_xbits<8, 5, 2, 0>(rq::XbitsArgs)",
-    "void rq::k_solve_ip<4>(rq::SolveArgs)",
-} | {
-    "void rq::k_apply<%d, %d, 2, %d, true>(rq::ApplyArgs, unsigned int, unsigned int, unsigned int)" % (kc, c, occ)
-    for c in CPLS for kc, occ in ((4, 4), (8, 3))
+    "void rq::k_apply<4, 1, 2, 4, true>(rq::ApplyArgs, unsigned int, unsigned int, unsigned int)",
+    "void rq::k_apply<8, 1, 2, 3, true>(rq::ApplyArgs, unsigned int, unsigned int, unsigned int)",
 }
 
 
@@ -63,5 +62,6 @@ def test_experiments_library_keeps_the_variants():
         pytest.skip(str(ex))
     got = kernels(rqhip.EXP_LIB_PATH)
     assert SHIPPED <= got
-    for k in ("k_solve_fast", "k_solve_pm", "k_solve_reg", "k_solve_lean", "k_solve_pq<1, 4, true>"):
+    for k in ("k_solve_fast", "k_solve_pm", "k_solve_reg", "k_solve_lean", "k_solve_pq<1, 4, true>", "k_solve_ip<4>",
+              "k_apply<8, 5, 2, 3, true>"):
         assert any(k in n for n in got), k
