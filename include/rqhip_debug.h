@@ -27,14 +27,14 @@ extern "C" {
  *                 n_remaining_rows, n_out}. */
 int rq_debug_colprog_eval(uint32_t K, uint32_t T, const uint32_t* esi, uint32_t n_out, const uint8_t* src,
                           uint8_t* out, uint32_t stats[12]);
-/* Allocate the column program (opts = {n_vgpr, n_agpr, la_load, la_reload, max_vmem, n_lds + 1},
- * 0 = default), emulate the machine program on one block when src/out are given (checks vmcnt and
+/* Allocate the column program (opts = {n_vgpr, n_agpr, la_load, la_reload, max_vmem, n_lds + 1,
+ * cross-item prefetch rows + 1, its batch, its gap}, 0 = default), emulate the machine program on one block when src/out are given (checks vmcnt and
  * lgkmcnt waits and scratch ordering), and optionally return its gfx950 assembly (size first with
  * NULL).  stats[0..17] = {instructions, valu, src loads, out stores, spill stores, spill loads,
  * accw, accr, waits, nops, unprefetched reloads, scratch slots, ir nodes, xtimes, LDS spill
  * stores, LDS reloads, lgkm waits, LDS slots}. */
 int rq_debug_colprog_emulate(uint32_t K, uint32_t T, const uint32_t* esi, uint32_t n_out, const uint8_t* src,
-                             uint8_t* out, const uint32_t opts[6], uint32_t stats[18], char* asm_buf, size_t asm_cap,
+                             uint8_t* out, const uint32_t opts[9], uint32_t stats[18], char* asm_buf, size_t asm_cap,
                              size_t* asm_len);
 /* Assemble the column program in process (amd_comgr) and return the code object size. */
 int rq_debug_colprog_assemble(uint32_t K, const uint32_t* esi, uint32_t n_out, size_t* code_bytes);

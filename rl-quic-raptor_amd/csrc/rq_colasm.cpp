@@ -43,6 +43,7 @@ struct Allocator {
     uint64_t inflight[512];                         // vector-memory load into the register (seq) or 0
     uint64_t linflight[512];                        // LDS load into the register (lgkm seq) or 0
     uint8_t pinned[512];
+    uint8_t reserved[512];                          // cross-item prefetch: head register handed to the next item
     int last_accw[512];                             // instruction index of the last ACCW into an AGPR
     std::vector<int> freeV, freeA;
     std::vector<int32_t> free_slots, free_lslots;
@@ -260,7 +261,7 @@ struct Allocator {
     }
     void release(int r) {
         owner[r] = -1;
-        (is_agpr(r) ? freeA : freeV).push_back(r);
+        if (!reserved[r]) (is_agpr(r) ? freeA : freeV).push_back(r);
     }
     void kill(uint32_t v) {  // value dead: free register and scratch slot
         if (reg[v] >= 0) { release(reg[v]); reg[v] = -1; }
@@ -334,6 +335,38 @@ struct Allocator {
         owner[r] = (int32_t)v; reg[v] = (int16_t)r;
         issued[v] = 1;
     }
+    // Cross-item prefetch: head register r is handed to the next item from here on.  Its value (if any)
+    // moves to a free AGPR, else out like an eviction; a load still in flight into it completes first.
+    void vacate(int r) {
+        if (inflight[r]) wait_seq(inflight[r]);
+        if (linflight[r]) wait_lseq(linflight[r]);
+        if (owner[r] >= 0) {
+            mp->st.cip_evict++;
+            if (!is_agpr(r) && !freeA.empty()) {
+                const int a = freeA.back();
+                freeA.pop_back();
+                const int32_t v = owner[r];
+                emit(MI_ACCW, a, r);
+                mp->st.accw++;
+                last_accw[a] = (int)mp->ins.size() - 1;
+                owner[a] = v; reg[v] = (int16_t)a; owner[r] = -1;
+            } else {
+                spill_out(r);
+            }
+        } else {
+            std::vector<int>& fl = is_agpr(r) ? freeA : freeV;
+            fl.erase(std::remove(fl.begin(), fl.end(), r), fl.end());
+        }
+        reserved[r] = 1;
+    }
+    // head loads [f, f + nb) for the next item, issued back to back by one MI_PFX: room for all of them
+    // in the vmcnt budget first
+    void issue_pfx(uint32_t f, uint32_t nb) {
+        for (uint32_t k = 0; k < nb; ++k) vacate(mp->cip_reg[f + k]);
+        if (seq - retired + nb > o.max_vmem) wait_seq(seq + nb - o.max_vmem);
+        for (uint32_t k = 0; k < nb; ++k) issue_vmem();
+        emit(MI_PFX, -1, -1, -1, -1, (f << 16) | nb);
+    }
     // operand v into a VGPR (pinned by the caller)
     int to_vgpr(uint32_t v) {
         int r = reg[v];
@@ -378,7 +411,9 @@ struct Allocator {
         for (uint32_t q = 0; q < o.dma4; ++q) free_quads.push_back(q);
         issued.assign(nv, 0);
         dma_seq.assign(nv, 0);
-        for (int r = 0; r < 512; ++r) { owner[r] = -1; inflight[r] = 0; linflight[r] = 0; pinned[r] = 0; last_accw[r] = -100; }
+        for (int r = 0; r < 512; ++r) {
+            owner[r] = -1; inflight[r] = 0; linflight[r] = 0; pinned[r] = 0; reserved[r] = 0; last_accw[r] = -100;
+        }
         for (int r = (int)o.n_vgpr - 1; r >= 0; --r) freeV.push_back(r);
         for (int r = REG_A0 + (int)o.n_agpr - 1; r >= REG_A0; --r) freeA.push_back(r);
         std::vector<uint32_t> loads;
@@ -403,8 +438,36 @@ struct Allocator {
                 emit(MI_DMAT, 0, -1, -1, -1, 0);
             }
         }
+        // Cross-item prefetch: the first cip rows (loads with uses) are in flight at the item's start,
+        // issued by the previous item's tail into the top VGPRs (the allocator sees them as the item's first
+        // loads: its vmcnt counts then also cover the previous item's last stores, conservatively).  From
+        // the node after the last source load on, cip_batch of them every cip_gap nodes are re-issued for
+        // the next item into the same registers, vacated first.
+        const uint32_t n_cip = o.cip && !o.dma4 && !o.la_dma ? std::min<uint32_t>({o.cip, (uint32_t)ld.size(), o.n_vgpr / 2}) : 0;
+        uint32_t t_pf = 0, cip_done = 0;
+        for (uint32_t k = 0; k < n_cip; ++k) {
+            const uint32_t v = ld[k];
+            const int r = (int)o.n_vgpr - 1 - (int)k;
+            freeV.erase(std::remove(freeV.begin(), freeV.end(), r), freeV.end());
+            const uint64_t q = issue_vmem();
+            emit(MI_HEAD, r, -1, -1, -1, ir.nodes[v].imm);
+            mp->st.ldsrc++;
+            inflight[r] = q;
+            pend_loads.push_back({q, r});
+            owner[r] = (int32_t)v; reg[v] = (int16_t)r;
+            issued[v] = 1;
+            mp->cip_reg.push_back((int16_t)r);
+            mp->cip_row.push_back(ir.nodes[v].imm);
+        }
+        if (n_cip) t_pf = ld.back() + 1;
         for (uint32_t i = 0; i < nv && !failed; ++i) {
             cur = i;
+            // -- cross-item prefetch: the next batch of the next item's head loads
+            if (cip_done < n_cip && i >= t_pf + (cip_done / std::max<uint32_t>(1, o.cip_batch)) * o.cip_gap) {
+                const uint32_t nb = std::min<uint32_t>(std::max<uint32_t>(1, o.cip_batch), n_cip - cip_done);
+                issue_pfx(cip_done, nb);
+                cip_done += nb;
+            }
             // -- four-row staging far ahead: one buffer_load_dwordx4 ... lds per group of four rows
             while (o.dma4 && lq < ld.size() && ld[lq] <= i + o.la_dma) {
                 if (free_quads.empty() || seq - retired >= o.max_vmem) break;
@@ -601,6 +664,12 @@ struct Allocator {
                 }
             }
         }
+        // a short tail: the rest of the prefetch at the end
+        while (!failed && cip_done < n_cip) {
+            const uint32_t nb = std::min<uint32_t>(std::max<uint32_t>(1, o.cip_batch), n_cip - cip_done);
+            issue_pfx(cip_done, nb);
+            cip_done += nb;
+        }
         return !failed;
     }
 };
@@ -631,6 +700,8 @@ double colprog_cost(const MProg& mp) {
             case MI_XT: case MI_XTX: slots += 5; break;
             case MI_LDSRC: slots += 1.125; break;
             case MI_STOUT: slots += 2; break;
+            case MI_HEAD: break;  // issued by the previous item's MI_PFX
+            case MI_PFX: slots += 2.0 * (m.imm & 0xFFFFu) + 2 + ((m.imm >> 16) ? 0 : 18); break;
             default: slots += 1;
         }
     }
@@ -678,6 +749,7 @@ bool compile_colprog(const Params& p, const uint32_t* esi, uint32_t n_out, const
     }();
     for (const auto& c : cap) {
         AllocOpts w = o;
+        w.cip = 0;  // the SIMD's other waves issue while one waits at its item's start
         w.n_vgpr = std::min(o.n_vgpr, c[0]);
         w.n_agpr = std::min(o.n_agpr, c[1]);
         w.n_lds = std::min(o.n_lds, c[2]);
@@ -735,7 +807,7 @@ std::vector<uint32_t> colprog_src_rows(const MProg& mp) {
 uint32_t colprog_row_end(const MProg& mp) {
     uint32_t e = 1;
     for (const MInst& m : mp.ins)
-        if (m.op == MI_LDSRC || m.op == MI_DMA) e = std::max(e, m.imm + 1);
+        if (m.op == MI_LDSRC || m.op == MI_DMA || m.op == MI_HEAD) e = std::max(e, m.imm + 1);
     for (uint32_t r : mp.dma4_rows) e = std::max(e, r + 1);
     return e;
 }
@@ -745,6 +817,58 @@ uint32_t colprog_row_end(const MProg& mp) {
 // soffset with an s_mov.
 uint32_t scratch_bases(const MProg& mp) {
     return std::min<uint32_t>(SCR_BASES, mp.n_slots > 16 ? (mp.n_slots - 1) / 16 : 0);
+}
+
+// Cross-item prefetch (MProg::cip_*): head loads [first, first + n) of the item at workgroup iteration
+// s52 (+ s49 when `next`), all 64 lanes (a last, partial item's columns beyond n_cols read in bounds or 0).
+// The item's lane offset is formed as the loop top forms V_SRCOFF, into V_LDS2 (free: the program's LDS
+// slots stay below 256) through the xtime temporaries; each load's soffset is row * T by an s_mul.  SALU
+// temporaries s39 / s40 / s42..s47 are dead between the body's instructions (W = 1).  Skipped past the
+// wave's last item.
+void emit_cip_loads(const MProg& mp, uint32_t first, uint32_t n, bool next, uint32_t label, std::string& s) {
+    static const Policy pol;
+    const Reserved rv(mp.n_vgpr);
+    char buf[256];
+    auto line = [&](const char* t) { s += '\t'; s += t; s += '\n'; };
+    auto R = [&](int r) { return std::string(is_agpr(r) ? "a" : "v") + std::to_string(is_agpr(r) ? r - REG_A0 : r); };
+    if (first == 0) {
+        line(next ? "s_add_u32 s39, s52, s49" : "s_mov_b32 s39, s52");
+        line("s_cmp_lt_u32 s39, s48");
+        std::snprintf(buf, sizeof buf, "s_cbranch_scc0 .Lcip%u", label); line(buf);
+        line("s_and_b32 s40, s39, 7");
+        line("s_mul_i32 s40, s40, s17");
+        line("s_lshr_b32 s42, s39, 3");
+        line("s_add_u32 s40, s40, s42");
+        line("s_cmp_lt_u32 s39, s18");
+        line("s_cselect_b32 s39, s40, s39");
+        line("s_lshl_b32 s39, s39, 6");
+        std::snprintf(buf, sizeof buf, "v_mbcnt_lo_u32_b32 v%d, -1, 0", rv.t1); line(buf);
+        std::snprintf(buf, sizeof buf, "v_mbcnt_hi_u32_b32 v%d, -1, v%d", rv.t1, rv.t1); line(buf);
+        std::snprintf(buf, sizeof buf, "v_add_u32_e32 v%d, s39, v%d", rv.t1, rv.t1); line(buf);
+        std::snprintf(buf, sizeof buf, "v_mul_hi_u32 v%d, v%d, s14", rv.t2, rv.t1); line(buf);
+        std::snprintf(buf, sizeof buf, "v_lshrrev_b32_e32 v%d, s15, v%d", rv.t2, rv.t2); line(buf);
+        std::snprintf(buf, sizeof buf, "v_mul_lo_u32 v%d, v%d, s21", rv.lds2, rv.t2); line(buf);
+        std::snprintf(buf, sizeof buf, "v_sub_u32_e32 v%d, v%d, v%d", rv.t1, rv.t1, rv.lds2); line(buf);
+        std::snprintf(buf, sizeof buf, "v_lshlrev_b32_e32 v%d, 2, v%d", rv.t1, rv.t1); line(buf);
+        std::snprintf(buf, sizeof buf, "v_mul_lo_u32 v%d, v%d, s10", rv.lds2, rv.t2); line(buf);
+        std::snprintf(buf, sizeof buf, "v_add_u32_e32 v%d, v%d, v%d", rv.lds2, rv.lds2, rv.t1); line(buf);
+    } else {
+        line(next ? "s_add_u32 s39, s52, s49" : "s_mov_b32 s39, s52");
+        line("s_cmp_lt_u32 s39, s48");
+        std::snprintf(buf, sizeof buf, "s_cbranch_scc0 .Lcip%u", label); line(buf);
+    }
+    line("s_mov_b64 exec, -1");
+    for (uint32_t k = first; k < first + n; ++k) {
+        const int q = 42 + (int)(k % 6);
+        std::snprintf(buf, sizeof buf, "s_mul_i32 s%d, s12, %u", q, mp.cip_row[k]); line(buf);
+        std::snprintf(buf, sizeof buf, "buffer_load_dword %s, v%d, s[24:27], s%d offen%s", R(mp.cip_reg[k]).c_str(), rv.lds2, q,
+                      pol.src.c_str());
+        line(buf);
+    }
+    if (next) line("s_mov_b64 exec, s[22:23]");
+    std::snprintf(buf, sizeof buf, ".Lcip%u:", label);
+    s += buf;
+    s += '\n';
 }
 
 // The per-item instruction stream of an allocated program (the body of the persistent loop): the
@@ -946,6 +1070,12 @@ void emit_colprog_body(const MProg& mp, uint32_t W, std::string& s) {
                 break;
             case MI_WAITL:
                 std::snprintf(buf, sizeof buf, "s_waitcnt lgkmcnt(%u)", m.imm); line(buf); break;
+            case MI_HEAD:
+                break;  // in flight since the previous item's MI_PFX (or the prologue)
+            case MI_PFX:
+                if (diag & 4) break;
+                emit_cip_loads(mp, m.imm >> 16, m.imm & 0xFFFFu, true, 1 + (m.imm >> 16), s);
+                break;
         }
     }
 }
@@ -1040,6 +1170,8 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
         "v_add_u32_e32 V_OUTOFF, v4, v3",
     };
     const uint32_t W = std::max<uint32_t>(1, mp.wg_waves);
+    if (!mp.cip_reg.empty() && (W > 1 || mp.dma4_quads || mp.lds_base + mp.n_lds_slots > 256))
+        s += "\t.error \"cross-item prefetch needs W = 1 and LDS slots below 256 (V_LDS2 holds its offsets)\"\n";
     auto put = [&](const char* p) {
         std::string l(p);
         if (l == "CPFETCH") {
@@ -1183,6 +1315,11 @@ std::string emit_colprog_asm(const MProg& mp, const std::string& kname) {
         line("s_cbranch_scc0 .Lnostagger");
         for (uint32_t i = 0; i < stagger; ++i) line("s_sleep 127");
         s += ".Lnostagger:\n";
+    }
+    if (!mp.cip_reg.empty()) {
+        // cross-item prefetch: the wave's first item's head loads (later items': the previous item's MI_PFX)
+        line("s_lshr_b32 s21, s12, 2");
+        if (!(diag & 4)) emit_cip_loads(mp, 0, (uint32_t)mp.cip_reg.size(), false, 0, s);
     }
     s += ".Lloop:\n";
     for (const char* p : pro_iter) {

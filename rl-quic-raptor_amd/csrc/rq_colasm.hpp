@@ -35,6 +35,12 @@ enum MOp : uint8_t {
     MI_BAR,     // pair programs: s_barrier (after an lgkmcnt(0) the allocator emits)
     MI_DMAT,    // four-row staging: row offsets of group imm -> reserved table VGPR d (ds_read_b32)
     MI_DMA4,    // four-row staging: the four rows of group imm -> LDS quad d (buffer_load_dwordx4 ... lds)
+    // Cross-item prefetch (AllocOpts::cip): MI_HEAD is one of the item's first source loads, d <- row imm,
+    // issued by the previous item's MI_PFX (or the kernel prologue for a wave's first item), so it emits
+    // nothing in the body; MI_PFX issues the next item's head loads cip_reg / cip_row [imm >> 16, + (imm &
+    // 0xffff)) into their registers, which nothing writes after it.
+    MI_HEAD,
+    MI_PFX,
 };
 
 constexpr int REG_A0 = 256;       // register ids: 0..255 VGPR, 256..511 AGPR
@@ -79,6 +85,13 @@ struct AllocOpts {
     uint32_t wait_age = 320;     // a vmcnt wait also covers operations issued this many instructions ago
     uint32_t lwait_age = 48;     // the same for lgkmcnt (LDS) waits
     uint32_t load_batch = 1;     // source-row prefetches issued in groups of this many (experiments)
+    // Cross-item prefetch: the next item's first `cip` source rows are loaded during this item's load-free
+    // tail (after its last source load), cip_batch at a time every cip_gap IR nodes, into registers the
+    // tail then leaves alone; the item finds them in place.  0 = off (W > 1, pair and four-row programs,
+    // several waves per SIMD).  K=1024: 0.340 -> 0.335 ms per launch (profiles/r06c/cip_ab.log).
+    uint32_t cip = 64;
+    uint32_t cip_batch = 8;
+    uint32_t cip_gap = 24;
 };
 
 struct MProg {
@@ -96,6 +109,9 @@ struct MProg {
     // (4 per group, padded with the group's first row)
     uint32_t dma4_quads = 0, dma4_slot0 = 0;
     std::vector<uint32_t> dma4_rows;
+    // cross-item prefetch: the head loads' registers and rows, in issue order (MI_HEAD / MI_PFX)
+    std::vector<int16_t> cip_reg;
+    std::vector<uint32_t> cip_row;
     struct Stats {
         uint32_t valu = 0, ldsrc = 0, stout = 0, spst = 0, spld = 0, accw = 0, accr = 0, wait = 0, nop = 0;
         uint32_t sync_reload = 0;  // reloads that were not prefetched
@@ -103,6 +119,7 @@ struct MProg {
         uint32_t migrate = 0;                    // LDS residents pushed out to global scratch
         uint32_t dma = 0;                        // source rows staged through LDS by DMA
         uint32_t rst = 0, rld = 0, bar = 0;      // pair programs: ring stores / loads, barriers
+        uint32_t cip_evict = 0;                  // values moved out of the head registers for the prefetch
     } st;
 };
 

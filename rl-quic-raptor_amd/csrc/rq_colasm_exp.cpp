@@ -27,6 +27,7 @@ bool compile_colprog_dma4(const ColIR& ir, const AllocOpts& o, uint32_t quads, u
         return false;
     }
     AllocOpts so = o;
+    so.cip = 0;
     so.dma4 = quads;
     so.la_dma = la;
     so.n_vgpr = std::min<uint32_t>(o.n_vgpr, V_ALLOC - (N_RESERVED_DMA4 - N_RESERVED));
@@ -109,6 +110,7 @@ bool compile_pair(const ColIR& ir, const AllocOpts& o, uint32_t bmask, uint32_t 
     }
     // B first (small live set: a few LDS slots at most), then A with the LDS that is left
     AllocOpts ob = o;
+    ob.cip = 0;
     ob.n_lds = std::min<uint32_t>(o.n_lds, 32);
     ob.la_dma = 0;
     ob.dma4 = 0;
@@ -119,6 +121,7 @@ bool compile_pair(const ColIR& ir, const AllocOpts& o, uint32_t bmask, uint32_t 
         return false;
     }
     AllocOpts oa = o;
+    oa.cip = 0;
     // four-row staging: the group table (16 B per group; at most one group per load) sits at LDS 0
     uint32_t n_loads = 0;
     for (const IrNode& d : px.A.nodes) n_loads += d.k == IR_LOAD;

@@ -84,6 +84,12 @@ struct WaveEmu {
     std::function<bool(uint32_t, const std::vector<uint32_t>&)> ring_store;
     std::function<bool(uint32_t, std::vector<uint32_t>*)> ring_load;
     std::function<void()> barrier;
+    // cross-item prefetch: pass 2 runs the item again as the wave's next item (MI_HEAD then finds the row
+    // the previous MI_PFX loaded; vmcnt keeps counting across the boundary); rows loaded into the head
+    // registers by MI_PFX, and those registers handed over (nothing may write them until MI_HEAD)
+    bool second = false;
+    std::vector<int64_t> pfx_row = std::vector<int64_t>(512, -1);
+    std::vector<uint8_t> handed = std::vector<uint8_t>(512, 0);
     uint64_t tbl_seq[2] = {0, 0};           // four-row staging: the table read into each table VGPR
     uint32_t tbl_grp[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};
     char buf[200];
@@ -102,7 +108,12 @@ struct WaveEmu {
     bool ready(int r) const {
         return r < 0 || ((pend[r] == 0 || pend[r] <= retired) && (lpend[r] == 0 || lpend[r] <= lretired));
     }
-    bool vmem() { return ++seq - retired <= 63; }
+    // at 63 outstanding the hardware holds issue until the oldest retires (pass 2 starts with the previous
+    // item's tail in flight); the allocator itself never lets more than max_vmem be outstanding
+    bool vmem() {
+        if (second && seq - retired >= 63) retired = seq - 62;
+        return ++seq - retired <= 63;
+    }
     // source row `row` into dst (T/4 dwords) through the bounded buffer resource
     void read_row(uint32_t row, uint32_t* dst) const {
         const uint64_t base = (uint64_t)row * T;
@@ -115,8 +126,10 @@ struct WaveEmu {
 
     bool step(size_t i, const MInst& m) {
         if (!ready(m.a) || !ready(m.b) || !ready(m.c)) return bad(i, "operand read before its load completed");
-        if (m.op != MI_DMA && m.op != MI_DMA4 && m.op != MI_DMAT && m.d >= 0 && !ready(m.d))
+        if (m.op != MI_DMA && m.op != MI_DMA4 && m.op != MI_DMAT && m.op != MI_HEAD && m.d >= 0 && !ready(m.d))
             return bad(i, "register overwritten while a load into it is pending");
+        if (m.op != MI_DMA && m.op != MI_DMA4 && m.op != MI_DMAT && m.op != MI_HEAD && m.d >= 0 && handed[m.d])
+            return bad(i, "write to a register handed to the next item");
         switch (m.op) {
             case MI_XOR2:
                 for (uint32_t c = 0; c < Td; ++c) R[m.d][c] = R[m.a][c] ^ R[m.b][c];
@@ -208,6 +221,32 @@ struct WaveEmu {
                 if (!barrier) return bad(i, "barrier outside a pair program");
                 barrier();
                 break;
+            case MI_HEAD:
+                if (m.imm >= mp.K) return bad(i, "source row >= K");
+                if (second) {  // loaded by the previous item's MI_PFX
+                    if (pfx_row[m.d] != (int64_t)m.imm) return bad(i, "head register does not hold its prefetched row");
+                    handed[m.d] = 0;
+                    pfx_row[m.d] = -1;
+                    break;
+                }
+                read_row(m.imm, R[m.d].data());
+                if (!vmem()) return bad(i, "more than 63 vector-memory operations outstanding");
+                pend[m.d] = seq;
+                break;
+            case MI_PFX: {
+                const uint32_t f = m.imm >> 16, n = m.imm & 0xFFFFu;
+                if ((size_t)f + n > mp.cip_reg.size()) return bad(i, "prefetch beyond the head list");
+                for (uint32_t k = f; k < f + n; ++k) {
+                    const int r = mp.cip_reg[k];
+                    if (handed[r] || !ready(r)) return bad(i, "prefetch into a busy register");
+                    read_row(mp.cip_row[k], R[r].data());
+                    if (!vmem()) return bad(i, "more than 63 vector-memory operations outstanding");
+                    pend[r] = seq;
+                    pfx_row[r] = mp.cip_row[k];
+                    handed[r] = 1;
+                }
+                break;
+            }
             case MI_DMAT:
                 if (m.d < 0 || m.d > 1) return bad(i, "table register out of range");
                 if ((size_t)m.imm * 4 + 4 > mp.dma4_rows.size()) return bad(i, "table read beyond the group table");
@@ -245,11 +284,21 @@ struct WaveEmu {
     }
     bool run() {
         // each item's allocation assumes no vector-memory operation outstanding at its start (the
-        // previous item's last ones are stores; at 63 outstanding the hardware holds further issue)
+        // previous item's last ones are stores; at 63 outstanding the hardware holds further issue).  With
+        // cross-item prefetch the item runs twice, the second time as its own next item (the counters
+        // carry over: its waits must also cover the previous item's prefetch and last stores).
         retired = seq;
         for (size_t i = 0; i < mp.ins.size(); ++i)
             if (!step(i, mp.ins[i])) return false;
         lretired = lseq;  // the loop end's lgkmcnt(0)
+        if (mp.cip_reg.empty()) return true;
+        for (size_t k = 0; k < mp.cip_reg.size(); ++k)
+            if (!handed[mp.cip_reg[k]] || pfx_row[mp.cip_reg[k]] != (int64_t)mp.cip_row[k])
+                return bad(mp.ins.size(), "a head register not prefetched for the next item");
+        second = true;
+        for (size_t i = 0; i < mp.ins.size(); ++i)
+            if (!step(i, mp.ins[i])) return false;
+        lretired = lseq;
         return true;
     }
 };

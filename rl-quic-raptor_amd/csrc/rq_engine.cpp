@@ -397,6 +397,9 @@ const AllocOpts& alloc_options() {
         if (const char* h = knob("RQHIP_SRC_LDS")) r.src_lds = (uint32_t)std::atoi(h);
         if (const char* h = knob("RQHIP_WAIT_AGE")) std::sscanf(h, "%u,%u", &r.wait_age, &r.lwait_age);
         if (const char* h = knob("RQHIP_LOAD_BATCH")) r.load_batch = (uint32_t)std::max(1, std::atoi(h));
+        if (const char* h = knob("RQHIP_CIP")) std::sscanf(h, "%u,%u,%u", &r.cip, &r.cip_batch, &r.cip_gap);
+        if (const char* h = knob("RQHIP_WG"))
+            if (std::atoi(h) > 1) r.cip = 0;  // the prefetch is a single-wave-workgroup layout
         return r;
     }();
     return o;
@@ -454,7 +457,7 @@ struct CacheHdr {
     MProg::Stats st;
     uint64_t body_hash;  // FNV-1a of the name, code object and row table (checked on load)
 };
-constexpr char CACHE_MAGIC[9] = "RQCO0008";
+constexpr char CACHE_MAGIC[9] = "RQCO0009";
 
 uint64_t cache_body_hash(const std::string& name, const std::vector<char>& co, const std::vector<uint32_t>& rows) {
     uint64_t h = fnv1a(name.data(), name.size());
@@ -2191,7 +2194,7 @@ int rq_debug_colprog_eval(uint32_t K, uint32_t T, const uint32_t* esi, uint32_t 
 }
 
 int rq_debug_colprog_emulate(uint32_t K, uint32_t T, const uint32_t* esi, uint32_t n_out, const uint8_t* src,
-                             uint8_t* out, const uint32_t opts[6], uint32_t stats[18], char* asm_buf, size_t asm_cap,
+                             uint8_t* out, const uint32_t opts[9], uint32_t stats[18], char* asm_buf, size_t asm_cap,
                              size_t* asm_len) {
     Params p;
     int rc = params_for_K(K, &p);
@@ -2207,6 +2210,9 @@ int rq_debug_colprog_emulate(uint32_t K, uint32_t T, const uint32_t* esi, uint32
         if (opts[3]) o.la_reload = opts[3];
         if (opts[4]) o.max_vmem = std::min<uint32_t>(opts[4], 60);
         if (opts[5]) o.n_lds = std::min<uint32_t>(opts[5] - 1, 512);
+        if (opts[6]) o.cip = opts[6] - 1;
+        if (opts[7]) o.cip_batch = opts[7];
+        if (opts[8]) o.cip_gap = opts[8];
     }
     MProg mp;
     if (!debug_compile(p, esi, n_out, o, &ir, &mp, &err)) return fail(RQ_ERR_PLAN, err);

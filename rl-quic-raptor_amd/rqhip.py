@@ -285,19 +285,20 @@ def colprog_stats(K, esis=None, opts=None):
     st = np.zeros(18, np.uint32)
     P32 = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
     e = np.asarray(esis if esis is not None else [0], np.uint32)
-    o = np.asarray(opts if opts is not None else [0] * 6, np.uint32)
+    o = np.asarray(list(opts or []) + [0] * (9 - len(opts or [])), np.uint32)
     _check(lib().rq_debug_colprog_emulate(K, 4, P32(e) if esis is not None else None, len(e), None, None, P32(o),
                                           P32(st), None, 0, None))
     return dict(zip(COLPROG_STAT_NAMES, (int(x) for x in st[:18])))
 
 
 def colprog_emulate(K, T, esis, src, opts=None):
-    """Run the allocated machine program on the host for one block (test infrastructure)."""
+    """Run the allocated machine program on the host for one block (test infrastructure).  opts: up to 9
+    allocation options (include/rqhip_debug.h), the rest 0 = default."""
     import numpy as np
     src = np.ascontiguousarray(src, np.uint8)
     e = np.asarray(esis, np.uint32)
     out = np.zeros((len(e), T), np.uint8)
-    o = np.asarray(opts if opts is not None else [0] * 6, np.uint32)
+    o = np.asarray(list(opts or []) + [0] * (9 - len(opts or [])), np.uint32)
     st = np.zeros(18, np.uint32)
     P32 = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
     _check(lib().rq_debug_colprog_emulate(K, T, P32(e), len(e), src.ctypes.data, out.ctypes.data, P32(o), P32(st),
@@ -317,15 +318,16 @@ def colprog_eval(K, T, esis, src):
     return out
 
 
-def colprog_asm(K, esis):
-    """gfx950 assembly text of the column program for (K, output ESIs)."""
+def colprog_asm(K, esis, opts=None):
+    """gfx950 assembly text of the column program for (K, output ESIs) (opts as colprog_emulate)."""
     import numpy as np
     e = np.asarray(esis, np.uint32)
     P32 = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+    o = np.asarray(list(opts or []) + [0] * (9 - len(opts or [])), np.uint32)
     n = ctypes.c_size_t(0)
-    _check(lib().rq_debug_colprog_emulate(K, 4, P32(e), len(e), None, None, None, None, None, 0, ctypes.byref(n)))
+    _check(lib().rq_debug_colprog_emulate(K, 4, P32(e), len(e), None, None, P32(o), None, None, 0, ctypes.byref(n)))
     buf = ctypes.create_string_buffer(n.value)
-    _check(lib().rq_debug_colprog_emulate(K, 4, P32(e), len(e), None, None, None, None, buf, n.value, ctypes.byref(n)))
+    _check(lib().rq_debug_colprog_emulate(K, 4, P32(e), len(e), None, None, P32(o), None, buf, n.value, ctypes.byref(n)))
     return buf.raw[:n.value].decode()
 
 

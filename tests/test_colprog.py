@@ -9,6 +9,7 @@
 * the generated gfx950 assembly assembles in process (amd_comgr).
 
 The GPU runs exactly this machine program (tests/test_gpu_parity.py)."""
+import ctypes
 import re
 
 import numpy as np
@@ -100,7 +101,8 @@ SCALAR_ALLOWED = {"s_add_u32", "s_addc_u32", "s_and_b32", "s_and_b64", "s_endpgm
                   "s_waitcnt", "s_cmp_ge_u32", "s_cbranch_scc1", "s_mov_b64", "s_cmp_lt_u32",
                   "s_cselect_b32", "s_load_dwordx2", "s_load_dwordx4", "s_load_dwordx16",
                   "s_getpc_b64", "s_sub_u32", "s_subb_u32", "s_setpc_b64",
-                  "s_min_u32", "s_cbranch_execz", "s_branch"}  # (the decode's descriptor-fetch loop)
+                  "s_min_u32", "s_cbranch_execz", "s_branch",  # (the decode's descriptor-fetch loop)
+                  "s_cbranch_scc0"}  # (cross-item prefetch: past the wave's last item)
 
 
 def test_program_size_and_assembly(rq):
@@ -116,6 +118,59 @@ def test_program_size_and_assembly(rq):
     assert rq.colprog_assemble(64, list(range(64, 80))) > 1000
     # a full-size program (>128 KiB of code: the loop back-edge must not be a 16-bit branch)
     assert rq.colprog_assemble(1024, list(range(1024, 1100))) > 131072
+
+
+# cross-item prefetch (AllocOpts::cip): opts[6] = head rows + 1, opts[7] = rows per batch, opts[8] = IR nodes
+# between batches
+@pytest.mark.parametrize("K,T,nrep,cip,batch,gap", [(1024, 16, 76, 64, 8, 24), (1024, 8, 76, 96, 16, 8),
+                                                    (64, 48, 16, 24, 4, 2), (5, 20, 6, 8, 1, 1), (1, 8, 4, 4, 8, 24),
+                                                    (257, 16, 20, 48, 8, 64), (2048, 8, 30, 40, 8, 24)])
+def test_cross_item_prefetch_matches_oracle(rq, oracle, K, T, nrep, cip, batch, gap):
+    """The next item's first source rows are loaded during the item's load-free tail (MI_PFX) into the
+    registers its first loads use (MI_HEAD).  The emulator runs the item twice, the second time as the
+    wave's next item: each head register must hold its row from the prefetch, nothing may write a
+    handed-over register in between, and the vmcnt waits must hold with the previous item's prefetch and
+    stores still counted.  Both runs give the reference bytes."""
+    rng = np.random.default_rng(K + cip)
+    data = rng.integers(0, 256, K * T, dtype=np.uint8)
+    esis = _esis(K, nrep)
+    out, st = rq.colprog_emulate(K, T, esis, data, [0] * 6 + [cip + 1, batch, gap])
+    enc = oracle.OracleEncoder(data.tobytes(), T)
+    for i, e in enumerate(esis):
+        assert np.array_equal(out[i], enc.gen_symbol(e)), (K, e)
+
+
+@pytest.mark.parametrize("opts", [[64, 32, 40, 20, 8, 1, 17, 4, 8], [32, 4, 400, 400, 60, 9, 9, 8, 24],
+                                  [24, 1, 40, 20, 8, 17, 7, 2, 1], [200, 8, 16, 8, 4, 1, 49, 16, 4]])
+def test_cross_item_prefetch_under_register_pressure(rq, oracle, opts):
+    """Head registers vacated under pressure (values moved to AGPRs or out to LDS / scratch) and a small
+    vmcnt budget (a batch waits for room first)."""
+    K, T = 257, 12
+    rng = np.random.default_rng(sum(opts))
+    data = rng.integers(0, 256, K * T, dtype=np.uint8)
+    esis = list(range(K, K + 12)) + [3]
+    out, st = rq.colprog_emulate(K, T, esis, data, opts)
+    enc = oracle.OracleEncoder(data.tobytes(), T)
+    for i, e in enumerate(esis):
+        assert np.array_equal(out[i], enc.gen_symbol(e)), e
+
+
+def test_cross_item_prefetch_assembly(rq):
+    """The prologue loads the wave's first item's head rows and the tail the next item's (skipped past the
+    last item), into the top VGPRs, with V_LDS2 as the offset register; the program assembles."""
+    K, esis = 1024, list(range(1024, 1100))
+    asm = rq.colprog_asm(K, esis, [0] * 6 + [33, 8, 24])
+    assert asm.count(".Lcip0:") == 1 and asm.count("s_cbranch_scc0 .Lcip") == 1 + 4
+    pro, body = asm.split(".Lloop:", 1)
+    head = "buffer_load_dword v249, v255, s[24:27], s42 offen"  # the first head row (V_LDS2 = v255)
+    assert pro.count(head) == 1 and body.count(head) == 1 and body.count(", v255, s[24:27]") == 32
+    assert body.count("s_mov_b64 exec, s[22:23]") >= 4
+    assert ".error" not in asm
+    scalar_ops = set(re.findall(r"^\s*(s_[a-z0-9_]+)", asm, re.M))
+    assert scalar_ops <= SCALAR_ALLOWED, scalar_ops - SCALAR_ALLOWED
+    size = ctypes.c_size_t(0)
+    rq._check(rq.lib().rq_debug_assemble(asm.encode(), len(asm), ctypes.byref(size)))
+    assert size.value > 131072
 
 
 SCHED_RS, SCHED_4R = 1 << 16, 1 << 17  # rq_colprog.hpp
