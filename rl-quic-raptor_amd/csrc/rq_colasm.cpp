@@ -820,21 +820,32 @@ uint32_t scratch_bases(const MProg& mp) {
 }
 
 // Cross-item prefetch (MProg::cip_*): head loads [first, first + n) of the item at workgroup iteration
-// s52 (+ s49 when `next`), all 64 lanes (a last, partial item's columns beyond n_cols read in bounds or 0).
-// The item's lane offset is formed as the loop top forms V_SRCOFF, into V_LDS2 (free: the program's LDS
-// slots stay below 256) through the xtime temporaries; each load's soffset is row * T by an s_mul.  SALU
-// temporaries s39 / s40 / s42..s47 are dead between the body's instructions (W = 1).  Skipped past the
-// wave's last item.
+// s52 + s49 (the wave's next item; the prologue: s52, its first item).  The first batch forms the item's
+// lane offset as the loop top forms V_SRCOFF, into V_LDS2 (free: the program's LDS slots stay below 256)
+// through the xtime temporaries, and its lane mask (columns below n_cols) into s[54:55] (free until the
+// loop end's s_getpc); later batches reuse both.  Each load's soffset is row * T by an s_mul (SALU
+// temporaries s39 / s40 / s42..s47 are dead between the body's instructions at W = 1).  Past the wave's
+// last item the loads re-read the current item's rows (V_SRCOFF under its own mask): the allocator counts
+// them in its vmcnt waits, so they are issued either way.  The prologue skips a wave that has no item.
 void emit_cip_loads(const MProg& mp, uint32_t first, uint32_t n, bool next, uint32_t label, std::string& s) {
     static const Policy pol;
     const Reserved rv(mp.n_vgpr);
     char buf[256];
     auto line = [&](const char* t) { s += '\t'; s += t; s += '\n'; };
+    auto lab = [&](const char* t) { std::snprintf(buf, sizeof buf, ".Lcip%s%u:\n", t, label); s += buf; };
     auto R = [&](int r) { return std::string(is_agpr(r) ? "a" : "v") + std::to_string(is_agpr(r) ? r - REG_A0 : r); };
     if (first == 0) {
         line(next ? "s_add_u32 s39, s52, s49" : "s_mov_b32 s39, s52");
         line("s_cmp_lt_u32 s39, s48");
-        std::snprintf(buf, sizeof buf, "s_cbranch_scc0 .Lcip%u", label); line(buf);
+        if (next) {
+            std::snprintf(buf, sizeof buf, "s_cbranch_scc1 .Lcipn%u", label); line(buf);
+            std::snprintf(buf, sizeof buf, "v_mov_b32_e32 v%d, v%d", rv.lds2, rv.srcoff); line(buf);
+            line("s_mov_b64 s[54:55], s[22:23]");
+            std::snprintf(buf, sizeof buf, "s_branch .Lcipg%u", label); line(buf);
+            lab("n");
+        } else {
+            std::snprintf(buf, sizeof buf, "s_cbranch_scc0 .Lcipe%u", label); line(buf);
+        }
         line("s_and_b32 s40, s39, 7");
         line("s_mul_i32 s40, s40, s17");
         line("s_lshr_b32 s42, s39, 3");
@@ -845,6 +856,7 @@ void emit_cip_loads(const MProg& mp, uint32_t first, uint32_t n, bool next, uint
         std::snprintf(buf, sizeof buf, "v_mbcnt_lo_u32_b32 v%d, -1, 0", rv.t1); line(buf);
         std::snprintf(buf, sizeof buf, "v_mbcnt_hi_u32_b32 v%d, -1, v%d", rv.t1, rv.t1); line(buf);
         std::snprintf(buf, sizeof buf, "v_add_u32_e32 v%d, s39, v%d", rv.t1, rv.t1); line(buf);
+        std::snprintf(buf, sizeof buf, "v_cmp_gt_u32_e64 s[54:55], s13, v%d", rv.t1); line(buf);
         std::snprintf(buf, sizeof buf, "v_mul_hi_u32 v%d, v%d, s14", rv.t2, rv.t1); line(buf);
         std::snprintf(buf, sizeof buf, "v_lshrrev_b32_e32 v%d, s15, v%d", rv.t2, rv.t2); line(buf);
         std::snprintf(buf, sizeof buf, "v_mul_lo_u32 v%d, v%d, s21", rv.lds2, rv.t2); line(buf);
@@ -852,12 +864,9 @@ void emit_cip_loads(const MProg& mp, uint32_t first, uint32_t n, bool next, uint
         std::snprintf(buf, sizeof buf, "v_lshlrev_b32_e32 v%d, 2, v%d", rv.t1, rv.t1); line(buf);
         std::snprintf(buf, sizeof buf, "v_mul_lo_u32 v%d, v%d, s10", rv.lds2, rv.t2); line(buf);
         std::snprintf(buf, sizeof buf, "v_add_u32_e32 v%d, v%d, v%d", rv.lds2, rv.lds2, rv.t1); line(buf);
-    } else {
-        line(next ? "s_add_u32 s39, s52, s49" : "s_mov_b32 s39, s52");
-        line("s_cmp_lt_u32 s39, s48");
-        std::snprintf(buf, sizeof buf, "s_cbranch_scc0 .Lcip%u", label); line(buf);
+        if (next) lab("g");
     }
-    line("s_mov_b64 exec, -1");
+    line("s_mov_b64 exec, s[54:55]");
     for (uint32_t k = first; k < first + n; ++k) {
         const int q = 42 + (int)(k % 6);
         std::snprintf(buf, sizeof buf, "s_mul_i32 s%d, s12, %u", q, mp.cip_row[k]); line(buf);
@@ -865,10 +874,8 @@ void emit_cip_loads(const MProg& mp, uint32_t first, uint32_t n, bool next, uint
                       pol.src.c_str());
         line(buf);
     }
-    if (next) line("s_mov_b64 exec, s[22:23]");
-    std::snprintf(buf, sizeof buf, ".Lcip%u:", label);
-    s += buf;
-    s += '\n';
+    line(next ? "s_mov_b64 exec, s[22:23]" : "s_mov_b64 exec, -1");
+    if (!next) lab("e");
 }
 
 // The per-item instruction stream of an allocated program (the body of the persistent loop): the

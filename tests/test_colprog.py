@@ -156,11 +156,15 @@ def test_cross_item_prefetch_under_register_pressure(rq, oracle, opts):
 
 
 def test_cross_item_prefetch_assembly(rq):
-    """The prologue loads the wave's first item's head rows and the tail the next item's (skipped past the
-    last item), into the top VGPRs, with V_LDS2 as the offset register; the program assembles."""
+    """The prologue loads the wave's first item's head rows and the tail the next item's, into the top
+    VGPRs, with V_LDS2 as the offset register and the item's lane mask in s[54:55].  Past the wave's last
+    item the tail's loads re-read the current item's rows instead of being skipped: the allocator's vmcnt
+    waits after them count them (a skipped batch left those waits short: a GPU race in round 6, two wrong
+    rows of 552 on a one-item launch).  The program assembles."""
     K, esis = 1024, list(range(1024, 1100))
     asm = rq.colprog_asm(K, esis, [0] * 6 + [33, 8, 24])
-    assert asm.count(".Lcip0:") == 1 and asm.count("s_cbranch_scc0 .Lcip") == 1 + 4
+    assert asm.count(".Lcipe0:") == 1 and asm.count("s_cbranch_scc0 .Lcip") == 1
+    assert asm.count("s_cbranch_scc1 .Lcipn1") == 1 and asm.count("s_mov_b64 exec, s[54:55]") == 1 + 4
     pro, body = asm.split(".Lloop:", 1)
     head = "buffer_load_dword v249, v255, s[24:27], s42 offen"  # the first head row (V_LDS2 = v255)
     assert pro.count(head) == 1 and body.count(head) == 1 and body.count(", v255, s[24:27]") == 32
