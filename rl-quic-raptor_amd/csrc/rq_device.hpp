@@ -125,6 +125,9 @@ struct SolveArgs {
     uint32_t row_margin;
     uint32_t n_map;             // entries of blk_map (the general solver's grid strides over them)
     uint32_t diag_steps;        // experiments builds (RQHIP_SOLVE_STEPS): pivot steps of k_solve_pq (timing only)
+    // experiments builds (RQHIP_SOLVE_DIAG, timing only, wrong results): k_solve_pq's step without its pinfo
+    // read (1), barrier (2), dependent table read (4), GF(256) row updates (8)
+    uint32_t diag;
     // k_solve also writes the register-table apply's index stream (the shipped shape 8, 5, 2) when set
     uint32_t xb_on;
     XbitsArgs xb;

@@ -1461,6 +1461,7 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     s.row_margin = solve_row_margin();
     s.n_map = nw;
     s.diag_steps = 0;
+    s.diag = 0;
     // the register-table apply's index stream: written by the solvers (below), else k_xbits after them
     XbitsArgs xa{};
     if (gi) {

@@ -155,8 +155,13 @@ int launch_xbits(const XbitsArgs& a, uint32_t n_blocks, const GiShape& s, void* 
 // PF (experiments, RQHIP_SOLVE_PF=1): the column buffer carries each row's pinfo word instead of its
 // coefficient byte, looked up by the wave that writes it while it updates its other quads, so a step
 // starts one dependent LDS round trip later in its chain.
-template <int RPL, int NW, bool PF = false>
+// RR (RPL = 1): the rows stay in registers across the steps -- wave g owns quads g, g + NW, ... of every
+// row for the whole solve (quads below the step's column are final and skipped, as the shifting
+// assignment skips them) -- and the pivot row's dwords are v_readlane'd from lane p: no row quad
+// goes through LDS per step (RR's rows are written back once, after the last step, for X).
+template <int RPL, int NW, bool PF = false, bool RR = false>
 __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
+    static_assert(!RR || (RPL == 1 && !PF), "RR: one row per lane, coefficient-byte column buffer");
     constexpr uint32_t NT = 64 * NW;
     constexpr uint32_t NROWS = 64 * RPL, SW = 32 * RPL + 4;  // rows, row stride (dwords)
     constexpr uint32_t QW = (8 * RPL + NW - 1) / NW;          // quads per row a wave may update
@@ -229,6 +234,60 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
     for (int q = 0; q < RPL; ++q) used[q] = lane + 64 * q >= nrow;
     const uint8_t* rb = reinterpret_cast<const uint8_t*>(rows);
     const uint32_t ksteps = a.diag_steps ? min(e, a.diag_steps) : e;
+    if constexpr (RR) {
+        constexpr uint32_t QR = (8 + NW - 1) / NW;  // quads per row this wave owns
+        uint4* myrow = reinterpret_cast<uint4*>(rows + lane * SW);
+        uint4 R[QR];
+#pragma unroll
+        for (int j = 0; j < (int)QR; ++j) R[j] = myrow[min(g + NW * j, 8u)];
+        bool used0 = used[0];
+        for (uint32_t k = 0; k < ksteps; ++k) {
+            const uint32_t f = fcol[k & 1][lane];
+            const uint32_t pif = pinfo[f];
+            const uint64_t bal = __ballot(f != 0 && !used0);
+            if (!bal) {  // uniform over the block: every wave saw the same rows
+                if (tid == 0) a.status[b] = (nr > nrow) ? ST_FALLBACK : 0;
+                if (a.xb_on && nr <= nrow)
+                    gi_stream<8, 5, 2>(a.xb, blockIdx.x, b, e, false, tid, NT, [](uint32_t, uint32_t) { return 0u; },
+                                       [](uint32_t) { return 0u; });
+                return;
+            }
+            const uint32_t p = (uint32_t)__ffsll((unsigned long long)bal) - 1;
+            const bool piv = lane == p;
+            used0 = used0 || piv;
+            if (tid == 0) pivl[k] = (uint8_t)p;
+            const uint32_t pip = __builtin_amdgcn_readlane(pif, p);
+            const uint32_t ilgp = 255u - (pip & 0xFFu);
+            const bool act = piv ? ((pif >> 16) & 1u) != 0 : f != 0;
+            const uint32_t l = piv ? (pif >> 8) & 0xFFu : (pif & 0xFFu) + ilgp;  // < 510
+            const uint4 A = tlA[l];
+            const uint32_t B = tlB[l];
+            const uint32_t kq = k >> 4, kn = k + 1;
+#pragma unroll
+            for (int j = 0; j < (int)QR; ++j) {
+                const uint32_t w = g + NW * j;
+                if (w >= q1 || w < kq) continue;  // wave-uniform
+                const uint32_t px = __builtin_amdgcn_readlane(R[j].x, p), py = __builtin_amdgcn_readlane(R[j].y, p);
+                const uint32_t pz = __builtin_amdgcn_readlane(R[j].z, p), pw = __builtin_amdgcn_readlane(R[j].w, p);
+                uint4 r = R[j];
+                r.x ^= perm_mul(A, B, px);
+                r.y ^= perm_mul(A, B, py);
+                r.z ^= perm_mul(A, B, pz);
+                r.w ^= perm_mul(A, B, pw);
+                if (act) R[j] = r;
+                if (kn < ksteps && w == (kn >> 4)) {  // wave-uniform: this wave owns column k + 1
+                    const uint32_t d = (kn >> 2) & 3u;
+                    const uint32_t dw = d == 0 ? R[j].x : d == 1 ? R[j].y : d == 2 ? R[j].z : R[j].w;
+                    fcol[kn & 1][lane] = (FC)((dw >> ((kn & 3u) * 8)) & 0xFFu);
+                }
+            }
+            __syncthreads();
+        }
+#pragma unroll
+        for (int j = 0; j < (int)QR; ++j)
+            if (g + NW * j <= 8u) myrow[g + NW * j] = R[j];
+        __syncthreads();
+    } else
     for (uint32_t k = 0; k < ksteps; ++k) {
         // (1) this wave's row quads for the step and every row's coefficient in column k
         const uint32_t w0 = (k >> 4) + g;
@@ -253,6 +312,10 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
             // (2) pinfo of every row's coefficient, beside the ballot
 #pragma unroll
             for (int q = 0; q < RPL; ++q) pif[q] = pinfo[f[q]];
+#ifdef RQHIP_EXPERIMENTS
+            if (a.diag & 1)
+                for (int q = 0; q < RPL; ++q) pif[q] = f[q] | 0x10100u;
+#endif
         }
         uint32_t p = 0xFFFFFFFFu;
 #pragma unroll
@@ -288,7 +351,10 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
         for (int q = 0; q < RPL; ++q) {
             const bool piv = lane + 64 * q == p;
             act[q] = piv ? ((pif[q] >> 16) & 1u) != 0 : f[q] != 0;
-            const uint32_t l = piv ? (pif[q] >> 8) & 0xFFu : (pif[q] & 0xFFu) + ilgp;  // < 510
+            uint32_t l = piv ? (pif[q] >> 8) & 0xFFu : (pif[q] & 0xFFu) + ilgp;  // < 510
+#ifdef RQHIP_EXPERIMENTS
+            if (a.diag & 4) l = lane;
+#endif
             A[q] = tlA[l];
             B[q] = tlB[l];
         }
@@ -303,10 +369,17 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
 #pragma unroll
             for (int q = 0; q < RPL; ++q) {
                 uint4 r = R[q][j];
+#ifdef RQHIP_EXPERIMENTS
+                if (a.diag & 8) {
+                    r.x ^= px; r.y ^= py; r.z ^= pz; r.w ^= pw;
+                } else
+#endif
+                {
                 r.x ^= perm_mul(A[q], B[q], px);
                 r.y ^= perm_mul(A[q], B[q], py);
                 r.z ^= perm_mul(A[q], B[q], pz);
                 r.w ^= perm_mul(A[q], B[q], pw);
+                }
                 if (act[q]) reinterpret_cast<uint4*>(rows + (lane + 64 * q) * SW)[w] = r;
                 if (kn < ksteps && w == (kn >> 4)) {  // wave-uniform: this wave owns column k + 1
                     const uint4 v = act[q] ? r : R[q][j];
@@ -317,6 +390,9 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
                 }
             }
         }
+#ifdef RQHIP_EXPERIMENTS
+        if (a.diag & 2) continue;
+#endif
         __syncthreads();
     }
     if (ksteps < e) {  // diagnostic step limit (timing only): valid pivot rows, meaningless X
@@ -627,17 +703,20 @@ int launch_solve(const SolveArgs& a_in, uint32_t n_blocks, bool need_general, bo
     if (!stream_ok) first.xb_on = 0;
     if (xbits_done) *xbits_done = first.xb_on != 0;
     first.diag_steps = 0;
+    first.diag = 0;
     const hipStream_t st = (hipStream_t)stream;
 #ifdef RQHIP_EXPERIMENTS
     static const uint32_t dsteps = [] { const char* e = std::getenv("RQHIP_SOLVE_STEPS"); return e ? (uint32_t)std::atoi(e) : 0u; }();
+    static const uint32_t sdiag = [] { const char* e = std::getenv("RQHIP_SOLVE_DIAG"); return e ? (uint32_t)std::atoi(e) : 0u; }();
     first.diag_steps = dsteps;
+    first.diag = sdiag;
 #endif
     SolveArgs a = first;
     a.status_init = nullptr;
 #ifdef RQHIP_EXPERIMENTS
     static const bool pm = knob_on("RQHIP_SOLVE_PM", true), lut = knob_on("RQHIP_SOLVE_LUT", true),
                       pq = knob_on("RQHIP_SOLVE_PQ", true), pf = knob_on("RQHIP_SOLVE_PF", false),
-                      lean = knob_on("RQHIP_SOLVE_LEAN", false);
+                      lean = knob_on("RQHIP_SOLVE_LEAN", false), rr = knob_on("RQHIP_SOLVE_RR", false);
     static const int nw = [] { const char* e = std::getenv("RQHIP_SOLVE_NW"); return e ? std::atoi(e) : 4; }();
     // solvers that take `a` (statuses uploaded first): k_solve_fast and k_solve_reg
     const bool takes_a = !lean && ((nw == 1 && !pm) || (nw == 4 && !pm) || (nw != 1 && nw != 2 && nw != 4 && nw != 8));
@@ -650,6 +729,7 @@ int launch_solve(const SolveArgs& a_in, uint32_t n_blocks, bool need_general, bo
         else if (nw == 2) hipLaunchKernelGGL((k_solve_pq<1, 2>), dim3(n_blocks), dim3(128), 0, st, first);
         else if (nw == 8) hipLaunchKernelGGL((k_solve_pq<1, 8>), dim3(n_blocks), dim3(512), 0, st, first);
         else if (pf) hipLaunchKernelGGL((k_solve_pq<1, 4, true>), dim3(n_blocks), dim3(256), 0, st, first);
+        else if (rr) hipLaunchKernelGGL((k_solve_pq<1, 4, false, true>), dim3(n_blocks), dim3(256), 0, st, first);
         else if (solve_in_place()) hipLaunchKernelGGL((k_solve_ip<4>), dim3(n_blocks), dim3(256), 0, st, first);
         else hipLaunchKernelGGL((k_solve_pq<1, 4>), dim3(n_blocks), dim3(256), 0, st, first);
         rx = (int)hipGetLastError();
