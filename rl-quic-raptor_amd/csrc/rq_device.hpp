@@ -125,8 +125,10 @@ struct SolveArgs {
     uint32_t row_margin;
     uint32_t n_map;             // entries of blk_map (the general solver's grid strides over them)
     uint32_t diag_steps;        // experiments builds (RQHIP_SOLVE_STEPS): pivot steps of k_solve_pq (timing only)
-    // experiments builds (RQHIP_SOLVE_DIAG, timing only, wrong results): k_solve_pq's step without its pinfo
-    // read (1), barrier (2), dependent table read (4), GF(256) row updates (8)
+    // experiments builds (RQHIP_SOLVE_DIAG, timing only, wrong X): k_solve_pq's step without its pinfo read
+    // (1), dependent table read (4), GF(256) row updates (8).  Every mode keeps the pivot choice uniform
+    // and within the block's rows (a no-barrier mode did not: the waves chose different pivots, the
+    // stream named received rows past the block's, and the apply read past the received-row buffer)
     uint32_t diag;
     // k_solve also writes the register-table apply's index stream (the shipped shape 8, 5, 2) when set
     uint32_t xb_on;
@@ -134,6 +136,10 @@ struct SolveArgs {
     // k_solve (the last solver launch) also writes every block's final status here: the caller's pinned
     // status array as the device sees it, so an async decode needs no status download (nullptr: none)
     int32_t* host_status;
+    // The first solver (k_solve_pq<1, ...>) finishes a block that is rank-deficient on its first e + margin
+    // rows with every received repair itself (general_block on its LDS rows) instead of deferring it, and
+    // writes host_status for its blocks.  Set when no block has e > 64: no later solver launch then.
+    uint32_t inline_general;
 };
 constexpr int32_t ST_PENDING = -100;   // queued for the solver
 constexpr int32_t ST_FALLBACK = -101;  // beyond the fast solvers: the general solver decides

@@ -1462,6 +1462,10 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     s.n_map = nw;
     s.diag_steps = 0;
     s.diag = 0;
+    // no block beyond the first solver's 64 rows: it finishes every block itself (launch_solve clears this
+    // for the experiments variants)
+    static const bool inl_off = [] { const char* e = knob("RQHIP_SOLVE_INLINE"); return e && e[0] == '0'; }();
+    s.inline_general = max_e <= 64 && !inl_off ? 1u : 0u;
     // the register-table apply's index stream: written by the solvers (below), else k_xbits after them
     XbitsArgs xa{};
     if (gi) {

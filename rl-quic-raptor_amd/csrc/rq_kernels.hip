@@ -139,6 +139,91 @@ int launch_xbits(const XbitsArgs& a, uint32_t n_blocks, const GiShape& s, void* 
 // rank e <=> the reference's system is full rank.
 // Output: X (e x e) and the e received repairs it combines: x_k = sum_m X[k][m] s_{piv[m]}, stored
 // as xcoef[m * xc_stride + k] (one uniform 64-byte row per m for k_apply's scalar loads).
+// The general algorithm on one block (k_solve's per-block body; the first solver runs it in place of a
+// deferral when inline_general is set): `ws` is an LDS working set of solve_ws_bytes(e) bytes, used when
+// e <= lds_e (else the block's global workspace); ex / lg the GF(256) tables in LDS; piv one LDS int.
+// Every thread of the workgroup calls it (barriers inside).
+__device__ __forceinline__ void general_block(const SolveArgs& a, uint32_t bi, uint32_t b, uint8_t* ws, const uint8_t* ex,
+                              const uint8_t* lg, int* piv, uint32_t tid, uint32_t nthr) {
+    const uint32_t e = a.erased_off[b + 1] - a.erased_off[b];
+    const uint32_t nr = a.rep_cnt[b];
+    const uint32_t* E = a.erased + a.erased_off[b];
+    const uint32_t* U = a.rep_uidx + a.rep_off[b];
+    const uint32_t W2 = basis_width(e);
+    // v (W2) | coefficient of v on each basis row (e) | pc (e x u16) | rowid (e x u16) | basis (e x W2):
+    // in LDS for e <= lds_e, else in this block's global workspace (solve_ws_bytes(e))
+    uint8_t* v = (e <= a.lds_e) ? ws : a.gws + 64ull * a.goff[bi];
+    uint8_t* cf = v + W2;
+    uint16_t* pc = reinterpret_cast<uint16_t*>(cf + ((e + 15) & ~15u));
+    uint16_t* rowid = pc + ((e + 7) & ~7u);
+    uint8_t* A = reinterpret_cast<uint8_t*>(rowid + ((e + 7) & ~7u));
+    __syncthreads();
+    auto gm = [&](uint8_t x, uint8_t y) -> uint8_t { return (x && y) ? ex[lg[x] + lg[y]] : (uint8_t)0; };
+    uint32_t np = 0;
+    for (uint32_t j = 0; j < nr && np < e; ++j) {
+        const uint8_t* mr = a.mrep + (size_t)U[j] * a.mrep_stride;
+        for (uint32_t c = tid; c < W2; c += nthr) v[c] = (c < e) ? mr[E[c]] : (uint8_t)(c == e + np);
+        __syncthreads();
+        for (uint32_t i = tid; i < np; i += nthr) cf[i] = v[pc[i]];
+        if (tid == 0) *piv = (int)e;
+        __syncthreads();
+        // v ^= sum_i cf[i] * basis_i (basis rows vanish on each other's pivot columns)
+        for (uint32_t c = tid; c < W2; c += nthr) {
+            uint8_t x = v[c];
+            for (uint32_t i = 0; i < np; ++i) {
+                const uint8_t f = cf[i];
+                if (f) x ^= gm(f, A[(size_t)i * W2 + c]);
+            }
+            v[c] = x;
+            if (c < e && x) atomicMin(piv, (int)c);
+        }
+        __syncthreads();
+        const uint32_t p = (uint32_t)*piv;
+        if (p >= e) {  // dependent on the rows kept so far
+            __syncthreads();
+            continue;
+        }
+        const uint8_t inv = ex[255 - lg[v[p]]];
+        __syncthreads();
+        for (uint32_t c = tid; c < W2; c += nthr) v[c] = gm(v[c], inv);
+        __syncthreads();
+        // clear column p from the basis, then append v
+        for (size_t idx = tid; idx < (size_t)np * W2; idx += nthr) {
+            const uint32_t i = (uint32_t)(idx / W2), c = (uint32_t)(idx - (size_t)i * W2);
+            const uint8_t f = A[(size_t)i * W2 + p];
+            if (f && c != p) A[idx] ^= gm(f, v[c]);
+        }
+        __syncthreads();
+        for (uint32_t i = tid; i < np; i += nthr) A[(size_t)i * W2 + p] = 0;
+        for (uint32_t c = tid; c < W2; c += nthr) A[(size_t)np * W2 + c] = v[c];
+        if (tid == 0) { pc[np] = (uint16_t)p; rowid[np] = (uint16_t)j; }
+        ++np;
+        __syncthreads();
+    }
+    if (np < e) {
+        if (tid == 0) a.status[b] = 0;
+        if (a.xb_on)
+            gi_stream<8, 5, 2>(a.xb, bi, b, e, false, tid, nthr, [](uint32_t, uint32_t) { return 0u; },
+                               [](uint32_t) { return 0u; });
+        return;
+    }
+    // basis row i solves erased column pc[i]: x_pc[i] = sum_m A[i][e + m] s_rowid[m]
+    uint8_t* xc = a.xcoef + 64ull * a.xoff[bi];
+    const uint32_t xs = x_stride(e);
+    uint16_t* XP = a.xpiv + a.erased_off[b];
+    for (uint32_t m = tid; m < e; m += nthr) XP[m] = rowid[m];
+    for (size_t idx = tid; idx < (size_t)e * e; idx += nthr) {
+        const uint32_t i = (uint32_t)(idx / e), m = (uint32_t)(idx - (size_t)i * e);
+        xc[(size_t)m * xs + pc[i]] = A[(size_t)i * W2 + e + m];
+    }
+    if (tid == 0) a.status[b] = 1;
+    if (a.xb_on) {  // the apply's stream from the X just written (visible to the workgroup after the barrier)
+        __syncthreads();
+        gi_stream<8, 5, 2>(a.xb, bi, b, e, true, tid, nthr, [&](uint32_t k, uint32_t m) { return (uint32_t)xc[(size_t)m * xs + k]; },
+                           [&](uint32_t m) { return (uint32_t)XP[m]; });
+    }
+}
+
 // The shipped solvers are k_solve_pq<1, 4> (e <= 64), k_solve_pq<2, 4> (e <= 128) and k_solve (any e);
 // the variants measured slower live in rq_kernels_exp.hip (experiments builds only).
 //
@@ -179,8 +264,12 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
     // (a late wave then sees column k already eliminated: a wrong X with status 1).
     using FC = typename std::conditional<PF, uint32_t, uint8_t>::type;
     __shared__ FC fcol[2][NROWS];
+    __shared__ int gpiv;  // general_block's pivot (inline_general)
+    static_assert(NROWS * SW * 4 >= 128 + 64 + 4 * 64 + 64 * 128, "general_block's working set for e <= 64 fits the rows");
     const uint32_t b = a.blk_map[blockIdx.x];
-    const uint32_t tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
+    // g made scalar: the per-step quad choice and its branches are then wave-uniform SALU, not exec-masked
+    // VALU (the compiler cannot prove tid >> 6 uniform)
+    const uint32_t tid = threadIdx.x, lane = tid & 63, g = __builtin_amdgcn_readfirstlane(tid >> 6);
     if (a.status_init)
         for (uint32_t i = blockIdx.x * NT + tid; i < a.n_all; i += gridDim.x * NT)
             if (a.status_init[i] != ST_PENDING) a.status[i] = a.status_init[i];
@@ -234,6 +323,23 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
     for (int q = 0; q < RPL; ++q) used[q] = lane + 64 * q >= nrow;
     const uint8_t* rb = reinterpret_cast<const uint8_t*>(rows);
     const uint32_t ksteps = a.diag_steps ? min(e, a.diag_steps) : e;
+    const bool inl = RPL == 1 && a.inline_general != 0;
+    // No pivot left (uniform over the block): rank-deficient on these rows.  With more received repairs
+    // the block is deferred to the later solvers, or (inline_general) finished here with all of them;
+    // otherwise final (status 0: the apply skips it).
+    auto no_pivot = [&]() {
+        if (nr > nrow && inl) {
+            __syncthreads();  // every wave is done with the rows (general_block's working set)
+            general_block(a, blockIdx.x, b, reinterpret_cast<uint8_t*>(rows), ex, lg, &gpiv, tid, NT);
+            if (tid == 0 && a.host_status) a.host_status[b] = a.status[b];
+            return;
+        }
+        if (tid == 0) a.status[b] = (nr > nrow) ? ST_FALLBACK : 0;
+        if (tid == 0 && inl && a.host_status) a.host_status[b] = 0;
+        if (a.xb_on && nr <= nrow)  // final: the apply skips it (a deferred block's solver writes its part)
+            gi_stream<8, 5, 2>(a.xb, blockIdx.x, b, e, false, tid, NT, [](uint32_t, uint32_t) { return 0u; },
+                               [](uint32_t) { return 0u; });
+    };
     if constexpr (RR) {
         constexpr uint32_t QR = (8 + NW - 1) / NW;  // quads per row this wave owns
         uint4* myrow = reinterpret_cast<uint4*>(rows + lane * SW);
@@ -246,10 +352,7 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
             const uint32_t pif = pinfo[f];
             const uint64_t bal = __ballot(f != 0 && !used0);
             if (!bal) {  // uniform over the block: every wave saw the same rows
-                if (tid == 0) a.status[b] = (nr > nrow) ? ST_FALLBACK : 0;
-                if (a.xb_on && nr <= nrow)
-                    gi_stream<8, 5, 2>(a.xb, blockIdx.x, b, e, false, tid, NT, [](uint32_t, uint32_t) { return 0u; },
-                                       [](uint32_t) { return 0u; });
+                no_pivot();
                 return;
             }
             const uint32_t p = (uint32_t)__ffsll((unsigned long long)bal) - 1;
@@ -324,10 +427,7 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
             if (bal) p = 64 * q + (uint32_t)__ffsll((unsigned long long)bal) - 1;
         }
         if (p == 0xFFFFFFFFu) {  // uniform over the block: every wave saw the same rows
-            if (tid == 0) a.status[b] = (nr > nrow) ? ST_FALLBACK : 0;
-            if (a.xb_on && nr <= nrow)  // final: the apply skips it (a deferred block's solver writes its part)
-                gi_stream<8, 5, 2>(a.xb, blockIdx.x, b, e, false, tid, NT, [](uint32_t, uint32_t) { return 0u; },
-                                   [](uint32_t) { return 0u; });
+            no_pivot();
             return;
         }
 #pragma unroll
@@ -366,9 +466,13 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
             if (w >= q1) break;
             const uint32_t px = __builtin_amdgcn_readfirstlane(P[j].x), py = __builtin_amdgcn_readfirstlane(P[j].y);
             const uint32_t pz = __builtin_amdgcn_readfirstlane(P[j].z), pw = __builtin_amdgcn_readfirstlane(P[j].w);
+            // a pivot-row quad of zeros leaves every row's quad as it is (the identity part of the pivot
+            // row is zero beyond the rows folded into it so far): a scalar branch skips its updates
+            const bool pzero = (px | py | pz | pw) == 0u;
 #pragma unroll
             for (int q = 0; q < RPL; ++q) {
                 uint4 r = R[q][j];
+                if (!pzero) {
 #ifdef RQHIP_EXPERIMENTS
                 if (a.diag & 8) {
                     r.x ^= px; r.y ^= py; r.z ^= pz; r.w ^= pw;
@@ -381,6 +485,7 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
                 r.w ^= perm_mul(A[q], B[q], pw);
                 }
                 if (act[q]) reinterpret_cast<uint4*>(rows + (lane + 64 * q) * SW)[w] = r;
+                }
                 if (kn < ksteps && w == (kn >> 4)) {  // wave-uniform: this wave owns column k + 1
                     const uint4 v = act[q] ? r : R[q][j];
                     const uint32_t d = (kn >> 2) & 3u;
@@ -390,9 +495,6 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
                 }
             }
         }
-#ifdef RQHIP_EXPERIMENTS
-        if (a.diag & 2) continue;
-#endif
         __syncthreads();
     }
     if (ksteps < e) {  // diagnostic step limit (timing only): valid pivot rows, meaningless X
@@ -415,6 +517,7 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
         }
     }
     if (tid == 0) a.status[b] = 1;
+    if (tid == 0 && inl && a.host_status) a.host_status[b] = 1;
 }
 
 
@@ -567,84 +670,7 @@ __global__ void __launch_bounds__(256) k_solve(SolveArgs a) {
         gf_tables_copy(ex, lg);
         tables = true;
     }
-    const uint32_t e = a.erased_off[b + 1] - a.erased_off[b];
-    const uint32_t nr = a.rep_cnt[b];
-    const uint32_t* E = a.erased + a.erased_off[b];
-    const uint32_t* U = a.rep_uidx + a.rep_off[b];
-    const uint32_t W2 = basis_width(e);
-    // v (W2) | coefficient of v on each basis row (e) | pc (e x u16) | rowid (e x u16) | basis (e x W2):
-    // in LDS for e <= lds_e, else in this block's global workspace (solve_ws_bytes(e))
-    uint8_t* v = (e <= a.lds_e) ? sm : a.gws + 64ull * a.goff[bi];
-    uint8_t* cf = v + W2;
-    uint16_t* pc = reinterpret_cast<uint16_t*>(cf + ((e + 15) & ~15u));
-    uint16_t* rowid = pc + ((e + 7) & ~7u);
-    uint8_t* A = reinterpret_cast<uint8_t*>(rowid + ((e + 7) & ~7u));
-    __syncthreads();
-    auto gm = [&](uint8_t x, uint8_t y) -> uint8_t { return (x && y) ? ex[lg[x] + lg[y]] : (uint8_t)0; };
-    uint32_t np = 0;
-    for (uint32_t j = 0; j < nr && np < e; ++j) {
-        const uint8_t* mr = a.mrep + (size_t)U[j] * a.mrep_stride;
-        for (uint32_t c = tid; c < W2; c += nthr) v[c] = (c < e) ? mr[E[c]] : (uint8_t)(c == e + np);
-        __syncthreads();
-        for (uint32_t i = tid; i < np; i += nthr) cf[i] = v[pc[i]];
-        if (tid == 0) piv = (int)e;
-        __syncthreads();
-        // v ^= sum_i cf[i] * basis_i (basis rows vanish on each other's pivot columns)
-        for (uint32_t c = tid; c < W2; c += nthr) {
-            uint8_t x = v[c];
-            for (uint32_t i = 0; i < np; ++i) {
-                const uint8_t f = cf[i];
-                if (f) x ^= gm(f, A[(size_t)i * W2 + c]);
-            }
-            v[c] = x;
-            if (c < e && x) atomicMin(&piv, (int)c);
-        }
-        __syncthreads();
-        const uint32_t p = (uint32_t)piv;
-        if (p >= e) {  // dependent on the rows kept so far
-            __syncthreads();
-            continue;
-        }
-        const uint8_t inv = ex[255 - lg[v[p]]];
-        __syncthreads();
-        for (uint32_t c = tid; c < W2; c += nthr) v[c] = gm(v[c], inv);
-        __syncthreads();
-        // clear column p from the basis, then append v
-        for (size_t idx = tid; idx < (size_t)np * W2; idx += nthr) {
-            const uint32_t i = (uint32_t)(idx / W2), c = (uint32_t)(idx - (size_t)i * W2);
-            const uint8_t f = A[(size_t)i * W2 + p];
-            if (f && c != p) A[idx] ^= gm(f, v[c]);
-        }
-        __syncthreads();
-        for (uint32_t i = tid; i < np; i += nthr) A[(size_t)i * W2 + p] = 0;
-        for (uint32_t c = tid; c < W2; c += nthr) A[(size_t)np * W2 + c] = v[c];
-        if (tid == 0) { pc[np] = (uint16_t)p; rowid[np] = (uint16_t)j; }
-        ++np;
-        __syncthreads();
-    }
-    if (np < e) {
-        if (tid == 0) a.status[b] = 0;
-        if (a.xb_on)
-            gi_stream<8, 5, 2>(a.xb, bi, b, e, false, tid, nthr, [](uint32_t, uint32_t) { return 0u; },
-                               [](uint32_t) { return 0u; });
-        __syncthreads();
-        continue;
-    }
-    // basis row i solves erased column pc[i]: x_pc[i] = sum_m A[i][e + m] s_rowid[m]
-    uint8_t* xc = a.xcoef + 64ull * a.xoff[bi];
-    const uint32_t xs = x_stride(e);
-    uint16_t* XP = a.xpiv + a.erased_off[b];
-    for (uint32_t m = tid; m < e; m += nthr) XP[m] = rowid[m];
-    for (size_t idx = tid; idx < (size_t)e * e; idx += nthr) {
-        const uint32_t i = (uint32_t)(idx / e), m = (uint32_t)(idx - (size_t)i * e);
-        xc[(size_t)m * xs + pc[i]] = A[(size_t)i * W2 + e + m];
-    }
-    if (tid == 0) a.status[b] = 1;
-    if (a.xb_on) {  // the apply's stream from the X just written (visible to the workgroup after the barrier)
-        __syncthreads();
-        gi_stream<8, 5, 2>(a.xb, bi, b, e, true, tid, nthr, [&](uint32_t k, uint32_t m) { return (uint32_t)xc[(size_t)m * xs + k]; },
-                           [&](uint32_t m) { return (uint32_t)XP[m]; });
-    }
+    general_block(a, bi, b, sm, ex, lg, &piv, tid, nthr);
     __syncthreads();  // the next block reuses the LDS
     }
     if (a.host_status) {  // this pass's blocks are final now (solved above, or by an earlier solver)
@@ -677,6 +703,10 @@ static bool knob_on(const char* name, bool dflt) {
     const char* e = std::getenv(name);
     return e ? e[0] != '0' : dflt;
 }
+static bool rr_knob() {
+    static const bool r = knob_on("RQHIP_SOLVE_RR", false);
+    return r;
+}
 #endif
 
 // The first solve in place (k_solve_ip, experiments library) or on [M | I] (k_solve_pq<1, 4>);
@@ -704,6 +734,9 @@ int launch_solve(const SolveArgs& a_in, uint32_t n_blocks, bool need_general, bo
     if (xbits_done) *xbits_done = first.xb_on != 0;
     first.diag_steps = 0;
     first.diag = 0;
+    // inline_general (no block with e > 64): the first solver finishes everything and writes the host
+    // statuses; only the shipped k_solve_pq<1, 4> implements it
+    first.inline_general = a_in.inline_general && !wide ? 1u : 0u;
     const hipStream_t st = (hipStream_t)stream;
 #ifdef RQHIP_EXPERIMENTS
     static const uint32_t dsteps = [] { const char* e = std::getenv("RQHIP_SOLVE_STEPS"); return e ? (uint32_t)std::atoi(e) : 0u; }();
@@ -713,10 +746,12 @@ int launch_solve(const SolveArgs& a_in, uint32_t n_blocks, bool need_general, bo
 #endif
     SolveArgs a = first;
     a.status_init = nullptr;
+    a.inline_general = 0;
 #ifdef RQHIP_EXPERIMENTS
+    if (!stream_ok || rr_knob()) first.inline_general = 0;  // the variants defer as before
     static const bool pm = knob_on("RQHIP_SOLVE_PM", true), lut = knob_on("RQHIP_SOLVE_LUT", true),
                       pq = knob_on("RQHIP_SOLVE_PQ", true), pf = knob_on("RQHIP_SOLVE_PF", false),
-                      lean = knob_on("RQHIP_SOLVE_LEAN", false), rr = knob_on("RQHIP_SOLVE_RR", false);
+                      lean = knob_on("RQHIP_SOLVE_LEAN", false), rr = rr_knob();
     static const int nw = [] { const char* e = std::getenv("RQHIP_SOLVE_NW"); return e ? std::atoi(e) : 4; }();
     // solvers that take `a` (statuses uploaded first): k_solve_fast and k_solve_reg
     const bool takes_a = !lean && ((nw == 1 && !pm) || (nw == 4 && !pm) || (nw != 1 && nw != 2 && nw != 4 && nw != 8));
@@ -734,7 +769,7 @@ int launch_solve(const SolveArgs& a_in, uint32_t n_blocks, bool need_general, bo
         else hipLaunchKernelGGL((k_solve_pq<1, 4>), dim3(n_blocks), dim3(256), 0, st, first);
         rx = (int)hipGetLastError();
     }
-    if (rx != hipSuccess || !need_general) return rx;
+    if (rx != hipSuccess || !need_general || first.inline_general) return rx;
     if (wide) {  // blocks with 64 < e <= 128; the rare rank-deficient-on-64-rows block goes to k_solve
         int rw = launch_solve_exp_wide(a, n_blocks, pm, lut, pq, stream);
         if (rw == -1) {
@@ -747,7 +782,7 @@ int launch_solve(const SolveArgs& a_in, uint32_t n_blocks, bool need_general, bo
     // e <= 64 on the first e + margin received repairs (statuses copied in by this launch)
     hipLaunchKernelGGL((k_solve_pq<1, 4>), dim3(n_blocks), dim3(256), 0, st, first);
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess || !need_general) return (int)e;
+    if (e != hipSuccess || !need_general || first.inline_general) return (int)e;
     if (wide) {  // blocks with 64 < e <= 128; the rare rank-deficient-on-64-rows block goes to k_solve
         hipLaunchKernelGGL((k_solve_pq<2, 4>), dim3(n_blocks), dim3(256), 0, st, a);
         if ((e = hipGetLastError()) != hipSuccess) return (int)e;

@@ -121,11 +121,49 @@ def test_rank_deficient_batch_and_second_pass(gpu, rq, oracle):
     more = [(data, {**h, **{e: syms[e] for e in range(N, N + 3)}}) for _, h in blocks]
     old = rq.lib().rq_debug_decode_margin(0)
     try:
-        st, out = _batch(rq, gpu, K, T, more, "sync")
+        # sync: the host's second pass; async: every received repair in one call, so the first solver
+        # finishes the block itself on all of them (inline_general)
+        res = {mode: _batch(rq, gpu, K, T, more, mode) for mode in ("sync", "async")}
     finally:
         rq.lib().rq_debug_decode_margin(old)
-    for b, (_, held) in enumerate(more):
-        ok, ref = _oracle_decode(oracle, data, T, held)
-        assert (st[b] == 1) == ok
-        if ok:
-            assert out[b].tobytes() == ref == data
+    for mode, (st, out) in res.items():
+        for b, (_, held) in enumerate(more):
+            ok, ref = _oracle_decode(oracle, data, T, held)
+            assert (st[b] == 1) == ok, (mode, b)
+            if ok:
+                assert out[b].tobytes() == ref == data, (mode, b)
+
+
+def test_first_solver_finishes_rank_deficient_rows_inline(gpu, rq, oracle):
+    """One erased source (e = 1) whose coefficient is zero in the first e + margin received repairs (the
+    first solver's rows are rank-deficient by construction) and nonzero in a later one: the block is
+    recovered in one call.  Round 6: with no block beyond e = 64 the first solver runs the general
+    algorithm on every received repair itself (SolveArgs::inline_general, general_block) instead of
+    deferring to a k_solve launch, and writes the async call's status; a block whose received repairs
+    all have a zero coefficient stays undecodable (status 0, as the oracle)."""
+    K, T, c = 32, 16, 5
+    rng = np.random.default_rng(41)
+    unit = np.zeros(K * T, np.uint8)
+    unit[c * T:(c + 1) * T] = 1
+    coef = oracle.OracleEncoder(unit.tobytes(), T)
+    margin = rq.lib().rq_debug_decode_margin(8)  # (returns the current margin; restored below)
+    rq.lib().rq_debug_decode_margin(margin)
+    zeros, esi = [], K  # the received list is sorted: its first e + margin rows are these
+    while len(zeros) < margin + 1:
+        if coef.gen_symbol(esi)[0] == 0:
+            zeros.append(esi)
+        esi += 1
+        assert esi < K + 40000, "not enough zero-coefficient repairs"
+    while coef.gen_symbol(esi)[0] == 0:
+        esi += 1
+    data = rng.integers(0, 256, K * T, dtype=np.uint8).tobytes()
+    syms = _oracle_symbols(oracle, data, T, list(range(K)) + zeros + [esi])
+    src = {i: syms[i] for i in range(K) if i != c}
+    solvable = {**src, **{e: syms[e] for e in zeros + [esi]}}
+    hopeless = {**src, **{e: syms[e] for e in zeros}}
+    assert _oracle_decode(oracle, data, T, solvable) == (True, data)
+    assert not _oracle_decode(oracle, data, T, hopeless)[0]
+    for mode in ("async", "sync"):
+        st, out = _batch(rq, gpu, K, T, [(data, solvable), (data, hopeless), (data, solvable)], mode)
+        assert list(st) == [1, 0, 1], (mode, st)
+        assert out[0].tobytes() == data and out[2].tobytes() == data, mode
