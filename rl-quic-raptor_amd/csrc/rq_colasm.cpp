@@ -350,6 +350,14 @@ struct Allocator {
                 mp->st.accw++;
                 last_accw[a] = (int)mp->ins.size() - 1;
                 owner[a] = v; reg[v] = (int16_t)a; owner[r] = -1;
+            } else if (is_agpr(r) && !freeV.empty()) {  // (an AGPR head row's register: to a free VGPR)
+                const int t = freeV.back();
+                freeV.pop_back();
+                const int32_t v = owner[r];
+                if (last_accw[r] >= (int)mp->ins.size() - 2) emit(MI_NOP, -1, -1, -1, -1, 1);
+                emit(MI_ACCR, t, r);
+                mp->st.accr++;
+                owner[t] = v; reg[v] = (int16_t)t; owner[r] = -1;
             } else {
                 spill_out(r);
             }
@@ -443,12 +451,15 @@ struct Allocator {
         // loads: its vmcnt counts then also cover the previous item's last stores, conservatively).  From
         // the node after the last source load on, cip_batch of them every cip_gap nodes are re-issued for
         // the next item into the same registers, vacated first.
-        const uint32_t n_cip = o.cip && !o.dma4 && !o.la_dma ? std::min<uint32_t>({o.cip, (uint32_t)ld.size(), o.n_vgpr / 2}) : 0;
+        const uint32_t n_cipv = o.cip && !o.dma4 && !o.la_dma ? std::min<uint32_t>({o.cip, (uint32_t)ld.size(), o.n_vgpr / 2}) : 0;
+        // experiments (cip_agpr): further head rows into the top AGPRs (read back by v_accvgpr_read at use)
+        const uint32_t n_cip = n_cipv ? n_cipv + std::min<uint32_t>({o.cip_agpr, (uint32_t)ld.size() - n_cipv, o.n_agpr / 2}) : 0;
         uint32_t t_pf = 0, cip_done = 0;
         for (uint32_t k = 0; k < n_cip; ++k) {
             const uint32_t v = ld[k];
-            const int r = (int)o.n_vgpr - 1 - (int)k;
-            freeV.erase(std::remove(freeV.begin(), freeV.end(), r), freeV.end());
+            const int r = k < n_cipv ? (int)o.n_vgpr - 1 - (int)k : REG_A0 + (int)o.n_agpr - 1 - (int)(k - n_cipv);
+            std::vector<int>& fl = is_agpr(r) ? freeA : freeV;
+            fl.erase(std::remove(fl.begin(), fl.end(), r), fl.end());
             const uint64_t q = issue_vmem();
             emit(MI_HEAD, r, -1, -1, -1, ir.nodes[v].imm);
             mp->st.ldsrc++;
@@ -868,6 +879,9 @@ void emit_cip_loads(const MProg& mp, uint32_t first, uint32_t n, bool next, uint
     }
     line("s_mov_b64 exec, s[54:55]");
     for (uint32_t k = first; k < first + n; ++k) {
+        // the prologue issues every head row at once: at most 48 outstanding before the next, well inside
+        // the 6-bit vmcnt (the tail's batches are bounded by the allocator, issue_pfx)
+        if (!next && k > first && (k - first) % 48 == 0) line("s_waitcnt vmcnt(24)");
         const int q = 42 + (int)(k % 6);
         std::snprintf(buf, sizeof buf, "s_mul_i32 s%d, s12, %u", q, mp.cip_row[k]); line(buf);
         std::snprintf(buf, sizeof buf, "buffer_load_dword %s, v%d, s[24:27], s%d offen%s", R(mp.cip_reg[k]).c_str(), rv.lds2, q,

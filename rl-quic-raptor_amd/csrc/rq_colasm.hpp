@@ -92,6 +92,7 @@ struct AllocOpts {
     uint32_t cip = 64;
     uint32_t cip_batch = 8;
     uint32_t cip_gap = 24;
+    uint32_t cip_agpr = 0;  // experiments: this many more head rows, into the top AGPRs
 };
 
 struct MProg {
