@@ -526,15 +526,18 @@ struct Allocator {
             // B back to back (fewer load/VALU transitions of the in-order issue)
             {
                 const uint32_t B = std::max<uint32_t>(1, o.load_batch);
+                // experiments (la_extra): a deeper look-ahead while la_free registers are free (the head and
+                // the tail of the program, where the live set is well below the file)
+                const uint32_t la = o.la_load + (o.la_extra && freeV.size() + freeA.size() >= o.la_free ? o.la_extra : 0);
                 size_t due = 0;
-                while (lp + due < loads.size() && loads[lp + due] <= i + o.la_load) ++due;
+                while (lp + due < loads.size() && loads[lp + due] <= i + la) ++due;
                 const bool go = B == 1 || due >= B || (lp < loads.size() && loads[lp] <= i + 8);
                 size_t quota = go ? std::max<size_t>(due, B) : 0;
                 while (quota && lp < loads.size()) {
                     const uint32_t v = loads[lp];
                     if (issued[v]) { ++lp; continue; }
                     if (uses[v].empty()) { issued[v] = 1; ++lp; continue; }
-                    if (B == 1 && v > i + o.la_load) break;
+                    if (B == 1 && v > i + la) break;
                     if (seq - retired >= o.max_vmem && v > i) break;
                     const int r = take_any(uses[v][0]);
                     if (r < 0) break;

@@ -93,6 +93,7 @@ struct AllocOpts {
     uint32_t cip_batch = 8;
     uint32_t cip_gap = 24;
     uint32_t cip_agpr = 0;  // experiments: this many more head rows, into the top AGPRs
+    uint32_t la_extra = 0, la_free = 96;  // experiments: look-ahead + la_extra while la_free registers are free
 };
 
 struct MProg {

@@ -398,6 +398,7 @@ const AllocOpts& alloc_options() {
         if (const char* h = knob("RQHIP_WAIT_AGE")) std::sscanf(h, "%u,%u", &r.wait_age, &r.lwait_age);
         if (const char* h = knob("RQHIP_LOAD_BATCH")) r.load_batch = (uint32_t)std::max(1, std::atoi(h));
         if (const char* h = knob("RQHIP_CIP")) std::sscanf(h, "%u,%u,%u,%u", &r.cip, &r.cip_batch, &r.cip_gap, &r.cip_agpr);
+        if (const char* h = knob("RQHIP_LA_ADAPT")) std::sscanf(h, "%u,%u", &r.la_extra, &r.la_free);
         if (const char* h = knob("RQHIP_WG"))
             if (std::atoi(h) > 1) r.cip = 0;  // the prefetch is a single-wave-workgroup layout
         return r;
