@@ -155,6 +155,27 @@ def test_cross_item_prefetch_under_register_pressure(rq, oracle, opts):
         assert np.array_equal(out[i], enc.gen_symbol(e)), e
 
 
+def test_cross_item_prefetch_random_shapes(rq, oracle):
+    """Seeded random (K, outputs, register budget, prefetch rows / batch / gap) combinations through the
+    two-item emulation: any head-register hand-over, vacate or vmcnt slip shows up as an emulator error
+    or wrong bytes."""
+    rng = np.random.default_rng(2026)
+    for it in range(40):
+        K = int(rng.integers(2, 300 if it % 4 else 1100))
+        T = 4 * int(rng.integers(1, 5))
+        nrep = int(rng.integers(1, 24))
+        esis = sorted(set(int(x) for x in rng.integers(K, K + 3 * nrep + 2, nrep))) + [int(rng.integers(0, K))]
+        nv = int(rng.choice([250, 120, 48, 24]))
+        na = int(rng.choice([256, 64, 8, 1]))
+        opts = [nv, na, int(rng.choice([0, 40, 320])), 0, int(rng.choice([0, 12, 56])), int(rng.choice([0, 9, 157])),
+                int(rng.integers(2, 80)), int(rng.integers(1, 17)), int(rng.integers(1, 64))]
+        data = rng.integers(0, 256, K * T, dtype=np.uint8)
+        out, st = rq.colprog_emulate(K, T, esis, data, opts)
+        enc = oracle.OracleEncoder(data.tobytes(), T)
+        for i, e in enumerate(esis):
+            assert np.array_equal(out[i], enc.gen_symbol(e)), (K, T, esis, opts, e)
+
+
 def test_cross_item_prefetch_assembly(rq):
     """The prologue loads the wave's first item's head rows and the tail the next item's, into the top
     VGPRs, with V_LDS2 as the offset register and the item's lane mask in s[54:55].  Past the wave's last
