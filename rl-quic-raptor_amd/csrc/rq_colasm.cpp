@@ -857,6 +857,7 @@ void emit_cip_loads(const MProg& mp, uint32_t first, uint32_t n, bool next, uint
             line("s_mov_b64 s[54:55], s[22:23]");
             std::snprintf(buf, sizeof buf, "s_branch .Lcipg%u", label); line(buf);
             lab("n");
+            line("s_mov_b64 exec, -1");  // the next item's offsets and mask on every lane, whatever this item's mask
         } else {
             std::snprintf(buf, sizeof buf, "s_cbranch_scc0 .Lcipe%u", label); line(buf);
         }
