@@ -270,6 +270,13 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
     // g made scalar: the per-step quad choice and its branches are then wave-uniform SALU, not exec-masked
     // VALU (the compiler cannot prove tid >> 6 uniform)
     const uint32_t tid = threadIdx.x, lane = tid & 63, g = __builtin_amdgcn_readfirstlane(tid >> 6);
+#ifdef RQHIP_SOLVE_STAMPS
+    // built with -DRQHIP_SOLVE_STAMPS (experiments only: device printf slows every solver launch ~2x even
+    // when it prints nothing), RQHIP_SOLVE_DIAG bit 16: phase stamps (100 MHz clock) of every 256th
+    // block's first thread
+    const bool stamp = (a.diag & 16) && blockIdx.x % 256 == 0 && tid == 0;
+    uint64_t t_0 = stamp ? __builtin_amdgcn_s_memrealtime() : 0, t_1 = 0, t_2 = 0;
+#endif
     if (a.status_init)
         for (uint32_t i = blockIdx.x * NT + tid; i < a.n_all; i += gridDim.x * NT)
             if (a.status_init[i] != ST_PENDING) a.status[i] = a.status_init[i];
@@ -318,6 +325,9 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
     }
     __syncthreads();
     const uint32_t q1 = (e + nrow + 15) >> 4;  // quads holding live columns
+#ifdef RQHIP_SOLVE_STAMPS
+    if (stamp) t_1 = __builtin_amdgcn_s_memrealtime();
+#endif
     bool used[RPL];
 #pragma unroll
     for (int q = 0; q < RPL; ++q) used[q] = lane + 64 * q >= nrow;
@@ -502,6 +512,9 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
         for (uint32_t m = ksteps + tid; m < e; m += NT) pivl[m] = (uint8_t)m;
         __syncthreads();
     }
+#ifdef RQHIP_SOLVE_STAMPS
+    if (stamp) t_2 = __builtin_amdgcn_s_memrealtime();
+#endif
     uint8_t* xc = a.xcoef + 64ull * a.xoff[blockIdx.x];
     const uint32_t xs = x_stride(e);
     uint16_t* XP = a.xpiv + a.erased_off[b];
@@ -518,6 +531,13 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
     }
     if (tid == 0) a.status[b] = 1;
     if (tid == 0 && inl && a.host_status) a.host_status[b] = 1;
+#ifdef RQHIP_SOLVE_STAMPS
+    if (stamp) {
+        const uint64_t t_3 = __builtin_amdgcn_s_memrealtime();
+        printf("[solve-stamp] block %u e %u setup %llu loop %llu out %llu (10 ns ticks)\n", blockIdx.x, e,
+               (unsigned long long)(t_1 - t_0), (unsigned long long)(t_2 - t_1), (unsigned long long)(t_3 - t_2));
+    }
+#endif
 }
 
 
