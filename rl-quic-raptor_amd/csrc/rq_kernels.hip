@@ -331,6 +331,9 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
     bool used[RPL];
 #pragma unroll
     for (int q = 0; q < RPL; ++q) used[q] = lane + 64 * q >= nrow;
+    uint64_t usedm[RPL];
+#pragma unroll
+    for (int q = 0; q < RPL; ++q) usedm[q] = __ballot(used[q]);
     const uint8_t* rb = reinterpret_cast<const uint8_t*>(rows);
     const uint32_t ksteps = a.diag_steps ? min(e, a.diag_steps) : e;
     const bool inl = RPL == 1 && a.inline_general != 0;
@@ -432,17 +435,15 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
         }
         uint32_t p = 0xFFFFFFFFu;
 #pragma unroll
-        for (int q = RPL - 1; q >= 0; --q) {
-            const uint64_t bal = __ballot(f[q] != 0 && !used[q]);
+        for (int q = RPL - 1; q >= 0; --q) {  // (the used rows as a scalar mask: no per-lane flag to test)
+            const uint64_t bal = __ballot(f[q] != 0) & ~usedm[q];
             if (bal) p = 64 * q + (uint32_t)__ffsll((unsigned long long)bal) - 1;
         }
         if (p == 0xFFFFFFFFu) {  // uniform over the block: every wave saw the same rows
             no_pivot();
             return;
         }
-#pragma unroll
-        for (int q = 0; q < RPL; ++q)
-            if (lane + 64 * q == p) used[q] = true;
+        usedm[p >> 6] |= 1ull << (p & 63u);
         if (tid == 0) pivl[k] = (uint8_t)p;
         uint4 P[QW];
         const uint4* prow = reinterpret_cast<const uint4*>(rows + p * SW);
@@ -497,10 +498,14 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
                 if (act[q]) reinterpret_cast<uint4*>(rows + (lane + 64 * q) * SW)[w] = r;
                 }
                 if (kn < ksteps && w == (kn >> 4)) {  // wave-uniform: this wave owns column k + 1
-                    const uint4 v = act[q] ? r : R[q][j];
+                    // the dword first (d is uniform: a scalar branch), then the updated or old value
                     const uint32_t d = (kn >> 2) & 3u;
-                    const uint32_t dw = d == 0 ? v.x : d == 1 ? v.y : d == 2 ? v.z : v.w;
-                    const uint32_t fb = (dw >> ((kn & 3u) * 8)) & 0xFFu;
+                    uint32_t dn, dold;
+                    if (d == 0) { dn = r.x; dold = R[q][j].x; }
+                    else if (d == 1) { dn = r.y; dold = R[q][j].y; }
+                    else if (d == 2) { dn = r.z; dold = R[q][j].z; }
+                    else { dn = r.w; dold = R[q][j].w; }
+                    const uint32_t fb = ((act[q] ? dn : dold) >> ((kn & 3u) * 8)) & 0xFFu;
                     fcol[kn & 1][lane + 64 * q] = PF ? (FC)pinfo[fb] : (FC)fb;
                 }
             }
