@@ -87,6 +87,12 @@ uint32_t rq_debug_decode_margin(uint32_t margin);
  * leave it) and returns the previous one; both give the same bytes.  Mode 1 also takes k_apply for a
  * batch beyond the register-table stream's bound (rq_debug_gi_fits). */
 uint32_t rq_debug_apply_mode(uint32_t mode);
+/* Experiments library: 1 = with the register-table apply, the first solver launch also XORs the received
+ * repair rows into their r0 rows (s = received ^ r0, beside the solves) and the apply loads one row per
+ * syndrome; 0 (the default) = the apply loads both rows.  Taken only for T % 16 == 0 and a 16-byte aligned
+ * repair buffer.  Sets the switch (values > 1 leave it) and returns the previous one; both give the same
+ * bytes.  The release library has no such path: it returns 0 and leaves the switch at 0. */
+uint32_t rq_debug_apply_sx(uint32_t on);
 /* 1 if a decode whose solve list has n_solve blocks and largest erasure count max_e runs the
  * register-table apply (its index stream: e <= 512 and at most 512 MiB for the list), 0 if k_apply. */
 int rq_debug_gi_fits(uint32_t max_e, uint32_t n_solve);
@@ -97,7 +103,8 @@ int rq_debug_gi_fits(uint32_t max_e, uint32_t n_solve);
 uint32_t rq_debug_solve_mode(uint32_t mode);
 /* The register-table apply kernel's assembly for shape (KC outputs per wave, groups of G syndromes,
  * loads PDG groups ahead, CPL dword columns per lane in bits 7:0 of cpl, two subset numbers per index
- * dword when bit 8 is set): copied into text (cap bytes, NUL-terminated) when given, its length in
+ * dword when bit 8 is set, one precomputed syndrome row per syndrome instead of the received and r0
+ * rows when bit 9 is set): copied into text (cap bytes, NUL-terminated) when given, its length in
  * *text_len, and, when code_bytes is given, assembled in process (its code object size). */
 int rq_debug_apply_gi_asm(uint32_t kc, uint32_t g, uint32_t pdg, uint32_t cpl, char* text, size_t cap, size_t* text_len,
                           size_t* code_bytes);

@@ -47,22 +47,22 @@ struct Asm {
 
 bool gi_shape_ok(const GiShape& sh) {
     return sh.KC >= 4 && sh.KC <= 16 && sh.KC % (sh.PACK ? 8 : 4) == 0 && sh.G >= 4 && sh.G <= 6 && sh.PDG >= 1 &&
-           sh.PDG <= 2 && sh.CPL >= 1 && sh.CPL <= 2 && sh.PACK <= 1 && gi_vgprs(sh) <= 256;
+           sh.PDG <= 2 && sh.CPL >= 1 && sh.CPL <= 2 && sh.PACK <= 1 && sh.SX <= 1 && gi_vgprs(sh) <= 256;
 }
 
 // VGPRs: v0 lane (prologue only), v1 the lane's byte offset in a row (column c at + 256 c), the syndrome
-// ring from v2 (per column, PDG slots of G received-row + G r0-row values; v2..v7 double as Horner
-// temporaries at the end), per column a table of 2^G entries (entry 0 = 0), then per column the KC x 8
-// bit planes (plane 0 starts as g_E).
+// ring from v2 (per column, PDG slots of G received-row + G r0-row values, or of G syndromes with SX; v2..v7
+// double as Horner temporaries at the end), per column a table of 2^G entries (entry 0 = 0), then per
+// column the KC x 8 bit planes (plane 0 starts as g_E).
 namespace {
-uint32_t gi_tb(const GiShape& sh) { return (2 + 2 * sh.G * sh.PDG * sh.CPL + 3) & ~3u; }
+uint32_t gi_tb(const GiShape& sh) { return (2 + (sh.SX ? 1 : 2) * sh.G * sh.PDG * sh.CPL + 3) & ~3u; }
 }  // namespace
 
 uint32_t gi_vgprs(const GiShape& sh) { return gi_tb(sh) + sh.CPL * ((1u << sh.G) + 8 * sh.KC); }
 
 std::string gi_kernel_name(const GiShape& sh) {
     return "rq_apply_gi_k" + std::to_string(sh.KC) + "_g" + std::to_string(sh.G) + "_p" + std::to_string(sh.PDG) +
-           "_c" + std::to_string(sh.CPL) + (sh.PACK ? "_x2" : "") + (sh.stpol ? "_st" + std::to_string(sh.stpol) : std::string()) + (sh.diag ? "_d" + std::to_string(sh.diag) : std::string());
+           "_c" + std::to_string(sh.CPL) + (sh.PACK ? "_x2" : "") + (sh.SX ? "_s" : "") + (sh.stpol ? "_st" + std::to_string(sh.stpol) : std::string()) + (sh.diag ? "_d" + std::to_string(sh.diag) : std::string());
 }
 
 std::string emit_apply_gi_asm(const GiShape& sh) {
@@ -71,8 +71,10 @@ std::string emit_apply_gi_asm(const GiShape& sh) {
     const uint32_t PK = sh.PACK, PAIRS = PK ? KC / 8 : KC / 4;  // 32 index dwords per pair of 16-dword pieces
     const uint32_t UNR = (PDG * PAIRS) % 2 ? 2 * PDG : PDG;  // groups per loop body: ring slots, and pieces A/B alternate
     const std::string kname = gi_kernel_name(sh);
-    auto RA = [&](uint32_t c, uint32_t p, uint32_t t) { return RING + (c * PDG + p) * 2 * G + t; };
-    auto RB = [&](uint32_t c, uint32_t p, uint32_t t) { return RING + (c * PDG + p) * 2 * G + G + t; };
+    // ring slot (c, p): G received-row values (RA) then G r0-row values (RB); with SX only the G syndromes (RB)
+    const uint32_t SX = sh.SX, RW = SX ? 1 : 2;
+    auto RA = [&](uint32_t c, uint32_t p, uint32_t t) { return RING + (c * PDG + p) * RW * G + t; };
+    auto RB = [&](uint32_t c, uint32_t p, uint32_t t) { return RING + (c * PDG + p) * RW * G + (SX ? 0 : G) + t; };
     auto TBC = [&](uint32_t c) { return TB + c * NT; };
     auto ACC = [&](uint32_t c, uint32_t k, uint32_t b) { return AC + (c * KC + k) * 8 + b; };
     // column c's memory operations: the row offset + 256 c, under column c's exec mask (s[96:97] for c = 1)
@@ -170,7 +172,7 @@ std::string emit_apply_gi_asm(const GiShape& sh) {
             a.f("buffer_load_dword v%u, v1, s[56:59], s%u offen offset:%u", ACC(c, k, 0), 80 + k, 256 * c);
         for (uint32_t p = 0; p < PDG; ++p)
             for (uint32_t t = 0; t < G; ++t) {
-                a.f("buffer_load_dword v%u, v1, s[48:51], s%u offen offset:%u", RA(c, p, t), 16 * p + 2 * t, 256 * c);
+                if (!SX) a.f("buffer_load_dword v%u, v1, s[48:51], s%u offen offset:%u", RA(c, p, t), 16 * p + 2 * t, 256 * c);
                 a.f("buffer_load_dword v%u, v1, s[52:55], s%u offen offset:%u", RB(c, p, t), 16 * p + 2 * t + 1, 256 * c);
             }
         col_exec(a, c, false);
@@ -197,15 +199,17 @@ std::string emit_apply_gi_asm(const GiShape& sh) {
         for (uint32_t r = 64; r < 96; r += 2) a.f("s_mov_b64 s[%u:%u], 0", r, r + 1);
     }
     // ---- the groups: UNR copies of the body (ring slot p = u mod PDG), each ending in the exit test
-    const uint32_t loads_per_group = 2 * G * CPL;
+    const uint32_t loads_per_group = RW * G * CPL;
     a.s += ".Lgroup:\n";
     uint32_t pair_no = 0;  // pieces alternate A, B over the whole body
     for (uint32_t u = 0; u < UNR; ++u) {
         const uint32_t p = u % PDG;
         a.f("s_waitcnt vmcnt(%u)", loads_per_group * (PDG - 1));
         for (uint32_t c = 0; c < CPL; ++c) {
-            for (uint32_t t = 0; t < G; ++t)
-                a.f("v_xor_b32_e32 v%u, v%u, v%u", TBC(c) + (1u << t), RA(c, p, t), RB(c, p, t));
+            for (uint32_t t = 0; t < G; ++t) {
+                if (SX) a.f("v_mov_b32_e32 v%u, v%u", TBC(c) + (1u << t), RB(c, p, t));
+                else a.f("v_xor_b32_e32 v%u, v%u, v%u", TBC(c) + (1u << t), RA(c, p, t), RB(c, p, t));
+            }
             for (uint32_t i = 3; i < NT; ++i) {
                 if ((i & (i - 1)) == 0) continue;
                 const uint32_t lo = i & (0u - i);
@@ -217,7 +221,7 @@ std::string emit_apply_gi_asm(const GiShape& sh) {
             for (uint32_t c = 0; c < CPL; ++c) {  // the group PDG ahead into the slot just consumed
                 col_exec(a, c, true);
                 for (uint32_t t = 0; t < G; ++t) {
-                    a.f("buffer_load_dword v%u, v1, s[48:51], s%u offen offset:%u", RA(c, p, t), 32 + 2 * t, 256 * c);
+                    if (!SX) a.f("buffer_load_dword v%u, v1, s[48:51], s%u offen offset:%u", RA(c, p, t), 32 + 2 * t, 256 * c);
                     a.f("buffer_load_dword v%u, v1, s[52:55], s%u offen offset:%u", RB(c, p, t), 33 + 2 * t, 256 * c);
                 }
                 col_exec(a, c, false);

@@ -52,6 +52,9 @@ struct GiShape {
     uint32_t PACK = 0;  // 1: two subset numbers per index dword (the high one by s_lshr_b32)
     uint32_t diag = 0;  // experiments (timing only, wrong bytes): 1 no index loads, 2 no syndrome loads, 4 no lookups
     uint32_t stpol = 0; // experiments: recovered-row store policy, 0 plain, 1 nt, 2 sc1, 3 sc0 sc1
+    // 1: the syndromes s = received ^ r0 are already in the r0 rows (the first solver launch's XOR
+    // workgroups, SolveArgs::sx_wgs, experiments library): one load per syndrome, a ring of G values per slot
+    uint32_t SX = 0;
 };
 
 // Per block bi of the solve list, the dword stream k_xbits writes at gi + bi * block and the apply kernel
@@ -140,6 +143,13 @@ struct SolveArgs {
     // rows with every received repair itself (general_block on its LDS rows) instead of deferring it, and
     // writes host_status for its blocks.  Set when no block has e > 64: no later solver launch then.
     uint32_t inline_general;
+    // Experiments library (RQHIP_APPLY_SX=1; measured not to pay):
+    // the last sx_wgs workgroups of the first solver launch (k_solve_pq<1, 4>) solve nothing: they XOR
+    // every received repair row of the solve list into its r0 row (xb.recv, xb.r0), so the apply reads
+    // s = received ^ r0 with one load per syndrome.  They need no HBM bandwidth the solvers use and run
+    // on the wave slots the solvers leave free.  0: off.
+    uint32_t sx_wgs;
+    uint32_t sx_pol;            // experiments (RQHIP_SX_POL): 1 non-temporal s stores, 2 non-temporal received loads
 };
 constexpr int32_t ST_PENDING = -100;   // queued for the solver
 constexpr int32_t ST_FALLBACK = -101;  // beyond the fast solvers: the general solver decides
@@ -192,8 +202,10 @@ int launch_pack_rows(const PackArgs& a, void* stream);
 // need_general: some block may end in the general solver (e or candidate repairs > 64); wide: some
 // block has 64 < e <= 128 (the two-row-per-lane fast solver runs first).
 // xbits_done (optional): set when the launches also wrote the index stream of a.xb (a.xb_on and k_solve ran).
+// sx_done (optional): set when the first launch also ran a.sx_wgs syndrome workgroups (the r0 rows then
+// hold s = received ^ r0 for every received repair of the solve list).
 int launch_solve(const SolveArgs& a, uint32_t n_blocks, bool need_general, bool wide, uint32_t max_lds_e,
-                 void* stream, bool* xbits_done = nullptr);
+                 void* stream, bool* xbits_done = nullptr, bool* sx_done = nullptr);
 int launch_apply(const ApplyArgs& a, uint32_t n_strips, uint32_t n_blocks, void* stream);
 int launch_gather(const DevParams& p, const uint8_t* C, uint32_t T, const uint32_t* esi, uint32_t n, uint8_t* out,
                   void* stream);

@@ -234,10 +234,11 @@ struct DevCtx {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> tev;
     size_t tev_used = 0;
     hipStream_t obj_stream = nullptr;  // per-object API: its own stream, pinned staging, device buffer
-    // the register-table apply kernel (rq_applygi.cpp), assembled on first use for `gi_shape`
-    hipModule_t gi_mod = nullptr;
-    hipFunction_t gi_fn = nullptr;
-    GiShape gi_shape;
+    // the register-table apply kernels (rq_applygi.cpp), assembled on first use for `gi_shape`: slot 1
+    // reads precomputed syndromes (GiShape::SX), slot 0 the received and r0 rows
+    hipModule_t gi_mod[2] = {};
+    hipFunction_t gi_fn[2] = {};
+    GiShape gi_shape[2];
     HostBuf obj_h;
     DevBuf obj_d;
     // Per-stream workspaces are bounded: a caller that uses a fresh stream per window would otherwise
@@ -288,7 +289,8 @@ struct DevCtx {
         ws.clear();
         dead.clear();
         colk.clear();
-        if (gi_mod) (void)hipModuleUnload(gi_mod);
+        for (hipModule_t m : gi_mod)
+            if (m) (void)hipModuleUnload(m);
         for (Stage& st : stage)
             if (st.s) (void)hipStreamDestroy(st.s);
         for (hipEvent_t e : kdone)
@@ -1197,6 +1199,9 @@ bool solve_beside() {
 // The decode's apply: 1 = the register-table kernel (rq_applygi.cpp, k_xbits + the generated kernel),
 // 0 = k_apply's v_perm byte tables.  rq_debug_apply_mode switches it (tests compare the two).
 uint32_t g_apply_mode = 1;
+// 1: the register-table apply reads syndromes precomputed beside the first solver (GiShape::SX; experiments
+// library only, RQHIP_APPLY_SX=1 or rq_debug_apply_sx: measured not to pay).
+uint32_t g_apply_sx = knob("RQHIP_APPLY_SX") && knob("RQHIP_APPLY_SX")[0] == '1' ? 1u : 0u;
 // Stream bound of the register-table apply: e <= kGiMaxE and the whole stream of the solve
 // list <= kGiMaxBytes.  Within it every byte offset the kernel forms (block base, slice records, their
 // one-pair prefetch) stays far below 2^32 and the allocation stays small; config 3 (e ~ 60) needs 27 MB.
@@ -1231,10 +1236,11 @@ const GiShape& apply_gi_shape() {
 
 // The apply kernel of this device, assembled (amd_comgr, in process) on first use.  Caller holds ctx->mu.
 int get_gi_kernel(DevCtx* ctx, const GiShape& sh, hipFunction_t* fn) {
-    if (ctx->gi_fn && ctx->gi_shape.KC == sh.KC && ctx->gi_shape.G == sh.G && ctx->gi_shape.PDG == sh.PDG &&
-        ctx->gi_shape.CPL == sh.CPL && ctx->gi_shape.PACK == sh.PACK && ctx->gi_shape.diag == sh.diag &&
-        ctx->gi_shape.stpol == sh.stpol) {
-        *fn = ctx->gi_fn;
+    const uint32_t slot = sh.SX ? 1 : 0;
+    const GiShape& have = ctx->gi_shape[slot];
+    if (ctx->gi_fn[slot] && have.KC == sh.KC && have.G == sh.G && have.PDG == sh.PDG && have.CPL == sh.CPL &&
+        have.PACK == sh.PACK && have.diag == sh.diag && have.stpol == sh.stpol) {
+        *fn = ctx->gi_fn[slot];
         return RQ_OK;
     }
     std::vector<char> co;
@@ -1248,10 +1254,10 @@ int get_gi_kernel(DevCtx* ctx, const GiShape& sh, hipFunction_t* fn) {
         if (mod) (void)hipModuleUnload(mod);
         return fail(RQ_ERR_DEVICE, "apply kernel load failed");
     }
-    if (ctx->gi_mod) (void)hipModuleUnload(ctx->gi_mod);  // a shape change (experiments): idle by then
-    ctx->gi_mod = mod;
-    ctx->gi_fn = f;
-    ctx->gi_shape = sh;
+    if (ctx->gi_mod[slot]) (void)hipModuleUnload(ctx->gi_mod[slot]);  // a shape change (experiments): idle by then
+    ctx->gi_mod[slot] = mod;
+    ctx->gi_fn[slot] = f;
+    ctx->gi_shape[slot] = sh;
     *fn = f;
     return RQ_OK;
 }
@@ -1272,8 +1278,17 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     // gi_stream_fits' bound; a batch beyond it (one block with e in the thousands) takes k_apply, whose
     // working set is e x 64 bytes of X per block.
     const bool gi = g_apply_mode == 1 && gi_stream_fits(max_e, nw, gsh);
-    hipFunction_t gi_fn = nullptr;
+    // Precomputed syndromes (GiShape::SX, experiments library): the first solver launch's extra workgroups
+    // XOR the received rows into the r0 rows beside the solves, and the apply loads one row per syndrome.
+    // Needs the r0 rows final before the solver (not the solve beside the syndrome program), 16-byte rows
+    // and a 16-byte aligned received-row buffer.  Apply -13 us, but the solve +5..27 us and the next
+    // column-program launch +5..8 us (profiles/r06_sx): off, and absent from the release library.
+    const bool want_sx = gi && g_apply_sx && T % 16 == 0 && (reinterpret_cast<uintptr_t>(repair) & 15) == 0;
+    GiShape gsx = gsh;
+    gsx.SX = 1;
+    hipFunction_t gi_fn = nullptr, gi_fn_sx = nullptr;
     if (gi && (rc = get_gi_kernel(ctx, gsh, &gi_fn))) return rc;
+    if (want_sx && (rc = get_gi_kernel(ctx, gsx, &gi_fn_sx))) return rc;
     const bool need_general = pl.need_general, wide = pl.wide;
     const uint64_t xo = pl.xo, go = pl.go;
     const size_t nz = pl.nz;
@@ -1501,9 +1516,15 @@ int decode_pass(DevCtx* ctx, const Params& p, uint32_t T, uint32_t n_blocks, voi
     // kernel and its gap, ~8 us per call).  Without the general solver the download stays.
     const bool status_by_solver = async && status_dev && need_general && !po;
     s.host_status = status_by_solver ? status_dev : nullptr;
-    bool xbits_done = false;
-    if (launch_solve(s, nw, need_general, wide, max_lds_e, beside ? (void*)w->cs : stream, &xbits_done))
+    // two blocks per syndrome workgroup: two such workgroups per CU run beside the four solving ones
+    static const uint32_t sx_cap = [] { const char* e = knob("RQHIP_SX_WGS"); return e ? (uint32_t)std::max(1, std::atoi(e)) : 512u; }();
+    static const uint32_t sx_pol = [] { const char* e = knob("RQHIP_SX_POL"); return e ? (uint32_t)std::atoi(e) & 31u : 0u; }();
+    s.sx_wgs = want_sx && !beside && nw && max_e ? std::min<uint32_t>(sx_cap, (nw + 1) / 2) : 0u;
+    s.sx_pol = sx_pol;
+    bool xbits_done = false, sx_done = false;
+    if (launch_solve(s, nw, need_general, wide, max_lds_e, beside ? (void*)w->cs : stream, &xbits_done, &sx_done))
         return fail(RQ_ERR_DEVICE, "k_solve launch failed");
+    if (sx_done) gi_fn = gi_fn_sx;  // the r0 rows hold the syndromes now
     if (beside) {
         HIP_TRY(hipEventRecord(w->solved, w->cs));
         if ((rc = launch_col(ctx, k, T, n_blocks, data, data_stride, w->r0.p, (uint64_t)uni.size() * T, stream)))
@@ -2456,9 +2477,10 @@ uint32_t rq_debug_virtual_shards(uint32_t n) {
 int rq_debug_apply_gi_asm(uint32_t kc, uint32_t g, uint32_t pdg, uint32_t cpl, char* text, size_t cap, size_t* text_len,
                           size_t* code_bytes) {
     GiShape sh;
-    sh.KC = kc; sh.G = g; sh.PDG = pdg; sh.CPL = cpl & 0xff; sh.PACK = cpl >> 8;
+    sh.KC = kc; sh.G = g; sh.PDG = pdg; sh.CPL = cpl & 0xff; sh.PACK = (cpl >> 8) & 1; sh.SX = (cpl >> 9) & 1;
     if (!gi_shape_ok(sh))
-        return fail(RQ_ERR_BAD_ARG, "apply shape: KC 4..16 (a multiple of 4, of 8 packed), G 4..6, PDG 1..2, CPL 1..2, <= 256 VGPRs");
+        return fail(RQ_ERR_BAD_ARG, "apply shape: KC 4..16 (a multiple of 4, of 8 packed), G 4..6, PDG 1..2, CPL 1..2 "
+                                    "(| 256 packed, | 512 precomputed syndromes), <= 256 VGPRs");
     const std::string src = emit_apply_gi_asm(sh);
     std::string cerr;
     if (!check_apply_gi_asm(src, sh, &cerr)) return fail(RQ_ERR_PLAN, cerr);
@@ -2512,7 +2534,7 @@ int rq_debug_gi_stream(uint32_t e, uint32_t max_e, uint32_t solved, const uint8_
 
 int rq_debug_apply_gi_check(uint32_t kc, uint32_t g, uint32_t pdg, uint32_t cpl, const char* text) {
     GiShape sh;
-    sh.KC = kc; sh.G = g; sh.PDG = pdg; sh.CPL = cpl & 0xff; sh.PACK = cpl >> 8;
+    sh.KC = kc; sh.G = g; sh.PDG = pdg; sh.CPL = cpl & 0xff; sh.PACK = (cpl >> 8) & 1; sh.SX = (cpl >> 9) & 1;
     if (!text || !gi_shape_ok(sh)) return fail(RQ_ERR_BAD_ARG, "apply shape or text");
     std::string err;
     return check_apply_gi_asm(text, sh, &err) ? RQ_OK : fail(RQ_ERR_PLAN, err);
@@ -2531,6 +2553,16 @@ uint32_t rq_debug_solve_mode(uint32_t mode) {
 uint32_t rq_debug_apply_mode(uint32_t mode) {
     const uint32_t old = g_apply_mode;
     if (mode <= 1) g_apply_mode = mode;
+    return old;
+}
+
+uint32_t rq_debug_apply_sx(uint32_t on) {
+    const uint32_t old = g_apply_sx;
+#ifdef RQHIP_EXPERIMENTS
+    if (on <= 1) g_apply_sx = on;
+#else
+    (void)on;  // the release library has no syndrome workgroups (experiments library only)
+#endif
     return old;
 }
 

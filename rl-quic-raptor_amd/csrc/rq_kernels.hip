@@ -217,12 +217,94 @@ __device__ __forceinline__ void general_block(const SolveArgs& a, uint32_t bi, u
         xc[(size_t)m * xs + pc[i]] = A[(size_t)i * W2 + e + m];
     }
     if (tid == 0) a.status[b] = 1;
+#ifdef RQHIP_EXPERIMENTS
+    if (a.sx_wgs && a.inline_general && a.row_margin && !(a.sx_pol & 16)) {
+        // the first solver launch's syndrome workgroups XOR the first e + margin received rows (sx_rows);
+        // a pivot row past them is XORed here (rows disjoint from theirs, so no race)
+        typedef uint32_t V4 __attribute__((ext_vector_type(4)));
+        const uint32_t xc = min(nr, e + a.row_margin), T = a.xb.T, cpr = T >> 4;
+        const uint8_t* rv = a.xb.recv + (size_t)a.rep_off[b] * T;
+        uint8_t* rz = const_cast<uint8_t*>(a.xb.r0) + (size_t)b * a.xb.n_union * T;
+        for (uint32_t m = 0; m < e; ++m) {
+            const uint32_t j = rowid[m];
+            if (j < xc) continue;
+            const V4* pv = reinterpret_cast<const V4*>(rv + (size_t)j * T);
+            V4* pz = reinterpret_cast<V4*>(rz + (size_t)U[j] * T);
+            for (uint32_t c = tid; c < cpr; c += nthr) pz[c] = pv[c] ^ pz[c];
+        }
+    }
+#endif
     if (a.xb_on) {  // the apply's stream from the X just written (visible to the workgroup after the barrier)
         __syncthreads();
         gi_stream<8, 5, 2>(a.xb, bi, b, e, true, tid, nthr, [&](uint32_t k, uint32_t m) { return (uint32_t)xc[(size_t)m * xs + k]; },
                            [&](uint32_t m) { return (uint32_t)XP[m]; });
     }
 }
+
+#ifdef RQHIP_EXPERIMENTS
+// Experiments library only (RQHIP_APPLY_SX=1; measured not to pay).
+// The syndromes for the register-table apply (SolveArgs::sx_wgs): workgroup w of nwk XORs every received
+// repair row of blocks bi = w, w + nwk, ... of the solve list into its r0 row, in place (a block's rows are
+// distinct r0 rows), so that the r0 rows hold s = received ^ r0.  A block's rows are one flat range of
+// 16-byte pieces (row j, piece c), dealt to the threads 256 at a time, U steps in flight per thread (the
+// loads of all U before any store); the rows' r0 positions are staged in LDS (ru, cap entries).  T is a
+// multiple of 16 and the received rows 16-byte aligned (the host checks both).  No solver reads the
+// syndrome rows, so this runs beside them in the same launch, on the wave slots they leave free.
+template <uint32_t NT, uint32_t U>
+__device__ __forceinline__ void sx_rows(const SolveArgs& a, uint32_t w, uint32_t nwk, uint32_t tid, uint32_t* ru,
+                                        uint32_t cap) {
+    typedef uint32_t V4 __attribute__((ext_vector_type(4)));
+    const XbitsArgs& x = a.xb;
+    const uint32_t T = x.T, cpr = T >> 4, dq = NT / cpr, dr = NT % cpr;
+    const uint32_t pol = a.sx_pol;  // experiments: 1 non-temporal stores, 2 non-temporal received-row loads
+    // (timing only, wrong bytes: 4 no work at all, 8 the loads without the stores)
+    if (pol & 4) return;
+    for (uint32_t bi = w; bi < a.n_map; bi += nwk) {
+        const uint32_t b = a.blk_map[bi];
+        // the rows a solver may pivot on: with inline_general the first solver finishes every block, on its
+        // first e + margin rows (general_block XORs any later pivot row itself); else every received row
+        const uint32_t nr = a.inline_general && a.row_margin && !(pol & 16)
+                                ? min(a.rep_cnt[b], a.erased_off[b + 1] - a.erased_off[b] + a.row_margin)
+                                : a.rep_cnt[b];
+        const uint8_t* rv = x.recv + (size_t)a.rep_off[b] * T;
+        uint8_t* rz = const_cast<uint8_t*>(x.r0) + (size_t)b * x.n_union * T;
+        const uint32_t* RU = a.rep_uidx + a.rep_off[b];
+        const bool staged = nr <= cap;
+        __syncthreads();  // the previous block's readers of ru are done
+        if (staged)
+            for (uint32_t i = tid; i < nr; i += NT) ru[i] = RU[i];
+        __syncthreads();
+        const uint32_t n = nr * cpr;
+        uint32_t j = tid / cpr, c = tid - j * cpr;  // piece tid: row j, piece c
+        for (uint32_t i0 = tid; i0 < n; i0 += U * NT) {
+            V4 v[U], u[U];
+            uint32_t off[U];
+#pragma unroll
+            for (uint32_t k = 0; k < U; ++k) {
+                const bool on = i0 + k * NT < n;
+                off[k] = on ? (staged ? ru[j] : RU[j]) * T + 16 * c : 0u;
+                if (on) {
+                    const V4* pv = reinterpret_cast<const V4*>(rv + (size_t)j * T + 16 * c);
+                    v[k] = (pol & 2) ? __builtin_nontemporal_load(pv) : *pv;
+                    u[k] = *reinterpret_cast<const V4*>(rz + off[k]);
+                }
+                c += dr;
+                j += dq;
+                if (c >= cpr) { c -= cpr; ++j; }
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < U; ++k)
+                if (i0 + k * NT < n) {
+                    V4* q = reinterpret_cast<V4*>(rz + off[k]);
+                    if (pol & 8) {
+                        if ((v[k] ^ u[k]).x == 0x5eed5eedu && (v[k] ^ u[k]).y == 0x5eed5eedu) *q = v[k];
+                    } else if (pol & 1) __builtin_nontemporal_store(v[k] ^ u[k], q);
+                    else *q = v[k] ^ u[k];
+                }
+        }
+    }
+}
+#endif
 
 // The shipped solvers are k_solve_pq<1, 4> (e <= 64), k_solve_pq<2, 4> (e <= 128) and k_solve (any e);
 // the variants measured slower live in rq_kernels_exp.hip (experiments builds only).
@@ -266,7 +348,6 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
     __shared__ FC fcol[2][NROWS];
     __shared__ int gpiv;  // general_block's pivot (inline_general)
     static_assert(NROWS * SW * 4 >= 128 + 64 + 4 * 64 + 64 * 128, "general_block's working set for e <= 64 fits the rows");
-    const uint32_t b = a.blk_map[blockIdx.x];
     // g made scalar: the per-step quad choice and its branches are then wave-uniform SALU, not exec-masked
     // VALU (the compiler cannot prove tid >> 6 uniform)
     const uint32_t tid = threadIdx.x, lane = tid & 63, g = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -280,6 +361,15 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
     if (a.status_init)
         for (uint32_t i = blockIdx.x * NT + tid; i < a.n_all; i += gridDim.x * NT)
             if (a.status_init[i] != ST_PENDING) a.status[i] = a.status_init[i];
+#ifdef RQHIP_EXPERIMENTS
+    if constexpr (RPL == 1 && !PF && !RR) {
+        if (a.sx_wgs && blockIdx.x >= gridDim.x - a.sx_wgs) {  // the syndrome workgroups
+            sx_rows<NT, 4>(a, blockIdx.x - (gridDim.x - a.sx_wgs), a.sx_wgs, tid, rows, NROWS * SW);
+            return;
+        }
+    }
+#endif
+    const uint32_t b = a.blk_map[blockIdx.x];
     if (RPL > 1 && a.status[b] != ST_FALLBACK) return;
     const uint32_t e = a.erased_off[b + 1] - a.erased_off[b];
     const uint32_t nr = a.rep_cnt[b];
@@ -744,9 +834,12 @@ static bool solve_in_place() { return false; }
 #endif
 
 int launch_solve(const SolveArgs& a_in, uint32_t n_blocks, bool need_general, bool wide, uint32_t max_lds_e,
-                 void* stream, bool* xbits_done) {
+                 void* stream, bool* xbits_done, bool* sx_done) {
     // the first solver launch copies the host-decided statuses (a_in.status_init); later launches never do
     SolveArgs first = a_in;
+    // the syndrome workgroups (a_in.sx_wgs) ride on the shipped first solver only (sx below)
+    first.sx_wgs = 0;
+    if (sx_done) *sx_done = false;
     // k_solve_pq and k_solve write the apply's stream themselves (xb_on); any other first solver writes X
     // only, and the caller runs k_xbits
     bool stream_ok = solve_in_place() == false;
@@ -791,7 +884,12 @@ int launch_solve(const SolveArgs& a_in, uint32_t n_blocks, bool need_general, bo
         else if (pf) hipLaunchKernelGGL((k_solve_pq<1, 4, true>), dim3(n_blocks), dim3(256), 0, st, first);
         else if (rr) hipLaunchKernelGGL((k_solve_pq<1, 4, false, true>), dim3(n_blocks), dim3(256), 0, st, first);
         else if (solve_in_place()) hipLaunchKernelGGL((k_solve_ip<4>), dim3(n_blocks), dim3(256), 0, st, first);
-        else hipLaunchKernelGGL((k_solve_pq<1, 4>), dim3(n_blocks), dim3(256), 0, st, first);
+        else {
+            SolveArgs sx = first;
+            sx.sx_wgs = a_in.sx_wgs;
+            hipLaunchKernelGGL((k_solve_pq<1, 4>), dim3(n_blocks + sx.sx_wgs), dim3(256), 0, st, sx);
+            if (sx_done) *sx_done = sx.sx_wgs != 0;
+        }
         rx = (int)hipGetLastError();
     }
     if (rx != hipSuccess || !need_general || first.inline_general) return rx;

@@ -44,7 +44,7 @@ EXPORTED = (
     "rq_decoder_create", "rq_decoder_k", "rq_decoder_add", "rq_decoder_decode", "rq_decoder_free",
     "rq_encode_batch", "rq_decode_batch", "rq_decode_batch_async", "rq_encode_batch_host", "rq_decode_batch_host", "rq_device_count", "rq_set_device",
     "rq_debug_colprog_eval", "rq_debug_colprog_emulate", "rq_debug_colprog_assemble", "rq_debug_decode_margin",
-    "rq_debug_apply_mode", "rq_debug_apply_gi_asm", "rq_debug_solve_mode",
+    "rq_debug_apply_mode", "rq_debug_apply_sx", "rq_debug_apply_gi_asm", "rq_debug_solve_mode",
     "rq_decode_blocks_host", "rq_host_alloc", "rq_host_free", "rq_debug_colprog_passes",
     "rq_debug_shard_plan", "rq_debug_virtual_shards", "rq_debug_tuple", "rq_stream_release", "rq_shutdown",
     "rq_launch_timing", "rq_launch_time", "rq_debug_pair_emulate", "rq_debug_dma4_emulate", "rq_debug_decode_plan",
@@ -197,6 +197,7 @@ def _load(path):
                                       ctypes.c_int),
         "rq_debug_decode_margin": ([ctypes.c_uint32], ctypes.c_uint32),
         "rq_debug_apply_mode": ([ctypes.c_uint32], ctypes.c_uint32),
+        "rq_debug_apply_sx": ([ctypes.c_uint32], ctypes.c_uint32),
         "rq_debug_solve_mode": ([ctypes.c_uint32], ctypes.c_uint32),
         "rq_debug_gi_fits": ([ctypes.c_uint32, ctypes.c_uint32], ctypes.c_int),
         "rq_debug_gi_stream": ([ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp, vp, ctypes.c_uint32,
@@ -402,10 +403,11 @@ def assemble(text):
     return n.value
 
 
-def apply_gi_asm(kc=8, g=5, pdg=2, cpl=1, pack=0, assemble=True):
-    """rq_debug_apply_gi_asm: (assembly text, code object size or None) of the register-table apply kernel."""
+def apply_gi_asm(kc=8, g=5, pdg=2, cpl=1, pack=0, assemble=True, sx=0):
+    """rq_debug_apply_gi_asm: (assembly text, code object size or None) of the register-table apply kernel
+    (sx = 1: the shape that reads precomputed syndromes)."""
     n = ctypes.c_size_t(0)
-    cpl |= pack << 8
+    cpl |= pack << 8 | sx << 9
     _check(lib().rq_debug_apply_gi_asm(kc, g, pdg, cpl, None, 0, ctypes.byref(n), None))
     buf = ctypes.create_string_buffer(n.value + 1)
     co = ctypes.c_size_t(0)
@@ -421,6 +423,12 @@ def solve_mode(mode):
 def apply_mode(mode):
     """rq_debug_apply_mode: 1 = register-table apply, 0 = v_perm k_apply; returns the previous mode."""
     return lib().rq_debug_apply_mode(mode)
+
+
+def apply_sx(on):
+    """rq_debug_apply_sx: 1 = syndromes precomputed beside the first solver (the default), 0 = the apply
+    XORs the received and r0 rows itself; returns the previous setting."""
+    return lib().rq_debug_apply_sx(on)
 
 
 def colprog_bound(K, T, esis, src, src_bytes):

@@ -47,6 +47,23 @@ def test_shipped_shape_occupancy():
     assert "rq_apply_gi_k8_g5_p2_c1" in text
 
 
+@pytest.mark.parametrize("shape", [(8, 5, 2, 1), (8, 4, 1, 1), (8, 5, 1, 2), (16, 6, 2, 1)])
+def test_precomputed_syndrome_shapes(shape):
+    """GiShape::SX (syndromes precomputed into the r0 rows beside the first solver): one load per
+    syndrome, from the r0 rows' buffer resource s[52:55] only (never the received rows' s[48:51]), a ring of
+    G values per slot (fewer VGPRs than the two-row shape), the same index-mode guard."""
+    kc, g, pdg, cpl = shape
+    text, code = rqhip.apply_gi_asm(kc, g, pdg, cpl, sx=1)
+    text2, _ = rqhip.apply_gi_asm(kc, g, pdg, cpl)
+    assert code > 0 and f".globl rq_apply_gi_k{kc}_g{g}_p{pdg}_c{cpl}_s\n" in text
+    assert "s[48:51]" not in "\n".join(l for l in text.splitlines() if "buffer_load" in l)
+    loads = lambda t: sum(1 for l in t.splitlines() if "buffer_load_dword" in l and "s[52:55]" in l)
+    assert loads(text) == loads(text2)  # the r0-row loads stay, the received-row ones go
+    assert sum(1 for l in text2.splitlines() if "s[48:51]" in l and "buffer_load" in l) == loads(text2)
+    assert _vgprs(text) == _vgprs(text2) - ((g * pdg * cpl) // 4) * 4 or _vgprs(text) < _vgprs(text2)
+    assert rqhip.lib().rq_debug_apply_gi_check(kc, g, pdg, cpl | 512, text.encode()) == 0
+
+
 def test_bad_shapes_refused():
     for shape in ((6, 5, 2, 1), (8, 7, 2, 1), (8, 5, 3, 1), (8, 5, 2, 3), (16, 6, 2, 2), (4, 4, 1, 1, 1), (12, 5, 2, 1, 1)):
         with pytest.raises(rqhip.RaptorQError):

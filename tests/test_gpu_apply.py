@@ -3,7 +3,11 @@
 The register-table apply (k_xbits + the generated rq_apply_gi kernel, rq_applygi.cpp; the default) and
 k_apply's v_perm byte tables (rq_debug_apply_mode(0)) compute x_E = g_E ^ X s from the same X.  Each case
 decodes one batch with both and compares every block's bytes and status; solved blocks must equal their
-source, unsolved ones keep their bytes.  Cases cover e from 1 to past 128 in one batch (a slice of 16
+source, unsolved ones keep their bytes.  The register-table apply runs twice, with rq_debug_apply_sx 1 and
+0: in the experiments library (tests/test_gpu_experimental_programs.py runs this file against it) the first
+reads syndromes that the first solver launch's extra workgroups precomputed into the r0 rows (when
+T % 16 == 0 and the repair buffer is 16-byte aligned), the second XORs the received and r0 rows itself;
+the two must give the same bytes.  (The release library has only the second.)  Cases cover e from 1 to past 128 in one batch (a slice of 16
 outputs partly used, a last group of 1..5 syndromes), T not a multiple of 256 (a strip with lanes off)
 and T = 8 (two dwords), and a block left unsolved beside solved ones.  (The in-place first solver lives in
 the experiments library: tests/test_gpu_experimental_programs.py.)"""
@@ -40,17 +44,24 @@ def _case(rq, gpu, K, T, R, erase_counts, seed):
 
 
 def _decode_both(rq, K, T, data, erased, reps, rep):
+    """[(bytes, statuses) under k_apply, under the register-table apply]; the register-table apply without
+    the precomputed syndromes is checked against it here."""
     res = []
-    for mode in (0, 1):
+    for mode, sx in ((0, 1), (1, 1), (1, 0)):
         d = data.clone()
-        old = rq.apply_mode(mode)
+        old, old_sx = rq.apply_mode(mode), rq.apply_sx(sx)
         try:
             st = rq.DecodeBatch(K, T, erased, reps).run(d, rep)
             torch.cuda.synchronize()
         finally:
             rq.apply_mode(old)
+            rq.apply_sx(old_sx)
         res.append((d, np.array(st)))
-    return res
+    (d1, st1), (d2, st2) = res[1], res[2]
+    assert np.array_equal(st1, st2)
+    bad = [b for b in range(d1.shape[0]) if not torch.equal(d1[b], d2[b])]
+    assert not bad, ("blocks whose bytes differ with and without precomputed syndromes", bad)
+    return res[:2]
 
 
 @pytest.mark.parametrize("K,T,R,erase_counts", [
@@ -104,3 +115,19 @@ def test_apply_stream_bound_falls_back(gpu, rq):
         assert list(st1) == [1] * len(ec) and list(st0) == list(st1), (ec, st0, st1)
         assert torch.equal(d0, d1), ec
         assert torch.equal(d1, src), ec
+
+
+def test_apply_unaligned_repairs_skip_precomputed_syndromes(gpu, rq):
+    """The precomputed syndromes take 16-byte row pieces: a repair buffer at a 4-byte offset (and T = 1 204,
+    not a multiple of 16) decodes through the apply's own XOR, with the same bytes."""
+    for T, off in ((1200, 4), (1204, 0)):
+        K, R = 256, 40
+        src, data, erased, reps, rep = _case(rq, gpu, K, T, R, [30, 7, 1, 22], 11 + off + T)
+        buf = torch.empty(rep.numel() + 16, dtype=torch.uint8, device=gpu)
+        base = (16 - buf.data_ptr() % 16) % 16 + off
+        rep2 = buf[base:base + rep.numel()].view(rep.shape)
+        rep2.copy_(rep)
+        assert rep2.data_ptr() % 16 == off
+        (d0, st0), (d1, st1) = _decode_both(rq, K, T, data, erased, reps, rep2)
+        assert list(st1) == [1] * 4 and list(st0) == list(st1)
+        assert torch.equal(d1, src) and torch.equal(d0, d1)

@@ -68,3 +68,14 @@ def test_descriptor_fetch_with_four_wave_workgroups():
     out, err = _run(["tools/experiments/fetch_wg_check.py"], {"RQHIP_WG": "4", "RQHIP_FETCH_LOG": "1"}, stderr=True)
     assert out.strip().endswith("ok"), out
     assert re.search(r"\[fetch\] carried=1 W=4 ", err), err[-2000:]
+
+
+def test_precomputed_syndromes_agree():
+    """The precomputed syndromes (experiments library, RQHIP_APPLY_SX=1: the first solver launch's extra
+    workgroups XOR the received rows into the r0 rows, the apply loads one row per syndrome; measured not
+    to pay) give the k_apply bytes on every case of tests/test_gpu_apply.py, and
+    a pivot row past the first e + margin rows (XORed by general_block itself) decodes."""
+    out = _run(["-m", "pytest", "-q", "-m", "gpu", "-p", "no:cacheprovider", "tests/test_gpu_apply.py",
+                "tests/test_gpu_decode_limits.py::test_first_solver_finishes_rank_deficient_rows_inline"],
+               {"RQHIP_APPLY_SX": "1"})
+    assert re.search(r"\b1[0-9] passed", out) and "failed" not in out, out

@@ -38,6 +38,8 @@ def main():
                                 torch.tensor([r for _, r in rows], device=dev)].contiguous()
     eb = torch.tensor([b for b in range(B) for _ in erased[b]], device=dev, dtype=torch.long)
     ei = torch.tensor([i for b in range(B) for i in erased[b]], device=dev, dtype=torch.long)
+    if os.environ.get("RQ_SX"):  # rq_debug_apply_sx: syndromes precomputed beside the first solver or not
+        rq.apply_sx(int(os.environ["RQ_SX"]))
     db = rq.DecodeBatch(K, T, erased, rl)
     d = src.clone()
     d.view(B, K, T)[eb, ei] = 0xA5
