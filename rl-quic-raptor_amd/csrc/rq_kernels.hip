@@ -326,7 +326,11 @@ __device__ __forceinline__ void sx_rows(const SolveArgs& a, uint32_t w, uint32_t
 // row for the whole solve (quads below the step's column are final and skipped, as the shifting
 // assignment skips them) -- and the pivot row's dwords are v_readlane'd from lane p: no row quad
 // goes through LDS per step (RR's rows are written back once, after the last step, for X).
-template <int RPL, int NW, bool PF = false, bool RR = false>
+// SV (shipped, round 6): the pivot row's dwords stay in VGPRs and the v_perm selectors are formed by the
+// VALU (five per dword) instead of by the CU's one scalar unit after a v_readfirstlane: a step's scalar
+// instructions are shared by the CU's sixteen waves, its vector ones by a SIMD's four.  68.0 -> 66.1 us
+// (profiles/r06_solve/sv); SV = false is the experiments library's RQHIP_SOLVE_SV=0.
+template <int RPL, int NW, bool PF = false, bool RR = false, bool SV = true>
 __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
     static_assert(!RR || (RPL == 1 && !PF), "RR: one row per lane, coefficient-byte column buffer");
     constexpr uint32_t NT = 64 * NW;
@@ -565,11 +569,20 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
         for (int j = 0; j < (int)QW; ++j) {
             const uint32_t w = w0 + NW * j;
             if (w >= q1) break;
-            const uint32_t px = __builtin_amdgcn_readfirstlane(P[j].x), py = __builtin_amdgcn_readfirstlane(P[j].y);
-            const uint32_t pz = __builtin_amdgcn_readfirstlane(P[j].z), pw = __builtin_amdgcn_readfirstlane(P[j].w);
-            // a pivot-row quad of zeros leaves every row's quad as it is (the identity part of the pivot
-            // row is zero beyond the rows folded into it so far): a scalar branch skips its updates
-            const bool pzero = (px | py | pz | pw) == 0u;
+            uint32_t px, py, pz, pw;
+            bool pzero;
+            if constexpr (SV) {
+                // the quad as VGPRs the compiler may not move to SGPRs (an empty asm makes them divergent)
+                px = P[j].x; py = P[j].y; pz = P[j].z; pw = P[j].w;
+                asm volatile("" : "+v"(px), "+v"(py), "+v"(pz), "+v"(pw));
+                pzero = __builtin_amdgcn_readfirstlane(px | py | pz | pw) == 0u;
+            } else {
+                px = __builtin_amdgcn_readfirstlane(P[j].x); py = __builtin_amdgcn_readfirstlane(P[j].y);
+                pz = __builtin_amdgcn_readfirstlane(P[j].z); pw = __builtin_amdgcn_readfirstlane(P[j].w);
+                // a pivot-row quad of zeros leaves every row's quad as it is (the identity part of the pivot
+                // row is zero beyond the rows folded into it so far): a scalar branch skips its updates
+                pzero = (px | py | pz | pw) == 0u;
+            }
 #pragma unroll
             for (int q = 0; q < RPL; ++q) {
                 uint4 r = R[q][j];
@@ -600,6 +613,20 @@ __global__ void __launch_bounds__(64 * NW) k_solve_pq(SolveArgs a) {
                 }
             }
         }
+#ifdef RQHIP_EXPERIMENTS
+        // issue-bound probe (bits 32 / 64): 32 dependent SALU / VALU instructions more per step, results
+        // unused (what they cost says which issue unit binds the step)
+        if (a.diag & 32) {
+            uint32_t z = k;
+#pragma unroll
+            for (int t = 0; t < 32; ++t) asm volatile("s_add_u32 %0, %0, 1" : "+s"(z));
+        }
+        if (a.diag & 64) {
+            uint32_t z = lane;
+#pragma unroll
+            for (int t = 0; t < 32; ++t) asm volatile("v_add_u32_e32 %0, 1, %0" : "+v"(z));
+        }
+#endif
         __syncthreads();
     }
     if (ksteps < e) {  // diagnostic step limit (timing only): valid pivot rows, meaningless X
@@ -822,6 +849,10 @@ static bool rr_knob() {
     static const bool r = knob_on("RQHIP_SOLVE_RR", false);
     return r;
 }
+static bool sv_knob() {
+    static const bool r = knob_on("RQHIP_SOLVE_SV", true);
+    return r;
+}
 #endif
 
 // The first solve in place (k_solve_ip, experiments library) or on [M | I] (k_solve_pq<1, 4>);
@@ -884,6 +915,7 @@ int launch_solve(const SolveArgs& a_in, uint32_t n_blocks, bool need_general, bo
         else if (pf) hipLaunchKernelGGL((k_solve_pq<1, 4, true>), dim3(n_blocks), dim3(256), 0, st, first);
         else if (rr) hipLaunchKernelGGL((k_solve_pq<1, 4, false, true>), dim3(n_blocks), dim3(256), 0, st, first);
         else if (solve_in_place()) hipLaunchKernelGGL((k_solve_ip<4>), dim3(n_blocks), dim3(256), 0, st, first);
+        else if (!sv_knob()) hipLaunchKernelGGL((k_solve_pq<1, 4, false, false, false>), dim3(n_blocks), dim3(256), 0, st, first);
         else {
             SolveArgs sx = first;
             sx.sx_wgs = a_in.sx_wgs;

@@ -18,8 +18,8 @@ import rqhip
 
 ROOT = Path(__file__).resolve().parent.parent
 SHIPPED = {
-    "void rq::k_solve_pq<1, 4, false, false>(rq::SolveArgs)",
-    "void rq::k_solve_pq<2, 4, false, false>(rq::SolveArgs)",
+    "void rq::k_solve_pq<1, 4, false, false, true>(rq::SolveArgs)",
+    "void rq::k_solve_pq<2, 4, false, false, true>(rq::SolveArgs)",
     "rq::k_solve(rq::SolveArgs)",
     "rq::k_pack_rows(rq::PackArgs)",
     "rq::k_gather(rq::DevParams, unsigned char const*, unsigned int, unsigned int const*, unsigned int, unsigned char*)",
@@ -62,6 +62,7 @@ def test_experiments_library_keeps_the_variants():
         pytest.skip(str(ex))
     got = kernels(rqhip.EXP_LIB_PATH)
     assert SHIPPED <= got
-    for k in ("k_solve_fast", "k_solve_pm", "k_solve_reg", "k_solve_lean", "k_solve_pq<1, 4, true, false>", "k_solve_pq<1, 4, false, true>", "k_solve_ip<4>",
+    for k in ("k_solve_fast", "k_solve_pm", "k_solve_reg", "k_solve_lean", "k_solve_pq<1, 4, true, false, true>", "k_solve_pq<1, 4, false, true, true>",
+              "k_solve_pq<1, 4, false, false, false>", "k_solve_ip<4>",
               "k_apply<8, 5, 2, 3, true>"):
         assert any(k in n for n in got), k
