@@ -249,6 +249,12 @@ std::string emit_apply_gi_asm(const GiShape& sh) {
             }
         }
         if (!(sh.diag & 4)) a.line("s_set_gpr_idx_off");
+        // issue probe (diag 8 / 16): 32 dependent scalar / vector instructions more per group, results unused
+        // (s97 is free at CPL 1, v0 after the prologue)
+        if ((sh.diag & 8) && CPL == 1)
+            for (int t = 0; t < 32; ++t) a.line("s_add_u32 s97, s97, 1");
+        if (sh.diag & 16)
+            for (int t = 0; t < 32; ++t) a.line("v_add_u32_e32 v0, 1, v0");
         a.line("s_sub_u32 s46, s46, 1");
         a.line("s_cmp_eq_u32 s46, 0");
         a.line("s_cbranch_scc1 .Lepi");
