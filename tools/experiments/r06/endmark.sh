@@ -1,3 +1,4 @@
+# (round 6 record: the RQHIP_END_MARKER knob this script A/Bs was removed after it measured no gain, profiles/r06_gap)
 # The decode call's marker bound to the apply's dispatch: GPU decode tests, then bench.py A/B
 # (experiments library, RQHIP_END_MARKER=1 keeps the separate marker) and a kernel trace of the bench.
 set -o pipefail
