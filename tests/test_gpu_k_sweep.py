@@ -9,7 +9,8 @@ ESIs and one far ESI, and blocks 0 and 2 are compared with the oracle byte for b
 decoded with a few source rows erased and all nine repairs received (a union that is not a dense
 range), and each block's status must equal the oracle decoder's decision on the same symbols
 (recovered bytes equal to the source when it decodes; above K = 600 a block that decodes to its source is
-taken as the oracle's decision without running its dense solve)."""
+taken as the oracle's decision without running its dense solve).  A second sweep runs the same checks over
+symbol sizes from 8 to 4 096 bytes at K = 300."""
 import numpy as np
 import pytest
 import torch
@@ -81,3 +82,44 @@ def test_k_sweep_matches_oracle(gpu, rq, oracle, K):
         assert st[b] == (1 if ok else 0), ("block", b, "status", st[b], "oracle decodes", ok)
         if ok:
             assert torch.equal(data[b], src[b]), ("block", b, "recovered bytes differ from the source")
+
+
+# symbol sizes: one dword, lanes partly off in the last 64-column strip, exact strips, 16-byte multiples and not
+TS = (8, 12, 20, 100, 252, 256, 260, 516, 1020, 1024, 1028, 1200, 1204, 2044, 4096)
+
+
+@pytest.mark.parametrize("T_", TS)
+def test_t_sweep_matches_oracle(gpu, rq, oracle, T_):
+    """The same checks over symbol sizes at K = 300: every strip and lane-mask shape of the column program
+    and the apply, 16-byte row multiples and not."""
+    K, nb = 300, 3
+    rng = np.random.default_rng(T_)
+    esis = list(range(K, K + 8)) + [K + FAR]
+    R = len(esis)
+    src_h = rng.integers(0, 256, (nb, K * T_), dtype=np.uint8)
+    src = torch.from_numpy(src_h).to(gpu)
+    out = torch.empty((nb, R * T_), dtype=torch.uint8, device=gpu)
+    rq.encode_batch(src, K, T_, esis, out)
+    torch.cuda.synchronize()
+    rep_h = out.view(nb, R, T_).cpu().numpy()
+    for b in (0, nb - 1):
+        enc = oracle.OracleEncoder(src_h[b].tobytes(), T_)
+        assert np.array_equal(rep_h[b], np.stack([enc.gen_symbol(e) for e in esis])), ("block", b)
+    erased = [sorted(rng.choice(K, e, replace=False).tolist()) for e in (8, 1, 5)]
+    data = src.clone()
+    for b, er in enumerate(erased):
+        for i in er:
+            data[b, i * T_:(i + 1) * T_] = 0x5A
+    st = np.array(rq.DecodeBatch(K, T_, erased, [list(esis)] * nb).run(data, out.view(nb * R, T_).contiguous()))
+    torch.cuda.synchronize()
+    for b, er in enumerate(erased):
+        dec = oracle.OracleDecoder(K * T_, T_)
+        for i in range(K):
+            if i not in er:
+                dec.add_symbol(i, src_h[b, i * T_:(i + 1) * T_].tobytes())
+        for j, e in enumerate(esis):
+            dec.add_symbol(e, rep_h[b, j].tobytes())
+        ok = dec.decode()[0]
+        assert st[b] == (1 if ok else 0), ("block", b, "status", st[b], "oracle decodes", ok)
+        if ok:
+            assert torch.equal(data[b], src[b]), ("block", b)
