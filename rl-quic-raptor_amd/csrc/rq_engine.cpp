@@ -1626,6 +1626,8 @@ struct DecodeJob {
 };
 
 // decode_begin's host part: offsets, argument checks, host-decided statuses, the blocks to solve.
+void lpt_order(std::vector<uint32_t>& map, const uint32_t* n_erased);
+
 int decode_args(DecodeJob* j, const uint32_t* n_erased, Fin fin) {
     const uint32_t n_blocks = j->n_blocks;
     j->eoff.assign(n_blocks + 1, 0);
@@ -1660,7 +1662,27 @@ int decode_args(DecodeJob* j, const uint32_t* n_erased, Fin fin) {
         j->cnt[b] = fin == Fin::Async ? nr : std::min(nr, e + g_subset_margin);
         j->blk_map.push_back(b);
     }
+    lpt_order(j->blk_map, n_erased);
     return RQ_OK;
+}
+
+// The solve list in decreasing erasure count (stable; a counting sort).  The solvers' and the apply's
+// workgroups are dealt out in list order and a block's work grows with e (e pivot steps; e^2 / 8 apply
+// slices), so the largest blocks start first and the per-CU loads even out (longest-first scheduling).
+// RQHIP_LPT=0 keeps the block order (experiments builds).
+void lpt_order(std::vector<uint32_t>& map, const uint32_t* n_erased) {
+    static const bool off = [] { const char* e = knob("RQHIP_LPT"); return e && e[0] == '0'; }();
+    if (off || map.size() < 2) return;
+    uint32_t emax = 0;
+    for (uint32_t b : map) emax = std::max(emax, n_erased[b]);
+    if (emax >= (1u << 16)) return;
+    static thread_local std::vector<uint32_t> cnt, out;
+    cnt.assign(emax + 2, 0);
+    for (uint32_t b : map) ++cnt[emax - n_erased[b] + 1];  // key emax - e: ascending key = descending e
+    for (uint32_t k = 1; k < cnt.size(); ++k) cnt[k] += cnt[k - 1];
+    out.resize(map.size());
+    for (uint32_t b : map) out[cnt[emax - n_erased[b]]++] = b;
+    map.swap(out);
 }
 
 // The largest candidate ESI of a pass over every block with all their received repairs: the argument
