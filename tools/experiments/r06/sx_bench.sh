@@ -7,8 +7,8 @@ mkdir -p $O
 export RQHIP_LIB=rl-quic-raptor_amd/build_exp/librqhip.so
 for r in 1 2 3; do
 for c in ${SETTINGS:-RQHIP_APPLY_SX=1 RQHIP_APPLY_SX=0}; do
-  t=${c//[=,]/_}
-  ( export ${c//,/ }; timeout -k 10 120 python3 -u bench.py --steps ${STEPS:-100} --warmup 10 > $O/bench_${r}_$t.json 2> $O/bench_${r}_$t.err ) || { tail -5 $O/bench_${r}_$t.err; exit 1; }
+  t=${c//[=,+]/_}
+  ( export ${c//+/ }; timeout -k 10 120 python3 -u bench.py --steps ${STEPS:-100} --warmup 10 > $O/bench_${r}_$t.json 2> $O/bench_${r}_$t.err ) || { tail -5 $O/bench_${r}_$t.err; exit 1; }
   python3 - $O/bench_${r}_$t.json "$r $c" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
