@@ -776,6 +776,132 @@ __global__ void __launch_bounds__(64 * NW) k_solve_ip(SolveArgs a) {
         for (uint32_t k = lane; k < e; k += 64) xc[m * xs + k] = rb[pivl[k] * SW * 4 + m];
     if (tid == 0) a.status[b] = 1;
 }
+
+// Experiments (RQHIP_SOLVE_IPX=1): k_solve_ip with round 6's first-solver changes -- scalar wave index,
+// used rows as a scalar mask, v_perm selectors on the VALU, the apply's index stream written from the
+// rows, and the general algorithm inline for a block rank-deficient on its first rows.  One quad of every
+// row per wave (rows are e bytes wide), against two for k_solve_pq<1, 4>.
+__global__ void __launch_bounds__(256) k_solve_ipx(SolveArgs a) {
+    constexpr uint32_t NW = 4, NT = 64 * NW, NROWS = 64, SW = 20;
+    // rows: 64 x 20 dwords, sized up to general_block's working set for e <= 64 (inline general)
+    __shared__ __attribute__((aligned(16))) uint32_t rows[2176];
+    static_assert(NROWS * SW <= 2176 && 2176 * 4 >= 128 + 64 + 4 * 64 + 64 * 128, "rows and general_block fit");
+    __shared__ __attribute__((aligned(4))) uint8_t ex[512], lg[256];
+    __shared__ uint8_t pivl[NROWS];
+    __shared__ uint32_t Es[NROWS];
+    __shared__ __attribute__((aligned(16))) uint4 tlA[510];
+    __shared__ uint32_t tlB[510];
+    __shared__ uint32_t pinfo[256];
+    __shared__ uint8_t fcol[2][NROWS];
+    __shared__ int gpiv;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, g = __builtin_amdgcn_readfirstlane(tid >> 6);
+    if (a.status_init)
+        for (uint32_t i = blockIdx.x * NT + tid; i < a.n_all; i += gridDim.x * NT)
+            if (a.status_init[i] != ST_PENDING) a.status[i] = a.status_init[i];
+    const uint32_t b = a.blk_map[blockIdx.x];
+    const uint32_t e = a.erased_off[b + 1] - a.erased_off[b];
+    const uint32_t nr = a.rep_cnt[b];
+    if (e > NROWS) {
+        if (tid == 0) a.status[b] = ST_FALLBACK;
+        return;
+    }
+    const uint32_t nrow = a.row_margin ? min(min(nr, NROWS), e + a.row_margin) : min(nr, NROWS);
+    const uint32_t* E = a.erased + a.erased_off[b];
+    const uint32_t* U = a.rep_uidx + a.rep_off[b];
+    for (uint32_t i = tid; i < e; i += NT) Es[i] = E[i];
+    gf_tables_copy(ex, lg);
+    for (uint32_t l = tid; l < 510; l += NT) {
+        const uint32_t lm = l < 255 ? l : l - 255;
+        tlA[l] = make_uint4(kPerm.A[lm][0], kPerm.A[lm][1], kPerm.A[lm][2], kPerm.A[lm][3]);
+        tlB[l] = kPerm.B[lm];
+    }
+    for (uint32_t i = tid; i < NROWS * SW; i += NT) rows[i] = 0;
+    __syncthreads();
+    if (lane < nrow) gather_row<NW>(reinterpret_cast<uint8_t*>(rows + lane * SW), a.mrep + (size_t)U[lane] * a.mrep_stride, Es, e, g);
+    for (uint32_t x = tid; x < 256; x += NT) {
+        uint32_t v = 0;
+        if (x) {
+            const uint32_t lx = lg[x], cp = 1u ^ ex[255u - lx];
+            v = lx | (cp ? (uint32_t)lg[cp] << 8 | 1u << 16 : 0u);
+        }
+        pinfo[x] = v;
+    }
+    __syncthreads();
+    for (uint32_t r = tid; r < NROWS; r += NT) fcol[0][r] = (uint8_t)(rows[r * SW] & 0xFFu);
+    __syncthreads();
+    const uint32_t q1 = (e + 15) >> 4;
+    uint64_t usedm = __ballot(lane >= nrow);
+    uint4* myq = reinterpret_cast<uint4*>(rows + lane * SW) + g;
+    const uint8_t* rb = reinterpret_cast<const uint8_t*>(rows);
+    const bool inl = a.inline_general != 0;
+    for (uint32_t k = 0; k < e; ++k) {
+        const uint4 R = *myq;
+        const uint32_t f = fcol[k & 1][lane];
+        const uint32_t pif = pinfo[f];
+        const uint64_t bal = __ballot(f != 0) & ~usedm;
+        if (!bal) {  // uniform over the block: rank-deficient on these rows
+            if (nr > nrow && inl) {
+                __syncthreads();
+                general_block(a, blockIdx.x, b, reinterpret_cast<uint8_t*>(rows), ex, lg, &gpiv, tid, NT);
+                if (tid == 0 && a.host_status) a.host_status[b] = a.status[b];
+                return;
+            }
+            if (tid == 0) a.status[b] = (nr > nrow) ? ST_FALLBACK : 0;
+            if (tid == 0 && inl && a.host_status) a.host_status[b] = 0;
+            if (a.xb_on && nr <= nrow)
+                gi_stream<8, 5, 2>(a.xb, blockIdx.x, b, e, false, tid, NT, [](uint32_t, uint32_t) { return 0u; },
+                                   [](uint32_t) { return 0u; });
+            return;
+        }
+        const uint32_t p = (uint32_t)__ffsll((unsigned long long)bal) - 1;
+        const bool piv = lane == p;
+        usedm |= 1ull << p;
+        if (tid == 0) pivl[k] = (uint8_t)p;
+        uint4 P = reinterpret_cast<const uint4*>(rows + p * SW)[g];
+        const uint32_t pip = __builtin_amdgcn_readlane(pif, p);
+        const uint32_t ilgp = 255u - (pip & 0xFFu);
+        const bool act = piv ? ((pif >> 16) & 1u) != 0 : f != 0;
+        const uint32_t l = piv ? (pif >> 8) & 0xFFu : (pif & 0xFFu) + ilgp;
+        const uint4 A = tlA[l];
+        const uint32_t B = tlB[l];
+        const uint32_t kn = k + 1;
+        if (g < q1) {
+            asm volatile("" : "+v"(P.x), "+v"(P.y), "+v"(P.z), "+v"(P.w));
+            uint4 r = R;
+            r.x ^= perm_mul(A, B, P.x);
+            r.y ^= perm_mul(A, B, P.y);
+            r.z ^= perm_mul(A, B, P.z);
+            r.w ^= perm_mul(A, B, P.w);
+            if (g == (k >> 4)) {  // byte k: c_j, or 1 / f_p on the pivot row
+                const uint32_t cb = ((A.x >> 8) & 0xFFu) ^ (piv ? 1u : 0u), sh = (k & 3u) * 8, d = (k >> 2) & 3u;
+                uint32_t& dw = d == 0 ? r.x : d == 1 ? r.y : d == 2 ? r.z : r.w;
+                dw = (dw & ~(0xFFu << sh)) | (cb << sh);
+            }
+            if (act) *myq = r;
+            if (kn < e && g == (kn >> 4)) {
+                const uint4 v = act ? r : R;
+                const uint32_t d = (kn >> 2) & 3u;
+                const uint32_t dw = d == 0 ? v.x : d == 1 ? v.y : d == 2 ? v.z : v.w;
+                fcol[kn & 1][lane] = (uint8_t)((dw >> ((kn & 3u) * 8)) & 0xFFu);
+            }
+        }
+        __syncthreads();
+    }
+    uint16_t* XP = a.xpiv + a.erased_off[b];
+    for (uint32_t m = tid; m < e; m += NT) XP[m] = pivl[m];
+    if (a.xb_on) {
+        gi_stream<8, 5, 2>(a.xb, blockIdx.x, b, e, true, tid, NT,
+                           [&](uint32_t k, uint32_t m) { return (uint32_t)rb[pivl[k] * SW * 4 + m]; },
+                           [&](uint32_t m) { return (uint32_t)pivl[m]; });
+    } else {
+        uint8_t* xc = a.xcoef + 64ull * a.xoff[blockIdx.x];
+        const uint32_t xs = x_stride(e);
+        for (uint32_t m = g; m < e; m += NW)
+            for (uint32_t k = lane; k < e; k += 64) xc[m * xs + k] = rb[pivl[k] * SW * 4 + m];
+    }
+    if (tid == 0) a.status[b] = 1;
+    if (tid == 0 && inl && a.host_status) a.host_status[b] = 1;
+}
 #endif
 
 // General solver for the blocks the fast solvers deferred: any e, every received repair.  The
@@ -849,6 +975,10 @@ static bool rr_knob() {
     static const bool r = knob_on("RQHIP_SOLVE_RR", false);
     return r;
 }
+static bool ipx_knob() {
+    static const bool r = knob_on("RQHIP_SOLVE_IPX", false);
+    return r;
+}
 static bool sv_knob() {
     static const bool r = knob_on("RQHIP_SOLVE_SV", true);
     return r;
@@ -916,6 +1046,7 @@ int launch_solve(const SolveArgs& a_in, uint32_t n_blocks, bool need_general, bo
         else if (rr) hipLaunchKernelGGL((k_solve_pq<1, 4, false, true>), dim3(n_blocks), dim3(256), 0, st, first);
         else if (solve_in_place()) hipLaunchKernelGGL((k_solve_ip<4>), dim3(n_blocks), dim3(256), 0, st, first);
         else if (!sv_knob()) hipLaunchKernelGGL((k_solve_pq<1, 4, false, false, false>), dim3(n_blocks), dim3(256), 0, st, first);
+        else if (ipx_knob()) hipLaunchKernelGGL(k_solve_ipx, dim3(n_blocks), dim3(256), 0, st, first);
         else {
             SolveArgs sx = first;
             sx.sx_wgs = a_in.sx_wgs;

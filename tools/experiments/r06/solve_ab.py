@@ -38,6 +38,8 @@ def main():
                                 torch.tensor([r for _, r in rows], device=dev)].contiguous()
     eb = torch.tensor([b for b in range(B) for _ in erased[b]], device=dev, dtype=torch.long)
     ei = torch.tensor([i for b in range(B) for i in erased[b]], device=dev, dtype=torch.long)
+    if os.environ.get("RQ_SOLVE_IP"):  # rq_debug_solve_mode: 1 = the in-place first solver (experiments library)
+        rq.solve_mode(int(os.environ["RQ_SOLVE_IP"]))
     if os.environ.get("RQ_SX"):  # rq_debug_apply_sx: syndromes precomputed beside the first solver or not
         rq.apply_sx(int(os.environ["RQ_SX"]))
     db = rq.DecodeBatch(K, T, erased, rl)
